@@ -1,0 +1,305 @@
+"""MI355X-native IVF-Flat search engine — Python host mirror of the reference API.
+
+The product is ``lib/libvdb_ivf.so`` (hand-written gfx950 HIP kernels behind the C ABI
+in ``include/vdb_ivf.h``). This module binds that ABI with ctypes and mirrors the
+reference's ``vdb::IVFFlatIndex`` surface (``engine/ivf_flat_index.h:14-67``):
+``Config``, ``SearchParams``, ``train``, ``add``, ``search``, ``warmup_lists``,
+``evict_list``, ``get_gpu_memory_usage``, ``get_total_vectors``, plus the
+device-resident and list-sharded forms used by ``bench.py``.
+
+There is no CPU fallback: if the library is missing or no GPU is present, calls
+raise. Import under any name, e.g. ``importlib`` with the directory path
+(the directory name is not a Python identifier); ``load()`` below does that.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libvdb_ivf.so")
+CPP_LIB_PATH = os.path.join(_HERE, "lib", "libvdb_ivf_cpp.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "vdb_ivf.h")
+
+_lib = None
+
+
+class Metric(enum.IntEnum):
+    """kernels::Metric (engine/kernels.cuh:24-28)."""
+    L2 = 0
+    InnerProduct = 1
+    Cosine = 2
+
+
+class VdbError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"vdb error {code}: {msg}")
+        self.code = code
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("dimension", ctypes.c_uint32), ("nlist", ctypes.c_uint32), ("metric", ctypes.c_int32),
+                ("use_gpu", ctypes.c_int32), ("max_gpu_memory", ctypes.c_uint64), ("device", ctypes.c_int32)]
+
+
+class Profile(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("scan_launches", ctypes.c_uint64), ("scan_ms", ctypes.c_double),
+                ("coarse_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("scan_vectors", ctypes.c_uint64),
+                ("distinct_lists", ctypes.c_uint64), ("work_items", ctypes.c_uint64),
+                ("scan_bytes", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+def build(jobs: int = 8) -> str:
+    """Compile the HIP library for gfx950 (hipcc; cross-compiles without a GPU)."""
+    subprocess.check_call(["make", "-s", f"-j{jobs}", "-C", _HERE])
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C {_HERE}` (no CPU fallback exists)")
+    # torch ships its own libamdhip64 (SONAME libamdhip64.so.7). Loading torch first
+    # lets libvdb_ivf.so bind to that same HIP runtime by SONAME, so torch tensors and
+    # streams and this library share one runtime; the other order loads two.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+    sigs = {
+        "vdb_last_error": (ctypes.c_char_p, []),
+        "vdb_version": (ctypes.c_char_p, []),
+        "vdb_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+        "vdb_ivf_create": (ctypes.c_int, [ctypes.POINTER(_Config), ctypes.POINTER(vp)]),
+        "vdb_ivf_destroy": (ctypes.c_int, [vp]),
+        "vdb_ivf_train": (ctypes.c_int, [vp, vp, u64]),
+        "vdb_ivf_train_device": (ctypes.c_int, [vp, vp, u64]),
+        "vdb_ivf_set_centroids": (ctypes.c_int, [vp, vp]),
+        "vdb_ivf_get_centroids": (ctypes.c_int, [vp, vp]),
+        "vdb_ivf_add": (ctypes.c_int, [vp, vp, vp, u64]),
+        "vdb_ivf_add_device": (ctypes.c_int, [vp, vp, vp, u64]),
+        "vdb_ivf_search": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp]),
+        "vdb_ivf_search_device": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp, vp]),
+        "vdb_ivf_set_shard": (ctypes.c_int, [vp, u32, u32]),
+        "vdb_merge_ranks_device": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp, vp]),
+        "vdb_shard_plan": (ctypes.c_int, [vp, u32, u32, vp]),
+        "vdb_ivf_warmup": (ctypes.c_int, [vp, vp, u32]),
+        "vdb_ivf_evict": (ctypes.c_int, [vp, u32]),
+        "vdb_ivf_gpu_bytes": (u64, [vp]),
+        "vdb_ivf_ntotal": (u64, [vp]),
+        "vdb_ivf_list_sizes": (ctypes.c_int, [vp, vp]),
+        "vdb_ivf_get_list": (ctypes.c_int, [vp, u32, vp, vp]),
+        "vdb_ivf_set_batch": (ctypes.c_int, [vp, u32]),
+        "vdb_ivf_set_stale_slots": (ctypes.c_int, [vp, i32]),
+        "vdb_ivf_profile_enable": (ctypes.c_int, [vp, i32]),
+        "vdb_ivf_profile_reset": (ctypes.c_int, [vp]),
+        "vdb_ivf_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(Profile)]),
+        "vdb_ivf_synchronize": (ctypes.c_int, [vp]),
+        "vdb_ivf_stream": (vp, [vp]),
+        "vdb_gen_normal_device": (ctypes.c_int, [vp, u64, u64, u64, vp]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise VdbError(rc, lib().vdb_last_error().decode())
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def device_count() -> int:
+    c = ctypes.c_int(0)
+    _check(lib().vdb_device_count(ctypes.byref(c)))
+    return c.value
+
+
+def shard_plan(list_sizes, world: int) -> np.ndarray:
+    """LPT owner rank of every list (host-only, identical on every rank)."""
+    s = np.ascontiguousarray(list_sizes, dtype=np.uint64)
+    out = np.empty(len(s), dtype=np.uint32)
+    _check(lib().vdb_shard_plan(_ptr(s), len(s), world, _ptr(out)))
+    return out
+
+
+def gen_normal_device(ptr: int, n: int, seed: int, offset: int = 0, stream: int | None = None):
+    """Fill n fp32 at device address ``ptr`` with deterministic N(0,1) draws."""
+    _check(lib().vdb_gen_normal_device(ctypes.c_void_p(ptr), n, seed, offset, ctypes.c_void_p(stream or 0)))
+
+
+def merge_ranks_device(dist_ptr: int, ids_ptr: int, nranks: int, n: int, k: int, out_dist_ptr: int,
+                       out_ids_ptr: int, stream: int | None = None):
+    _check(lib().vdb_merge_ranks_device(ctypes.c_void_p(dist_ptr), ctypes.c_void_p(ids_ptr), nranks, n, k,
+                                        ctypes.c_void_p(out_dist_ptr), ctypes.c_void_p(out_ids_ptr),
+                                        ctypes.c_void_p(stream or 0)))
+
+
+class IVFFlatIndex:
+    """vdb::IVFFlatIndex (engine/ivf_flat_index.h:14-67) on one MI355X."""
+
+    @dataclass
+    class Config:
+        dimension: int
+        nlist: int
+        metric: Metric = Metric.L2
+        use_gpu: bool = True
+        max_gpu_memory: int = 8 << 30
+        device: int = 0
+
+    @dataclass
+    class SearchParams:
+        nprobe: int = 10
+        k: int = 10
+        use_exact_rerank: bool = False  # accepted, unused — as in the reference
+
+    def __init__(self, config: "IVFFlatIndex.Config"):
+        self.config = config
+        if config.dimension <= 0 or config.nlist <= 0:
+            raise ValueError("Invalid configuration: dimension and nlist must be > 0")
+        c = _Config(config.dimension, config.nlist, int(config.metric), int(config.use_gpu),
+                    config.max_gpu_memory, config.device)
+        h = ctypes.c_void_p()
+        _check(lib().vdb_ivf_create(ctypes.byref(c), ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vdb_ivf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def dimension(self) -> int:
+        return self.config.dimension
+
+    # ---- build ----
+    def train(self, vectors: np.ndarray):
+        v = np.ascontiguousarray(vectors, dtype=np.float32).reshape(-1, self.dimension)
+        _check(lib().vdb_ivf_train(self._h, _ptr(v), v.shape[0]))
+
+    def train_device(self, ptr: int, n: int):
+        _check(lib().vdb_ivf_train_device(self._h, ctypes.c_void_p(ptr), n))
+
+    def add(self, vectors: np.ndarray, ids: np.ndarray):
+        v = np.ascontiguousarray(vectors, dtype=np.float32).reshape(-1, self.dimension)
+        i = np.ascontiguousarray(ids, dtype=np.uint64)
+        if i.shape[0] != v.shape[0]:
+            raise ValueError("vectors and ids differ in length")
+        _check(lib().vdb_ivf_add(self._h, _ptr(v), _ptr(i), v.shape[0]))
+
+    def add_device(self, vec_ptr: int, ids_ptr: int, n: int):
+        _check(lib().vdb_ivf_add_device(self._h, ctypes.c_void_p(vec_ptr), ctypes.c_void_p(ids_ptr), n))
+
+    @property
+    def centroids(self) -> np.ndarray:
+        out = np.empty((self.config.nlist, self.dimension), dtype=np.float32)
+        _check(lib().vdb_ivf_get_centroids(self._h, _ptr(out)))
+        return out
+
+    @centroids.setter
+    def centroids(self, c: np.ndarray):
+        c = np.ascontiguousarray(c, dtype=np.float32).reshape(self.config.nlist, self.dimension)
+        _check(lib().vdb_ivf_set_centroids(self._h, _ptr(c)))
+
+    # ---- search ----
+    def search(self, queries: np.ndarray, params: "IVFFlatIndex.SearchParams | None" = None, *,
+               nprobe: int | None = None, k: int | None = None):
+        p = params or IVFFlatIndex.SearchParams()
+        nprobe = p.nprobe if nprobe is None else nprobe
+        k = p.k if k is None else k
+        q = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, self.dimension)
+        n = q.shape[0]
+        D = np.empty((n, k), dtype=np.float32)
+        I = np.empty((n, k), dtype=np.uint64)
+        _check(lib().vdb_ivf_search(self._h, _ptr(q), n, nprobe, k, _ptr(D), _ptr(I)))
+        return D, I
+
+    def search_device(self, q_ptr: int, n: int, nprobe: int, k: int, d_ptr: int, i_ptr: int,
+                      stream: int | None = None):
+        _check(lib().vdb_ivf_search_device(self._h, ctypes.c_void_p(q_ptr), n, nprobe, k, ctypes.c_void_p(d_ptr),
+                                           ctypes.c_void_p(i_ptr), ctypes.c_void_p(stream or 0)))
+
+    def search_batch(self, queries, params, distances, indices):
+        """search_batch (ivf_flat_index.h:55-58; declared, never defined in the reference)."""
+        for q, p, d, i in zip(queries, params, distances, indices):
+            D, I = self.search(q, p)
+            d[...] = D.reshape(d.shape)
+            i[...] = I.reshape(i.shape)
+
+    # ---- sharding ----
+    def set_shard(self, rank: int, world: int):
+        _check(lib().vdb_ivf_set_shard(self._h, rank, world))
+
+    # ---- residency / stats ----
+    def warmup_lists(self, list_ids):
+        a = np.ascontiguousarray(list_ids, dtype=np.uint32)
+        _check(lib().vdb_ivf_warmup(self._h, _ptr(a), len(a)))
+
+    def evict_list(self, list_id: int):
+        _check(lib().vdb_ivf_evict(self._h, list_id))
+
+    def get_gpu_memory_usage(self) -> int:
+        return int(lib().vdb_ivf_gpu_bytes(self._h))
+
+    def get_total_vectors(self) -> int:
+        return int(lib().vdb_ivf_ntotal(self._h))
+
+    def list_sizes(self) -> np.ndarray:
+        out = np.empty(self.config.nlist, dtype=np.uint64)
+        _check(lib().vdb_ivf_list_sizes(self._h, _ptr(out)))
+        return out
+
+    def get_list(self, list_id: int):
+        n = int(self.list_sizes()[list_id])
+        v = np.empty((n, self.dimension), dtype=np.float32)
+        i = np.empty(n, dtype=np.uint64)
+        _check(lib().vdb_ivf_get_list(self._h, list_id, _ptr(v), _ptr(i)))
+        return v, i
+
+    def set_batch(self, batch: int):
+        _check(lib().vdb_ivf_set_batch(self._h, batch))
+
+    def set_stale_slots(self, enable: bool):
+        _check(lib().vdb_ivf_set_stale_slots(self._h, int(enable)))
+
+    def profile_enable(self, on: bool = True):
+        _check(lib().vdb_ivf_profile_enable(self._h, int(on)))
+
+    def profile_reset(self):
+        _check(lib().vdb_ivf_profile_reset(self._h))
+
+    def profile_read(self) -> dict:
+        p = Profile()
+        _check(lib().vdb_ivf_profile_read(self._h, ctypes.byref(p)))
+        return p.as_dict()
+
+    def synchronize(self):
+        _check(lib().vdb_ivf_synchronize(self._h))
+
+    @property
+    def stream(self) -> int:
+        return int(lib().vdb_ivf_stream(self._h) or 0)

@@ -1,0 +1,777 @@
+// engine.cpp — host side of the MI355X IVF-Flat engine: the C ABI of
+// include/vdb_ivf.h over the kernels of kernels.hip.
+//
+// One handle = one index on one device. The whole index is HBM-resident in an
+// interleaved list arena (kernels.hpp); a search is a short sequence of kernels
+// per batch of queries, all enqueued on one stream with no host synchronisation:
+//   pad queries -> coarse distances -> probe selection -> probe inversion (plan)
+//   -> ivf_scan -> per-(query, probe) top-k -> per-query merge -> slot carry.
+// Build-side calls (train/add/set_shard) synchronise where the reference
+// algorithm needs a host decision (k-means++ draws from std::mt19937 on the host,
+// exactly as ivf_flat_index.cpp:53-92 does).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <queue>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/vdb_ivf.h"
+#include "kernels.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct VdbError : std::runtime_error {
+    int code;
+    VdbError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void check(hipError_t e, const char* what) {
+    if (e != hipSuccess) {
+        int code = (e == hipErrorOutOfMemory) ? VDB_ERR_OUT_OF_MEMORY : VDB_ERR_DEVICE;
+        (void)hipGetLastError();
+        throw VdbError(code, std::string(what) + ": " + hipGetErrorString(e));
+    }
+}
+#define HIPCHECK(x) check((x), #x)
+
+void require(bool ok, const std::string& msg, int code = VDB_ERR_INVALID_ARGUMENT) {
+    if (!ok) throw VdbError(code, msg);
+}
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return VDB_OK;
+    } catch (const VdbError& e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "host allocation failed";
+        return VDB_ERR_OUT_OF_MEMORY;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return VDB_ERR_DEVICE;
+    }
+}
+
+// Growable device buffer (capacity in elements).
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    T* ensure(size_t n) {
+        if (n <= cap && p) return p;
+        release();
+        size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        HIPCHECK(hipMalloc(&p, bytes));
+        cap = std::max<size_t>(n, 1);
+        return p;
+    }
+    void swap(DevBuf& o) {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
+    }
+};
+
+inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+struct EventSet {
+    hipEvent_t begin, coarse_end, scan_begin, scan_end, end;
+};
+
+}  // namespace
+
+struct vdb_ivf {
+    uint32_t dim = 0, nlist = 0, dp = 0, d4 = 0;
+    int metric = 0;
+    int device = 0;
+    uint64_t max_gpu_memory = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+
+    DevBuf<float> cent_rm;   // [nlist][dp], zero pads
+    DevBuf<float4> cent_il;  // [ceil(nlist/64)][d4][64]
+
+    std::vector<uint64_t> count;      // per list, global (emptiness semantics)
+    std::vector<uint8_t> owned;       // lists this handle scans
+    std::vector<uint64_t> block_off;  // arena block offset per owned list
+    uint64_t arena_blocks = 0;
+    DevBuf<float4> arena;
+    DevBuf<uint64_t> arena_ids;
+    DevBuf<uint64_t> d_block_off;
+    DevBuf<uint32_t> d_count_local, d_count_global, d_nseg;
+    std::vector<uint64_t> nseg_prefix;  // sum of the j largest local segment counts
+    uint64_t total = 0;
+    uint32_t rank = 0, world = 1;
+    uint32_t batch = 256;
+    int stale = 1;
+
+    // search workspace
+    DevBuf<float> qpad, cd, part_d, slot_d, carry_d, out_d, qin;
+    DevBuf<uint64_t> part_i, slot_i, carry_i, out_i;
+    DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters;
+    DevBuf<vdbk::ScanItem> items;
+    DevBuf<unsigned long long> stats;
+
+    bool prof = false;
+    std::vector<EventSet> events;
+    size_t events_used = 0;
+
+    ~vdb_ivf() {
+        for (auto& e : events) {
+            (void)hipEventDestroy(e.begin);
+            (void)hipEventDestroy(e.coarse_end);
+            (void)hipEventDestroy(e.scan_begin);
+            (void)hipEventDestroy(e.scan_end);
+            (void)hipEventDestroy(e.end);
+        }
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    void set_device() { HIPCHECK(hipSetDevice(device)); }
+
+    // Upload the list directory and recompute the segment-count prefix.
+    void upload_directory() {
+        std::vector<uint32_t> cl(nlist), cg(nlist), ns(nlist);
+        for (uint32_t l = 0; l < nlist; ++l) {
+            require(count[l] < (1ull << 32), "list longer than 2^32 vectors", VDB_ERR_UNSUPPORTED);
+            cg[l] = (uint32_t)count[l];
+            cl[l] = owned[l] ? (uint32_t)count[l] : 0u;
+            ns[l] = (uint32_t)cdiv(cl[l], vdbk::kSegVectors);
+        }
+        HIPCHECK(hipMemcpyAsync(d_block_off.ensure(nlist), block_off.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemcpyAsync(d_count_local.ensure(nlist), cl.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemcpyAsync(d_count_global.ensure(nlist), cg.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemcpyAsync(d_nseg.ensure(nlist), ns.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+        std::vector<uint32_t> sorted(ns);
+        std::sort(sorted.begin(), sorted.end(), std::greater<uint32_t>());
+        nseg_prefix.assign(nlist + 1, 0);
+        for (uint32_t j = 0; j < nlist; ++j) nseg_prefix[j + 1] = nseg_prefix[j] + sorted[j];
+        HIPCHECK(hipStreamSynchronize(stream));  // host vectors above are stack-owned
+    }
+
+    // Rebuild the arena so list l holds `keep[l]` of its current blocks at new
+    // offsets sized for `new_count[l]` vectors (0 for lists this handle drops).
+    void relayout(const std::vector<uint64_t>& new_count, const std::vector<uint8_t>& new_owned) {
+        std::vector<uint64_t> new_off(nlist, 0), old_off(nlist, 0);
+        std::vector<uint32_t> nblocks(nlist, 0);
+        uint64_t blocks = 0;
+        for (uint32_t l = 0; l < nlist; ++l) {
+            new_off[l] = blocks;
+            if (new_owned[l]) blocks += cdiv(new_count[l], 64);
+            if (owned[l] && new_owned[l] && count[l] > 0) {
+                nblocks[l] = (uint32_t)cdiv(count[l], 64);
+                old_off[l] = block_off[l];
+            }
+        }
+        DevBuf<float4> na;
+        DevBuf<uint64_t> ni;
+        const size_t vec4 = (size_t)blocks * d4 * 64;
+        na.ensure(vec4);
+        ni.ensure((size_t)blocks * 64);
+        if (blocks) {
+            HIPCHECK(hipMemsetAsync(na.p, 0, vec4 * sizeof(float4), stream));
+            HIPCHECK(hipMemsetAsync(ni.p, 0xFF, (size_t)blocks * 64 * 8, stream));
+        }
+        if (arena_blocks && blocks) {
+            DevBuf<uint64_t> doo, dno;
+            DevBuf<uint32_t> dnb;
+            HIPCHECK(hipMemcpyAsync(doo.ensure(nlist), old_off.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+            HIPCHECK(hipMemcpyAsync(dno.ensure(nlist), new_off.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+            HIPCHECK(hipMemcpyAsync(dnb.ensure(nlist), nblocks.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+            vdbk::launch_copy_lists(arena.p, arena_ids.p, doo.p, dno.p, dnb.p, nlist, d4, na.p, ni.p, stream);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipStreamSynchronize(stream));
+        }
+        HIPCHECK(hipStreamSynchronize(stream));
+        arena.swap(na);
+        arena_ids.swap(ni);
+        arena_blocks = blocks;
+        block_off = new_off;
+        owned = new_owned;
+    }
+
+    // Row-major [n][dim] device input -> zero-padded [n][dp] (or the input itself).
+    const float* padded_rows(const float* d_v, uint64_t n, DevBuf<float>& tmp) {
+        if (dp == dim) return d_v;
+        vdbk::launch_pad_rows(d_v, n, dim, dp, tmp.ensure(n * dp), stream);
+        HIPCHECK(hipGetLastError());
+        return tmp.p;
+    }
+
+    void refresh_centroid_layout() {
+        vdbk::launch_interleave(cent_rm.p, nlist, dp, cent_il.p, stream);
+        HIPCHECK(hipGetLastError());
+    }
+
+    void assign(const float* vpad, uint64_t n, uint32_t* out) {
+        vdbk::launch_assign(metric, vpad, n, dp, cent_il.p, nlist, out, stream);
+        HIPCHECK(hipGetLastError());
+    }
+
+    // Stable grouping of row indices by key (input order kept within a key).
+    void group_by_key(const uint32_t* keys, uint64_t n, DevBuf<uint32_t>& sorted_keys, DevBuf<uint32_t>& order) {
+        require(n < (1ull << 31), "batch larger than 2^31 vectors", VDB_ERR_UNSUPPORTED);
+        DevBuf<uint32_t> iota;
+        vdbk::launch_iota(iota.ensure(n), n, stream);
+        int bits = 1;
+        while ((1ull << bits) < nlist) ++bits;
+        size_t tb = 0;
+        HIPCHECK(vdbk::radix_sort_pairs(nullptr, tb, keys, sorted_keys.ensure(n), iota.p, order.ensure(n), n, bits, stream));
+        DevBuf<unsigned char> temp;
+        temp.ensure(tb);
+        HIPCHECK(vdbk::radix_sort_pairs(temp.p, tb, keys, sorted_keys.p, iota.p, order.p, n, bits, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+    }
+
+    std::vector<uint32_t> key_counts(const uint32_t* keys, uint64_t n, DevBuf<uint32_t>& d_counts) {
+        HIPCHECK(hipMemsetAsync(d_counts.ensure(nlist), 0, nlist * 4, stream));
+        vdbk::launch_histogram(keys, n, d_counts.p, stream);
+        HIPCHECK(hipGetLastError());
+        std::vector<uint32_t> h(nlist);
+        HIPCHECK(hipMemcpyAsync(h.data(), d_counts.p, nlist * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        return h;
+    }
+
+    // ---- train: ivf_flat_index.cpp:49-145 ----
+    void train(const float* d_v, uint64_t n) {
+        require(n > 0, "train needs at least one vector");
+        DevBuf<float> tmp, mind, prefix, total;
+        const float* vpad = padded_rows(d_v, n, tmp);
+        DevBuf<float4> v_il;
+        vdbk::launch_interleave(vpad, n, dp, v_il.ensure(cdiv(n, 64) * d4 * 64), stream);
+        HIPCHECK(hipGetLastError());
+
+        std::mt19937 gen(42);
+        std::uniform_int_distribution<uint64_t> pick(0, n - 1);
+        const uint64_t first = pick(gen);
+        HIPCHECK(hipMemcpyAsync(cent_rm.p, vpad + first * dp, dp * 4, hipMemcpyDeviceToDevice, stream));
+
+        vdbk::launch_mindist_init(mind.ensure(n), n, stream);
+        prefix.ensure(n);
+        total.ensure(1);
+        DevBuf<unsigned long long> pick_idx;
+        pick_idx.ensure(1);
+        for (uint32_t c = 1; c < nlist; ++c) {
+            vdbk::launch_mindist_update(v_il.p, n, d4, cent_rm.p + (size_t)(c - 1) * dp, mind.p, stream);
+            vdbk::launch_serial_prefix(mind.p, n, prefix.p, total.p, stream);
+            HIPCHECK(hipGetLastError());
+            float tot = 0.0f;
+            HIPCHECK(hipMemcpyAsync(&tot, total.p, 4, hipMemcpyDeviceToHost, stream));
+            HIPCHECK(hipStreamSynchronize(stream));
+            std::uniform_real_distribution<float> prob(0.0f, tot);
+            const float target = prob(gen);
+            HIPCHECK(hipMemsetAsync(pick_idx.p, 0xFF, 8, stream));
+            vdbk::launch_first_geq(prefix.p, n, target, pick_idx.p, stream);
+            vdbk::launch_copy_row_if(vpad, n, dp, pick_idx.p, cent_rm.p + (size_t)c * dp, stream);
+            HIPCHECK(hipGetLastError());
+        }
+
+        DevBuf<uint32_t> asg, skeys, order, counts, offsets;
+        asg.ensure(n);
+        for (int it = 0; it < 10; ++it) {
+            refresh_centroid_layout();
+            assign(vpad, n, asg.p);
+            group_by_key(asg.p, n, skeys, order);
+            std::vector<uint32_t> h = key_counts(asg.p, n, counts);
+            std::vector<uint32_t> off(nlist, 0);
+            for (uint32_t l = 1; l < nlist; ++l) off[l] = off[l - 1] + h[l - 1];
+            HIPCHECK(hipMemcpyAsync(offsets.ensure(nlist), off.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+            vdbk::launch_centroid_update(vpad, dp, order.p, offsets.p, counts.p, nlist, dim, cent_rm.p, stream);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipStreamSynchronize(stream));
+        }
+        refresh_centroid_layout();
+        HIPCHECK(hipStreamSynchronize(stream));
+    }
+
+    // ---- add: ivf_flat_index.cpp:148-202 ----
+    void add(const float* d_v, const uint64_t* d_ids, uint64_t n) {
+        if (n == 0) return;
+        DevBuf<float> tmp;
+        const float* vpad = padded_rows(d_v, n, tmp);
+        DevBuf<uint32_t> asg, skeys, order, counts;
+        assign(vpad, n, asg.ensure(n));
+        group_by_key(asg.p, n, skeys, order);
+        std::vector<uint32_t> added = key_counts(asg.p, n, counts);
+
+        std::vector<uint64_t> new_count(count);
+        for (uint32_t l = 0; l < nlist; ++l) new_count[l] += added[l];
+        const std::vector<uint64_t> old_count = count;
+        relayout(new_count, owned);
+
+        std::vector<uint64_t> group_start(nlist, 0), base(nlist, ~0ull);
+        for (uint32_t l = 1; l < nlist; ++l) group_start[l] = group_start[l - 1] + added[l - 1];
+        for (uint32_t l = 0; l < nlist; ++l)
+            if (owned[l]) base[l] = block_off[l] * 64 + old_count[l];
+        DevBuf<uint64_t> d_gs, d_base, dest;
+        HIPCHECK(hipMemcpyAsync(d_gs.ensure(nlist), group_start.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemcpyAsync(d_base.ensure(nlist), base.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+        vdbk::launch_slots_from_order(skeys.p, n, d_gs.p, d_base.p, dest.ensure(n), stream);
+        vdbk::launch_scatter_rows(vpad, d_ids, order.p, n, dp, dest.p, arena.p, arena_ids.p, stream);
+        HIPCHECK(hipGetLastError());
+        count = new_count;
+        total += n;
+        upload_directory();
+    }
+
+    void set_shard(uint32_t r, uint32_t w) {
+        std::vector<uint32_t> owner(nlist);
+        vdb_shard_plan(count.data(), nlist, w, owner.data());
+        std::vector<uint8_t> new_owned(nlist);
+        for (uint32_t l = 0; l < nlist; ++l) new_owned[l] = owner[l] == r;
+        // Lists this handle no longer scans must have been stored here before.
+        for (uint32_t l = 0; l < nlist; ++l)
+            require(!new_owned[l] || owned[l] || count[l] == 0, "shard needs a list this handle dropped", VDB_ERR_STATE);
+        relayout(count, new_owned);
+        rank = r;
+        world = w;
+        upload_directory();
+    }
+
+    EventSet& next_events() {
+        if (events_used == events.size()) {
+            EventSet e;
+            HIPCHECK(hipEventCreate(&e.begin));
+            HIPCHECK(hipEventCreate(&e.coarse_end));
+            HIPCHECK(hipEventCreate(&e.scan_begin));
+            HIPCHECK(hipEventCreate(&e.scan_end));
+            HIPCHECK(hipEventCreate(&e.end));
+            events.push_back(e);
+        }
+        return events[events_used++];
+    }
+
+    // Size every per-batch buffer for B queries up front; growing a buffer frees
+    // the old one, so wait for earlier searches that may still read it.
+    void ensure_workspace(uint32_t B, uint32_t P, uint32_t k, hipStream_t s) {
+        const size_t BP = (size_t)B * P;
+        const size_t max_items = (size_t)B * nseg_prefix[P];
+        const bool grow = qpad.cap < (size_t)B * dp || cd.cap < (size_t)B * nlist || probes.cap < BP ||
+                          items.cap < max_items || part_d.cap < max_items * k || slot_d.cap < BP * k ||
+                          carry_d.cap < (size_t)P * k;
+        if (!grow) return;
+        HIPCHECK(hipStreamSynchronize(s));
+        HIPCHECK(hipStreamSynchronize(stream));
+        qpad.ensure((size_t)B * dp);
+        cd.ensure((size_t)B * nlist);
+        probes.ensure(BP);
+        nseg_qp.ensure(BP);
+        pbqp.ensure(BP);
+        sorted_pair.ensure(BP);
+        pbs.ensure(BP);
+        counters.ensure(2);
+        items.ensure(max_items);
+        part_d.ensure(max_items * k);
+        part_i.ensure(max_items * k);
+        slot_d.ensure(BP * k);
+        slot_i.ensure(BP * k);
+        carry_d.ensure((size_t)P * k);
+        carry_i.ensure((size_t)P * k);
+    }
+
+    // ---- search: ivf_flat_index.cpp:205-256, one batch of B queries ----
+    void run_batch(const float* d_q, uint32_t B, uint32_t P, uint32_t k, float* out_d_, uint64_t* out_i_,
+                   hipStream_t s) {
+        const int regs_k = vdbk::topk_regs(k);
+        const int regs_p = vdbk::topk_regs(P);
+        const uint32_t group = (uint32_t)vdbk::scan_group(regs_k);
+        const uint32_t BP = B * P;
+        const uint64_t max_items = (uint64_t)B * nseg_prefix[P];
+        require(max_items < (1ull << 32), "batch too large", VDB_ERR_UNSUPPORTED);
+        EventSet* ev = prof ? &next_events() : nullptr;
+        if (ev) HIPCHECK(hipEventRecord(ev->begin, s));
+
+        vdbk::launch_pad_rows(d_q, B, dim, dp, qpad.ensure((size_t)B * dp), s);
+        vdbk::launch_coarse(metric, cent_il.p, nlist, d4, qpad.p, B, cd.ensure((size_t)B * nlist), s);
+        vdbk::launch_select(regs_p, cd.p, nlist, B, P, probes.ensure(BP), s);
+        if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
+        vdbk::launch_plan(probes.p, d_nseg.p, d_count_local.p, B, P, group, items.ensure(max_items),
+                          counters.ensure(2), sorted_pair.ensure(BP), pbs.ensure(BP), pbqp.ensure(BP),
+                          nseg_qp.ensure(BP), stats.ensure(4), s);
+        part_d.ensure(max_items * k);
+        part_i.ensure(max_items * k);
+        if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
+        vdbk::launch_scan(metric, regs_k, (uint32_t)max_items, arena.p, arena_ids.p, d_block_off.p, d_count_local.p,
+                          qpad.p, d4, items.p, counters.p, sorted_pair.p, pbs.p, k, part_d.p, part_i.p, s);
+        if (ev) HIPCHECK(hipEventRecord(ev->scan_end, s));
+        vdbk::launch_slot_merge(regs_k, probes.p, d_count_global.p, nseg_qp.p, pbqp.p, part_d.p, part_i.p, BP, k,
+                                slot_d.ensure((size_t)BP * k), slot_i.ensure((size_t)BP * k), s);
+        vdbk::launch_query_merge(regs_k, probes.p, d_count_global.p, slot_d.p, slot_i.p, carry_d.p, carry_i.p, B, P, k,
+                                 stale, out_d_, out_i_, s);
+        if (stale) vdbk::launch_carry(probes.p, d_count_global.p, B, P, k, slot_d.p, slot_i.p, carry_d.p, carry_i.p, s);
+        if (ev) HIPCHECK(hipEventRecord(ev->end, s));
+        HIPCHECK(hipGetLastError());
+    }
+
+    void search_device(const float* d_q, uint32_t n, uint32_t nprobe, uint32_t k, float* d_dist, uint64_t* d_ids,
+                       hipStream_t s) {
+        if (n == 0 || k == 0) return;
+        require(k <= (uint32_t)vdbk::kMaxK, "k above 1024 is not supported", VDB_ERR_UNSUPPORTED);
+        const uint32_t P = std::min(nprobe, nlist);  // cpp:218-222 reads out of bounds beyond nlist
+        if (P == 0) {
+            vdbk::launch_fill_empty((uint64_t)n * k, d_dist, d_ids, s);
+            HIPCHECK(hipGetLastError());
+            return;
+        }
+        require(P <= (uint32_t)vdbk::kMaxK, "nprobe above 1024 is not supported", VDB_ERR_UNSUPPORTED);
+        if (!stats.p) {
+            stats.ensure(4);
+            HIPCHECK(hipMemsetAsync(stats.p, 0, 32, s));
+        }
+        const uint32_t bmax = std::max<uint32_t>(1, std::min<uint32_t>(batch, vdbk::kPlanMaxPairs / P));
+        ensure_workspace(std::min(bmax, n), P, k, s);
+        // Slot contents live for one search call (cpp:210-211).
+        HIPCHECK(hipMemsetAsync(carry_i.p, 0xFF, (size_t)P * k * 8, s));
+        for (uint32_t b0 = 0; b0 < n; b0 += bmax) {
+            const uint32_t B = std::min(bmax, n - b0);
+            run_batch(d_q + (size_t)b0 * dim, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s);
+        }
+    }
+};
+
+extern "C" {
+
+const char* vdb_last_error(void) { return g_last_error.c_str(); }
+const char* vdb_version(void) { return "vdb_ivf 0.1.0 (gfx950)"; }
+
+int vdb_device_count(int* count) {
+    return guarded([&] {
+        require(count != nullptr, "null count");
+        HIPCHECK(hipGetDeviceCount(count));
+    });
+}
+
+int vdb_ivf_create(const vdb_ivf_config* cfg, vdb_ivf** out) {
+    return guarded([&] {
+        require(cfg && out, "null argument");
+        // ivf_flat_index.cpp:17-19
+        require(cfg->dimension > 0 && cfg->nlist > 0, "Invalid configuration: dimension and nlist must be > 0");
+        require(cfg->metric >= 0 && cfg->metric <= 2, "unknown metric");
+        require(cfg->nlist < (1u << 19) - 1, "nlist above 524286 is not supported", VDB_ERR_UNSUPPORTED);
+        auto* h = new vdb_ivf();
+        try {
+            h->dim = cfg->dimension;
+            h->nlist = cfg->nlist;
+            h->d4 = (cfg->dimension + 3) / 4;
+            h->dp = h->d4 * 4;
+            h->metric = cfg->metric;
+            h->device = cfg->device;
+            h->max_gpu_memory = cfg->max_gpu_memory;
+            h->set_device();
+            HIPCHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+            h->cent_rm.ensure((size_t)h->nlist * h->dp);
+            h->cent_il.ensure(cdiv(h->nlist, 64) * h->d4 * 64);
+            HIPCHECK(hipMemsetAsync(h->cent_rm.p, 0, (size_t)h->nlist * h->dp * 4, h->stream));  // cpp:22
+            h->refresh_centroid_layout();
+            h->count.assign(h->nlist, 0);
+            h->owned.assign(h->nlist, 1);
+            h->block_off.assign(h->nlist, 0);
+            h->upload_directory();
+        } catch (...) {
+            delete h;
+            throw;
+        }
+        *out = h;
+    });
+}
+
+int vdb_ivf_destroy(vdb_ivf* h) {
+    return guarded([&] {
+        if (!h) return;
+        (void)hipSetDevice(h->device);
+        (void)hipStreamSynchronize(h->stream);
+        delete h;
+    });
+}
+
+int vdb_ivf_train(vdb_ivf* h, const float* v, uint64_t n) {
+    return guarded([&] {
+        require(h && (v || n == 0), "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        require(n > 0, "train needs at least one vector");
+        DevBuf<float> dv;
+        HIPCHECK(hipMemcpyAsync(dv.ensure(n * h->dim), v, n * h->dim * 4, hipMemcpyHostToDevice, h->stream));
+        h->train(dv.p, n);
+    });
+}
+
+int vdb_ivf_train_device(vdb_ivf* h, const float* d_v, uint64_t n) {
+    return guarded([&] {
+        require(h && (d_v || n == 0), "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        h->train(d_v, n);
+    });
+}
+
+int vdb_ivf_set_centroids(vdb_ivf* h, const float* c) {
+    return guarded([&] {
+        require(h && c, "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        HIPCHECK(hipMemcpy2DAsync(h->cent_rm.p, h->dp * 4, c, h->dim * 4, h->dim * 4, h->nlist,
+                                  hipMemcpyHostToDevice, h->stream));
+        h->refresh_centroid_layout();
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int vdb_ivf_get_centroids(vdb_ivf* h, float* c) {
+    return guarded([&] {
+        require(h && c, "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        HIPCHECK(hipMemcpy2DAsync(c, h->dim * 4, h->cent_rm.p, h->dp * 4, h->dim * 4, h->nlist,
+                                  hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int vdb_ivf_add(vdb_ivf* h, const float* v, const uint64_t* ids, uint64_t n) {
+    return guarded([&] {
+        require(h && ((v && ids) || n == 0), "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        if (n == 0) return;
+        DevBuf<float> dv;
+        DevBuf<uint64_t> di;
+        HIPCHECK(hipMemcpyAsync(dv.ensure(n * h->dim), v, n * h->dim * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHECK(hipMemcpyAsync(di.ensure(n), ids, n * 8, hipMemcpyHostToDevice, h->stream));
+        h->add(dv.p, di.p, n);
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int vdb_ivf_add_device(vdb_ivf* h, const float* d_v, const uint64_t* d_ids, uint64_t n) {
+    return guarded([&] {
+        require(h && ((d_v && d_ids) || n == 0), "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        h->add(d_v, d_ids, n);
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int vdb_ivf_search(vdb_ivf* h, const float* q, uint32_t n, uint32_t nprobe, uint32_t k, float* dist,
+                   uint64_t* ids) {
+    return guarded([&] {
+        require(h && ((q && dist && ids) || n == 0 || k == 0), "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        if (n == 0 || k == 0) return;
+        HIPCHECK(hipMemcpyAsync(h->qin.ensure((size_t)n * h->dim), q, (size_t)n * h->dim * 4, hipMemcpyHostToDevice,
+                                h->stream));
+        h->search_device(h->qin.p, n, nprobe, k, h->out_d.ensure((size_t)n * k), h->out_i.ensure((size_t)n * k),
+                         h->stream);
+        HIPCHECK(hipMemcpyAsync(dist, h->out_d.p, (size_t)n * k * 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipMemcpyAsync(ids, h->out_i.p, (size_t)n * k * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int vdb_ivf_search_device(vdb_ivf* h, const float* d_q, uint32_t n, uint32_t nprobe, uint32_t k, float* d_dist,
+                          uint64_t* d_ids, void* stream) {
+    return guarded([&] {
+        require(h && ((d_q && d_dist && d_ids) || n == 0 || k == 0), "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+        h->search_device(d_q, n, nprobe, k, d_dist, d_ids, s);
+    });
+}
+
+int vdb_ivf_set_shard(vdb_ivf* h, uint32_t rank, uint32_t world) {
+    return guarded([&] {
+        require(h && world > 0 && rank < world, "invalid shard");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        h->set_shard(rank, world);
+    });
+}
+
+int vdb_merge_ranks_device(const float* d_dist, const uint64_t* d_ids, uint32_t nranks, uint32_t n, uint32_t k,
+                           float* d_out_dist, uint64_t* d_out_ids, void* stream) {
+    return guarded([&] {
+        if (n == 0 || k == 0) return;
+        require(d_dist && d_ids && d_out_dist && d_out_ids && nranks > 0, "null argument");
+        require(k <= (uint32_t)vdbk::kMaxK, "k above 1024 is not supported", VDB_ERR_UNSUPPORTED);
+        vdbk::launch_rank_merge(vdbk::topk_regs(k), d_dist, d_ids, nranks, n, k, d_out_dist, d_out_ids,
+                                (hipStream_t)stream);
+        HIPCHECK(hipGetLastError());
+    });
+}
+
+int vdb_shard_plan(const uint64_t* sizes, uint32_t nlist, uint32_t world, uint32_t* owner) {
+    return guarded([&] {
+        require(sizes && owner && world > 0, "invalid argument");
+        std::vector<uint32_t> order(nlist);
+        std::iota(order.begin(), order.end(), 0u);
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return sizes[a] > sizes[b]; });
+        using Load = std::pair<uint64_t, uint32_t>;  // (load, rank): least load, then lowest rank
+        std::priority_queue<Load, std::vector<Load>, std::greater<Load>> pq;
+        for (uint32_t r = 0; r < world; ++r) pq.push({0, r});
+        for (uint32_t l : order) {
+            Load top = pq.top();
+            pq.pop();
+            owner[l] = top.second;
+            top.first += sizes[l];
+            pq.push(top);
+        }
+    });
+}
+
+int vdb_ivf_warmup(vdb_ivf* h, const uint32_t* lists, uint32_t n) {
+    return guarded([&] {
+        require(h && (lists || n == 0), "null argument");
+        for (uint32_t i = 0; i < n; ++i) require(lists[i] < h->nlist, "list id out of range");
+        // Every list is already HBM-resident (the reference loads on first touch,
+        // ivf_flat_index.cpp:387-444); nothing to move.
+    });
+}
+
+int vdb_ivf_evict(vdb_ivf* h, uint32_t list) {
+    return guarded([&] {
+        require(h && list < h->nlist, "list id out of range");
+        // Residency is permanent; eviction is accepted as a no-op.
+    });
+}
+
+uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* h) {
+    if (!h) return 0;
+    return h->arena_blocks * 64 * ((uint64_t)h->dp * 4 + 8) + (uint64_t)h->nlist * h->dp * 8;
+}
+
+uint64_t vdb_ivf_ntotal(const vdb_ivf* h) { return h ? h->total : 0; }
+
+int vdb_ivf_list_sizes(const vdb_ivf* h, uint64_t* sizes) {
+    return guarded([&] {
+        require(h && sizes, "null argument");
+        std::copy(h->count.begin(), h->count.end(), sizes);
+    });
+}
+
+int vdb_ivf_get_list(vdb_ivf* h, uint32_t list, float* vectors, uint64_t* ids) {
+    return guarded([&] {
+        require(h && list < h->nlist, "list id out of range");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        const uint64_t c = h->count[list];
+        if (c == 0) return;
+        require(h->owned[list], "list is not stored on this shard", VDB_ERR_STATE);
+        DevBuf<float> dv;
+        DevBuf<uint64_t> di;
+        vdbk::launch_export_list(h->arena.p, h->arena_ids.p, h->block_off[list], (uint32_t)c, h->dim, h->d4,
+                                 dv.ensure(c * h->dim), di.ensure(c), h->stream);
+        HIPCHECK(hipGetLastError());
+        if (vectors) HIPCHECK(hipMemcpyAsync(vectors, dv.p, c * h->dim * 4, hipMemcpyDeviceToHost, h->stream));
+        if (ids) HIPCHECK(hipMemcpyAsync(ids, di.p, c * 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int vdb_ivf_set_batch(vdb_ivf* h, uint32_t batch) {
+    return guarded([&] {
+        require(h && batch > 0, "invalid batch");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->batch = batch;
+    });
+}
+
+int vdb_ivf_set_stale_slots(vdb_ivf* h, int enable) {
+    return guarded([&] {
+        require(h, "null handle");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->stale = enable ? 1 : 0;
+    });
+}
+
+int vdb_ivf_profile_enable(vdb_ivf* h, int enable) {
+    return guarded([&] {
+        require(h, "null handle");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->prof = enable != 0;
+    });
+}
+
+int vdb_ivf_profile_reset(vdb_ivf* h) {
+    return guarded([&] {
+        require(h, "null handle");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        HIPCHECK(hipDeviceSynchronize());
+        h->events_used = 0;
+        HIPCHECK(hipMemsetAsync(h->stats.ensure(4), 0, 32, h->stream));
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
+    return guarded([&] {
+        require(h && out, "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        HIPCHECK(hipDeviceSynchronize());
+        vdb_ivf_profile p{};
+        for (size_t i = 0; i < h->events_used; ++i) {
+            const EventSet& e = h->events[i];
+            float a = 0, b = 0, c = 0;
+            HIPCHECK(hipEventElapsedTime(&a, e.scan_begin, e.scan_end));
+            HIPCHECK(hipEventElapsedTime(&b, e.begin, e.coarse_end));
+            HIPCHECK(hipEventElapsedTime(&c, e.begin, e.end));
+            p.scan_ms += a;
+            p.coarse_ms += b;
+            p.total_ms += c;
+            p.scan_launches++;
+        }
+        unsigned long long st[4] = {0, 0, 0, 0};
+        if (h->stats.p) HIPCHECK(hipMemcpy(st, h->stats.p, 32, hipMemcpyDeviceToHost));
+        p.distinct_lists = st[0];
+        p.scan_vectors = st[1];
+        p.work_items = st[2];
+        p.batches = st[3];
+        p.scan_bytes = st[1] * (uint64_t)h->dim * 4;
+        *out = p;
+    });
+}
+
+int vdb_ivf_synchronize(vdb_ivf* h) {
+    return guarded([&] {
+        require(h, "null handle");
+        h->set_device();
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+void* vdb_ivf_stream(vdb_ivf* h) { return h ? (void*)h->stream : nullptr; }
+
+int vdb_gen_normal_device(float* d_out, uint64_t n, uint64_t seed, uint64_t offset, void* stream) {
+    return guarded([&] {
+        require(d_out || n == 0, "null argument");
+        vdbk::launch_gen_normal(d_out, n, seed, offset, (hipStream_t)stream);
+        HIPCHECK(hipGetLastError());
+    });
+}
+
+}  // extern "C"

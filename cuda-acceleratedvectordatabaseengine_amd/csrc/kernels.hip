@@ -1,0 +1,1047 @@
+// kernels.hip — hand-written gfx950 kernels of the IVF-Flat search path.
+//
+// Exactness: every distance is the reference's sequential fp32 sum
+// (ivf_flat_index.cpp:308-318, 352-362): diff = a - b rounded, diff*diff rounded,
+// acc + term rounded, d = 0..D-1. This file is compiled with -ffp-contract=off and
+// the pragma below, so no multiply-add is ever fused; v_sub/v_mul/v_add_f32 are
+// IEEE round-to-nearest with denormals kept (the default gfx950 float mode), the
+// same results the x86 SSE path produces.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cfloat>
+
+#include "kernels.hpp"
+#include "wave_topk.hpp"
+
+namespace vdbk {
+
+enum { kL2 = 0, kIP = 1, kCos = 2 };
+
+template <int M>
+__device__ __forceinline__ float dist_term(float acc, float a, float b) {
+    if constexpr (M == kL2) {
+        const float diff = a - b;
+        return acc + diff * diff;
+    } else if constexpr (M == kIP) {
+        return acc + a * b;
+    } else {
+        return acc;  // Cosine: the CPU path never assigns a distance (cpp:351-362)
+    }
+}
+template <int M>
+__device__ __forceinline__ float dist_finish(float acc) {
+    if constexpr (M == kIP) return -acc;
+    return acc;
+}
+
+template <int M>
+__device__ __forceinline__ float acc4(float acc, const float4 q, const float4 x) {
+    acc = dist_term<M>(acc, q.x, x.x);
+    acc = dist_term<M>(acc, q.y, x.y);
+    acc = dist_term<M>(acc, q.z, x.z);
+    acc = dist_term<M>(acc, q.w, x.w);
+    return acc;
+}
+
+__device__ __forceinline__ uint32_t wave_index() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+// ============================================================================
+// Query padding: [n][dim] -> [n][dp] with +0.0f pads.
+// ============================================================================
+__global__ void k_pad_rows(const float* __restrict__ src, uint64_t n, uint32_t dim, uint32_t dp,
+                           float* __restrict__ dst) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * dp) return;
+    const uint64_t r = e / dp;
+    const uint32_t c = (uint32_t)(e - r * dp);
+    dst[e] = c < dim ? src[r * dim + c] : 0.0f;
+}
+
+// ============================================================================
+// Coarse quantiser, distance part (select_nprobe_lists, cpp:302-321).
+// One lane = one centroid of an interleaved 64-centroid block; each wave takes
+// 4 queries whose dims are wave-uniform (scalar loads). Exact sequential sums.
+// ============================================================================
+template <int M>
+__global__ __launch_bounds__(256) void k_coarse(const float4* __restrict__ cent, uint32_t nlist, uint32_t d4,
+                                                const float* __restrict__ qpad, uint32_t B,
+                                                float* __restrict__ cd) {
+    constexpr int G = 4;
+    const int lane = lane_id();
+    const uint32_t cb = blockIdx.x;
+    const uint32_t q0 = (blockIdx.y * 4 + wave_index()) * G;
+    if (q0 >= B) return;
+    const uint32_t dp = d4 * 4;
+    const float4* q[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) q[g] = (const float4*)(qpad + (size_t)min(q0 + g, B - 1) * dp);
+    const float4* vb = cent + (size_t)cb * d4 * 64 + lane;
+    float acc[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) acc[g] = 0.0f;
+#pragma unroll 4
+    for (uint32_t t = 0; t < d4; ++t) {
+        const float4 x = vb[(size_t)t * 64];
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g] = acc4<M>(acc[g], q[g][t], x);
+    }
+    const uint32_t c = cb * 64 + lane;
+    if (c < nlist) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+            if (q0 + g < B) cd[(size_t)(q0 + g) * nlist + c] = dist_finish<M>(acc[g]);
+    }
+}
+
+// ============================================================================
+// Coarse quantiser, selection part: the first min(nprobe, nlist) lists by
+// (dist, list_id) — partial_sort on std::pair (cpp:324-333). One wave per query.
+// ============================================================================
+template <int R>
+__global__ __launch_bounds__(256) void k_select(const float* __restrict__ cd, uint32_t nlist, uint32_t B,
+                                                uint32_t P, uint32_t* __restrict__ probes) {
+    const uint32_t q = blockIdx.x * 4 + wave_index();
+    if (q >= B) return;
+    const int lane = lane_id();
+    WaveTopK<R> tk;
+    tk.init();
+    float kd = __builtin_inff();
+    uint64_t ki = kNoId;
+    const float* row = cd + (size_t)q * nlist;
+    for (uint32_t c0 = 0; c0 < nlist; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        const bool valid = c < nlist;
+        const float d = valid ? row[c] : __builtin_inff();
+        offer_lanes<R>(tk, valid && d <= kd, d, (uint64_t)c, (int)P, kd, ki);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t e = r * 64 + lane;
+        if (e < P) probes[(size_t)q * P + e] = (uint32_t)tk.id[r];
+    }
+}
+
+// ============================================================================
+// Probe inversion (one workgroup): sort the batch's (query, probe) pairs by list,
+// give every pair its range of partial-result slots, and emit scan work items
+// (list, segment, group of <= G pairs). Items of one list are ordered
+// (segment, group) so the groups that re-read a segment sit in one workgroup.
+// ============================================================================
+constexpr uint32_t kInvalidKey = 0xFFFFFFFFu;
+
+__device__ uint32_t plan_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
+    const int lane = lane_id();
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t nw = blockDim.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t w = threadIdx.x < nw ? sh[threadIdx.x] : 0u;
+        uint32_t s = w;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(s, off);
+            if (lane >= off) s += y;
+        }
+        if (threadIdx.x < nw) sh[threadIdx.x] = s - w;
+        if (threadIdx.x == nw - 1) sh[32] = s;
+    }
+    __syncthreads();
+    const uint32_t res = sh[wid] + x - v;
+    total = sh[32];
+    __syncthreads();
+    return res;
+}
+
+__global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ probes,
+                                               const uint32_t* __restrict__ nseg_local,
+                                               const uint32_t* __restrict__ count_local, uint32_t B,
+                                               uint32_t P, uint32_t NP, uint32_t G, ScanItem* __restrict__ items,
+                                               uint32_t* __restrict__ counters,
+                                               uint32_t* __restrict__ sorted_pair,
+                                               uint32_t* __restrict__ part_base_sorted,
+                                               uint32_t* __restrict__ part_base_qp,
+                                               uint32_t* __restrict__ nseg_qp,
+                                               unsigned long long* __restrict__ stats) {
+    __shared__ uint32_t keys[kPlanMaxPairs];
+    __shared__ uint32_t starts[kPlanMaxPairs + 1];
+    __shared__ uint32_t ibase[kPlanMaxPairs];
+    __shared__ uint32_t sh[33];
+    __shared__ uint32_t s_nvalid;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t BP = B * P;
+
+    if (tid == 0) s_nvalid = 0;
+    for (uint32_t i = tid; i < NP; i += blockDim.x) {
+        uint32_t key = kInvalidKey;
+        if (i < BP) {
+            const uint32_t l = probes[i];
+            const uint32_t ns = nseg_local[l];
+            nseg_qp[i] = ns;
+            if (ns) key = (l << 13) | i;
+        }
+        keys[i] = key;
+    }
+    __syncthreads();
+
+    for (uint32_t kk = 2; kk <= NP; kk <<= 1) {
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < NP; i += blockDim.x) {
+                const uint32_t x = i ^ j;
+                if (x > i) {
+                    const uint32_t a = keys[i], b = keys[x];
+                    const bool asc = (i & kk) == 0;
+                    if ((a > b) == asc) {
+                        keys[i] = b;
+                        keys[x] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = tid; i < NP; i += blockDim.x)
+        if (keys[i] != kInvalidKey && (i + 1 == NP || keys[i + 1] == kInvalidKey)) s_nvalid = i + 1;
+    __syncthreads();
+    const uint32_t nvalid = s_nvalid;
+
+    // Each thread owns a contiguous chunk of sorted positions.
+    const uint32_t per = (nvalid + blockDim.x - 1) / blockDim.x;
+    const uint32_t c0 = min(nvalid, tid * per), c1 = min(nvalid, c0 + per);
+    auto list_of = [&](uint32_t s) { return keys[s] >> 13; };
+    auto is_head = [&](uint32_t s) { return s == 0 || list_of(s - 1) != list_of(s); };
+
+    uint32_t hsum = 0, nsum = 0;
+    for (uint32_t s = c0; s < c1; ++s) {
+        hsum += is_head(s) ? 1u : 0u;
+        nsum += nseg_local[list_of(s)];
+    }
+    uint32_t nd, nparts;
+    const uint32_t dl_base = plan_excl_scan(hsum, sh, nd);
+    const uint32_t pb_base = plan_excl_scan(nsum, sh, nparts);
+    {
+        int cur = (int)dl_base - 1;
+        uint32_t pb = pb_base;
+        for (uint32_t s = c0; s < c1; ++s) {
+            const uint32_t l = list_of(s);
+            if (is_head(s)) starts[++cur] = s;
+            const uint32_t i = keys[s] & 8191u;
+            sorted_pair[s] = ((i / P) << 16) | (i % P);
+            part_base_sorted[s] = pb;
+            part_base_qp[i] = pb;
+            pb += nseg_local[l];
+        }
+    }
+    if (tid == 0) starts[nd] = nvalid;
+    __syncthreads();
+
+    uint32_t isum = 0;
+    {
+        int cur = (int)dl_base - 1;
+        for (uint32_t s = c0; s < c1; ++s) {
+            if (!is_head(s)) continue;
+            ++cur;
+            const uint32_t m = starts[cur + 1] - starts[cur];
+            isum += ((m + G - 1) / G) * nseg_local[list_of(s)];
+        }
+    }
+    uint32_t nitems;
+    const uint32_t ib_base = plan_excl_scan(isum, sh, nitems);
+    {
+        int cur = (int)dl_base - 1;
+        uint32_t ib = ib_base;
+        for (uint32_t s = c0; s < c1; ++s) {
+            if (!is_head(s)) continue;
+            ++cur;
+            const uint32_t l = list_of(s);
+            const uint32_t m = starts[cur + 1] - starts[cur];
+            ibase[cur] = ib;
+            ib += ((m + G - 1) / G) * nseg_local[l];
+            atomicAdd(&stats[1], (unsigned long long)count_local[l]);
+        }
+    }
+    __syncthreads();
+    {
+        int cur = (int)dl_base - 1;
+        for (uint32_t s = c0; s < c1; ++s) {
+            if (is_head(s)) ++cur;
+            const uint32_t rank = s - starts[cur];
+            if (rank % G) continue;
+            const uint32_t l = list_of(s);
+            const uint32_t m = starts[cur + 1] - starts[cur];
+            const uint32_t ng = (m + G - 1) / G;
+            const uint32_t gi = rank / G;
+            const uint32_t gs = min(G, m - rank);
+            const uint32_t ns = nseg_local[l];
+            for (uint32_t seg = 0; seg < ns; ++seg) {
+                ScanItem it;
+                it.list = l;
+                it.seg = seg;
+                it.pair_start = s;
+                it.npairs = gs;
+                items[ibase[cur] + seg * ng + gi] = it;
+            }
+        }
+    }
+    if (tid == 0) {
+        counters[0] = nitems;
+        counters[1] = nparts;
+        atomicAdd(&stats[0], (unsigned long long)nd);
+        atomicAdd(&stats[2], (unsigned long long)nitems);
+        atomicAdd(&stats[3], 1ull);
+    }
+}
+
+// ============================================================================
+// ivf_scan: the fine scan of one list segment for a group of <= G queries
+// (search_list_cpu, cpp:347-370). One lane = one list vector; one wave-load reads
+// 1 KiB of the interleaved block; query dims are wave-uniform (scalar loads).
+// Each query keeps a wave top-k of (dist, id); the segment's top-k becomes one
+// partial result of that (query, probe) pair.
+// ============================================================================
+struct ScanArgs {
+    const float4* __restrict__ arena;
+    const uint64_t* __restrict__ ids;
+    const uint64_t* __restrict__ block_off;
+    const uint32_t* __restrict__ count;
+    const float* __restrict__ qpad;
+    const ScanItem* __restrict__ items;
+    const uint32_t* __restrict__ counters;
+    const uint32_t* __restrict__ sorted_pair;
+    const uint32_t* __restrict__ part_base_sorted;
+    float* __restrict__ part_d;
+    uint64_t* __restrict__ part_i;
+    uint32_t d4;
+    uint32_t k;
+};
+
+template <int R, int G, int M>
+__device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) {
+    const int lane = lane_id();
+    const uint32_t count = a.count[it.list];
+    const uint64_t b0 = a.block_off[it.list] + (uint64_t)it.seg * kSegBlocks;
+    const uint32_t v0 = it.seg * kSegVectors;
+    const uint32_t nv = min(count - v0, (uint32_t)kSegVectors);
+    const uint32_t nb = (nv + 63) >> 6;
+    const uint32_t d4 = a.d4;
+    const int k = (int)a.k;
+
+    const float4* q[G];
+    uint32_t part[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint32_t pr = a.sorted_pair[it.pair_start + g];
+        q[g] = (const float4*)(a.qpad + (size_t)(pr >> 16) * d4 * 4);
+        part[g] = a.part_base_sorted[it.pair_start + g] + it.seg;
+    }
+    WaveTopK<R> tk[G];
+    float kd[G];
+    uint64_t ki[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        tk[g].init();
+        kd[g] = __builtin_inff();
+        ki[g] = kNoId;
+    }
+
+    for (uint32_t j = 0; j < nb; ++j) {
+        const float4* vb = a.arena + (b0 + j) * d4 * 64 + lane;
+        float acc[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g] = 0.0f;
+#pragma unroll 8
+        for (uint32_t t = 0; t < d4; ++t) {
+            const float4 x = vb[(size_t)t * 64];
+#pragma unroll
+            for (int g = 0; g < G; ++g) acc[g] = acc4<M>(acc[g], q[g][t], x);
+        }
+        const bool valid = j * 64 + lane < nv;
+        bool want[G];
+        bool any = false;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            acc[g] = dist_finish<M>(acc[g]);
+            want[g] = valid && acc[g] <= kd[g];
+            any |= want[g];
+        }
+        if (__ballot(any)) {
+            const uint64_t vid = valid ? a.ids[(b0 + j) * 64 + lane] : kNoId;
+#pragma unroll
+            for (int g = 0; g < G; ++g) offer_lanes<R>(tk[g], want[g], acc[g], vid, k, kd[g], ki[g]);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int e = r * 64 + lane;
+            if (e < k) {
+                a.part_d[(size_t)part[g] * k + e] = tk[g].d[r];
+                a.part_i[(size_t)part[g] * k + e] = tk[g].id[r];
+            }
+        }
+    }
+}
+
+template <int R, int M>
+__global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
+    constexpr int GMAX = (R == 1) ? 4 : (R == 2 ? 2 : 1);
+    const uint32_t idx = blockIdx.x * 4 + wave_index();
+    if (idx >= a.counters[0]) return;
+    const ScanItem it = a.items[idx];
+    switch (it.npairs) {
+        case 1: scan_item<R, 1, M>(a, it); break;
+        case 2: if constexpr (GMAX >= 2) scan_item<R, 2, M>(a, it); break;
+        case 3: if constexpr (GMAX >= 3) scan_item<R, 3, M>(a, it); break;
+        case 4: if constexpr (GMAX >= 4) scan_item<R, 4, M>(a, it); break;
+        default: break;
+    }
+}
+
+// ============================================================================
+// Per (query, probe) pair: top-min(k, n_l) of the list's segment partials, as
+// search_list_cpu's partial_sort yields for the whole list (cpp:368-377).
+// ============================================================================
+template <int R>
+__global__ __launch_bounds__(256) void k_slot_merge(const uint32_t* __restrict__ probes,
+                                                    const uint32_t* __restrict__ count_global,
+                                                    const uint32_t* __restrict__ nseg_qp,
+                                                    const uint32_t* __restrict__ part_base_qp,
+                                                    const float* __restrict__ part_d,
+                                                    const uint64_t* __restrict__ part_i, uint32_t BP, uint32_t k,
+                                                    float* __restrict__ slot_d, uint64_t* __restrict__ slot_i) {
+    const uint32_t i = blockIdx.x * 4 + wave_index();
+    if (i >= BP) return;
+    const int lane = lane_id();
+    const uint32_t ns = nseg_qp[i];
+    float* od = slot_d + (size_t)i * k;
+    uint64_t* oi = slot_i + (size_t)i * k;
+    if (ns == 0) {
+        for (uint32_t e = lane; e < k; e += 64) {
+            od[e] = __builtin_inff();
+            oi[e] = kNoId;
+        }
+        return;
+    }
+    const size_t base = (size_t)part_base_qp[i] * k;
+    if (ns == 1) {
+        for (uint32_t e = lane; e < k; e += 64) {
+            od[e] = part_d[base + e];
+            oi[e] = part_i[base + e];
+        }
+        return;
+    }
+    const int kk = (int)min(k, count_global[probes[i]]);
+    WaveTopK<R> tk;
+    tk.init();
+    float kd = __builtin_inff();
+    uint64_t ki = kNoId;
+    const uint32_t n = ns * k;
+    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        const bool valid = c < n;
+        const float d = valid ? part_d[base + c] : __builtin_inff();
+        const uint64_t id = valid ? part_i[base + c] : kNoId;
+        offer_lanes<R>(tk, valid && d <= kd, d, id, kk, kd, ki);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < (int)k) {
+            od[e] = e < kk ? tk.d[r] : __builtin_inff();
+            oi[e] = e < kk ? tk.id[r] : kNoId;
+        }
+    }
+}
+
+// Offer k slot entries to a de-duplicating list (merge_results, cpp:481-504):
+// ids == UINT64_MAX are not results (cpp:486).
+template <int R>
+__device__ __forceinline__ void offer_slot_unique(WaveTopK<R>& tk, const float* sd, const uint64_t* si,
+                                                  uint32_t k, float& kd, uint64_t& ki) {
+    const int lane = lane_id();
+    for (uint32_t c0 = 0; c0 < k; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        const bool valid = c < k;
+        const float d = valid ? sd[c] : __builtin_inff();
+        const uint64_t id = valid ? si[c] : kNoId;
+        uint64_t mask = __ballot(valid && id != kNoId && d <= kd);
+        while (mask) {
+            const int l = __ffsll((long long)mask) - 1;
+            mask &= mask - 1;
+            tk.offer_unique(rd_lane(d, l), rd_lane(id, l), (int)k, kd, ki);
+        }
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void write_final(const WaveTopK<R>& tk, uint32_t k, float* od, uint64_t* oi) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < (int)k) {
+            const bool real = tk.id[r] != kNoId;
+            od[e] = real ? tk.d[r] : FLT_MAX;  // padding as cpp:513-517
+            oi[e] = tk.id[r];
+        }
+    }
+}
+
+// ============================================================================
+// Per query: merge the P slots (with the reference's stale-slot reuse for empty
+// lists, cpp:210-233) into the unique-id top-k.
+// ============================================================================
+template <int R>
+__global__ __launch_bounds__(256) void k_query_merge(const uint32_t* __restrict__ probes,
+                                                     const uint32_t* __restrict__ count_global,
+                                                     const float* __restrict__ slot_d,
+                                                     const uint64_t* __restrict__ slot_i,
+                                                     const float* __restrict__ carry_d,
+                                                     const uint64_t* __restrict__ carry_i, uint32_t B, uint32_t P,
+                                                     uint32_t k, int stale, float* __restrict__ out_d,
+                                                     uint64_t* __restrict__ out_i) {
+    const uint32_t q = blockIdx.x * 4 + wave_index();
+    if (q >= B) return;
+    WaveTopK<R> tk;
+    tk.init();
+    float kd = __builtin_inff();
+    uint64_t ki = kNoId;
+    for (uint32_t p = 0; p < P; ++p) {
+        const float* sd = nullptr;
+        const uint64_t* si = nullptr;
+        if (count_global[probes[(size_t)q * P + p]] > 0) {
+            sd = slot_d + ((size_t)q * P + p) * k;
+            si = slot_i + ((size_t)q * P + p) * k;
+        } else if (stale) {
+            uint32_t q2 = q;
+            bool found = false;
+            while (q2 > 0) {
+                --q2;
+                if (count_global[probes[(size_t)q2 * P + p]] > 0) {
+                    found = true;
+                    break;
+                }
+            }
+            if (found) {
+                sd = slot_d + ((size_t)q2 * P + p) * k;
+                si = slot_i + ((size_t)q2 * P + p) * k;
+            } else {
+                sd = carry_d + (size_t)p * k;
+                si = carry_i + (size_t)p * k;
+            }
+        }
+        if (sd) offer_slot_unique<R>(tk, sd, si, k, kd, ki);
+    }
+    write_final<R>(tk, k, out_d + (size_t)q * k, out_i + (size_t)q * k);
+}
+
+// Slot content that survives into the next batch of the same search call.
+__global__ void k_carry(const uint32_t* __restrict__ probes, const uint32_t* __restrict__ count_global,
+                        uint32_t B, uint32_t P, uint32_t k, const float* __restrict__ slot_d,
+                        const uint64_t* __restrict__ slot_i, float* __restrict__ carry_d,
+                        uint64_t* __restrict__ carry_i) {
+    __shared__ int s_q;
+    const uint32_t p = blockIdx.x;
+    if (threadIdx.x == 0) {
+        int found = -1;
+        for (int q = (int)B - 1; q >= 0; --q)
+            if (count_global[probes[(size_t)q * P + p]] > 0) {
+                found = q;
+                break;
+            }
+        s_q = found;
+    }
+    __syncthreads();
+    if (s_q < 0) return;
+    const size_t src = ((size_t)s_q * P + p) * k;
+    for (uint32_t e = threadIdx.x; e < k; e += blockDim.x) {
+        carry_d[(size_t)p * k + e] = slot_d[src + e];
+        carry_i[(size_t)p * k + e] = slot_i[src + e];
+    }
+}
+
+// Final combine of per-rank partials [nranks][n][k] (list-sharded multi-GPU).
+template <int R>
+__global__ __launch_bounds__(256) void k_rank_merge(const float* __restrict__ d, const uint64_t* __restrict__ ids,
+                                                    uint32_t nranks, uint32_t n, uint32_t k,
+                                                    float* __restrict__ out_d, uint64_t* __restrict__ out_i) {
+    const uint32_t q = blockIdx.x * 4 + wave_index();
+    if (q >= n) return;
+    WaveTopK<R> tk;
+    tk.init();
+    float kd = __builtin_inff();
+    uint64_t ki = kNoId;
+    for (uint32_t r = 0; r < nranks; ++r)
+        offer_slot_unique<R>(tk, d + ((size_t)r * n + q) * k, ids + ((size_t)r * n + q) * k, k, kd, ki);
+    write_final<R>(tk, k, out_d + (size_t)q * k, out_i + (size_t)q * k);
+}
+
+__global__ void k_fill_empty(uint64_t n, float* __restrict__ d, uint64_t* __restrict__ i) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) {
+        d[e] = FLT_MAX;
+        i[e] = kNoId;
+    }
+}
+
+// ============================================================================
+// Build-side kernels: layout, assignment (assign_to_lists, cpp:259-295),
+// k-means++ seeding and Lloyd update (train, cpp:49-145).
+// ============================================================================
+// rows [n][dp] -> interleaved blocks [ceil(n/64)][d4][64] float4 (tail lanes zero).
+__global__ void k_interleave(const float* __restrict__ rows, uint64_t n, uint32_t d4, float4* __restrict__ out) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (block, t, lane)
+    const uint64_t nb = (n + 63) / 64;
+    if (e >= nb * d4 * 64) return;
+    const uint32_t lane = e & 63;
+    const uint64_t bt = e >> 6;
+    const uint64_t b = bt / d4;
+    const uint32_t t = (uint32_t)(bt - b * d4);
+    const uint64_t r = b * 64 + lane;
+    out[e] = r < n ? ((const float4*)(rows + r * (uint64_t)d4 * 4))[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__global__ void k_scatter_rows(const float* __restrict__ rows, const uint64_t* __restrict__ row_ids,
+                               const uint32_t* __restrict__ order, uint64_t n, uint32_t d4,
+                               const uint64_t* __restrict__ dest_slot, float4* __restrict__ arena,
+                               uint64_t* __restrict__ arena_ids) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (j, t)
+    if (e >= n * d4) return;
+    const uint64_t j = e / d4;
+    const uint32_t t = (uint32_t)(e - j * d4);
+    const uint64_t slot = dest_slot[j];
+    if (slot == ~0ull) return;  // list stored on another shard
+    const uint64_t row = order[j];
+    arena[((slot >> 6) * d4 + t) * 64 + (slot & 63)] = ((const float4*)(rows + row * (uint64_t)d4 * 4))[t];
+    if (t == 0) arena_ids[slot] = row_ids[row];
+}
+
+// Move each list's first nblocks[l] blocks from old_off[l] to new_off[l].
+__global__ void k_copy_lists(const float4* __restrict__ old_arena, const uint64_t* __restrict__ old_ids,
+                             const uint64_t* __restrict__ old_off, const uint64_t* __restrict__ new_off,
+                             const uint32_t* __restrict__ nblocks, uint32_t d4, float4* __restrict__ new_arena,
+                             uint64_t* __restrict__ new_ids) {
+    const uint32_t l = blockIdx.y;
+    const uint64_t nvec4 = (uint64_t)nblocks[l] * d4 * 64;
+    const float4* src = old_arena + old_off[l] * d4 * 64;
+    float4* dst = new_arena + new_off[l] * d4 * 64;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nvec4; e += (uint64_t)gridDim.x * blockDim.x)
+        dst[e] = src[e];
+    const uint64_t nid = (uint64_t)nblocks[l] * 64;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nid; e += (uint64_t)gridDim.x * blockDim.x)
+        new_ids[new_off[l] * 64 + e] = old_ids[old_off[l] * 64 + e];
+}
+
+__global__ void k_export_list(const float4* __restrict__ arena, const uint64_t* __restrict__ ids,
+                              uint64_t block_off, uint32_t count, uint32_t dim, uint32_t d4,
+                              float* __restrict__ out, uint64_t* __restrict__ out_ids) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (v, d)
+    if (e >= (uint64_t)count * dim) return;
+    const uint32_t v = (uint32_t)(e / dim), d = (uint32_t)(e - (uint64_t)v * dim);
+    const float* blk = (const float*)(arena + ((block_off + (v >> 6)) * d4 + (d >> 2)) * 64 + (v & 63));
+    out[e] = blk[d & 3];
+    if (d == 0 && out_ids) out_ids[v] = ids[(block_off << 6) + v];
+}
+
+// Exact argmin over centroids with the reference's strict '<' (lowest index wins
+// ties; a distance must beat FLT_MAX to count, else list 0). Lane = centroid,
+// 8 row vectors per wave whose dims are wave-uniform.
+template <int M>
+__global__ __launch_bounds__(256) void k_assign(const float* __restrict__ vpad, uint64_t n, uint32_t d4,
+                                                const float4* __restrict__ cent, uint32_t nlist,
+                                                uint32_t* __restrict__ out) {
+    constexpr int G = 8;
+    const int lane = lane_id();
+    const uint64_t v0 = ((uint64_t)blockIdx.x * 4 + wave_index()) * G;
+    if (v0 >= n) return;
+    const float4* q[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) q[g] = (const float4*)(vpad + min(v0 + g, n - 1) * (uint64_t)d4 * 4);
+    float bd[G];
+    uint32_t bc[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        bd[g] = FLT_MAX;
+        bc[g] = 0;
+    }
+    const uint32_t ncb = (nlist + 63) / 64;
+    for (uint32_t cb = 0; cb < ncb; ++cb) {
+        const float4* vb = cent + (size_t)cb * d4 * 64 + lane;
+        float acc[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g] = 0.0f;
+#pragma unroll 4
+        for (uint32_t t = 0; t < d4; ++t) {
+            const float4 x = vb[(size_t)t * 64];
+#pragma unroll
+            for (int g = 0; g < G; ++g) acc[g] = acc4<M>(acc[g], q[g][t], x);
+        }
+        const uint32_t c = cb * 64 + lane;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float d = dist_finish<M>(acc[g]);
+            if (c < nlist && d < bd[g]) {
+                bd[g] = d;
+                bc[g] = c;
+            }
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        float d = bd[g];
+        uint32_t c = bc[g];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const float od = __shfl_xor(d, off);
+            const uint32_t oc = (uint32_t)__shfl_xor((int)c, off);
+            if (od < d || (od == d && oc < c)) {
+                d = od;
+                c = oc;
+            }
+        }
+        if (lane == 0 && v0 + g < n) out[v0 + g] = c;
+    }
+}
+
+__global__ void k_histogram(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ counts) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) atomicAdd(&counts[keys[e]], 1u);
+}
+
+__global__ void k_fill_f32(float* __restrict__ p, uint64_t n, float v) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) p[e] = v;
+}
+
+// k-means++: min_dist[v] = std::min(min_dist[v], L2(v, newest centroid)) (cpp:68-84).
+// Lane = training vector (interleaved copy); centroid dims are wave-uniform.
+__global__ __launch_bounds__(256) void k_mindist_update(const float4* __restrict__ v_il, uint64_t n, uint32_t d4,
+                                                        const float* __restrict__ crow,
+                                                        float* __restrict__ mind) {
+    const uint64_t blk = (uint64_t)blockIdx.x * 4 + wave_index();
+    const int lane = lane_id();
+    if (blk * 64 >= n) return;
+    const float4* vb = v_il + blk * d4 * 64 + lane;
+    const float4* c4 = (const float4*)crow;
+    float acc = 0.0f;
+#pragma unroll 8
+    for (uint32_t t = 0; t < d4; ++t) acc = acc4<kL2>(acc, vb[(size_t)t * 64], c4[t]);
+    const uint64_t v = blk * 64 + lane;
+    if (v < n) {
+        const float m = mind[v];
+        mind[v] = (acc < m) ? acc : m;  // std::min(m, acc)
+    }
+}
+
+// The serial float sum of cpp:87 and the cumsum of cpp:95-96 produce the same
+// running values; one wave walks them in order, lane j latching element j.
+__global__ void k_serial_prefix(const float* __restrict__ mind, uint64_t n, float* __restrict__ prefix,
+                                float* __restrict__ total) {
+    const int lane = lane_id();
+    float s = 0.0f;
+    for (uint64_t c0 = 0; c0 < n; c0 += 64) {
+        const uint64_t e = c0 + lane;
+        const float v = e < n ? mind[e] : 0.0f;
+        float mine = 0.0f;
+        const int cnt = (int)min<uint64_t>(64, n - c0);
+        for (int j = 0; j < cnt; ++j) {
+            s = s + rd_lane(v, j);
+            if (lane == j) mine = s;
+        }
+        if (e < n) prefix[e] = mine;
+    }
+    if (lane == 0) *total = s;
+}
+
+// First v with cumsum >= target (cpp:95-103); n if none.
+__global__ void k_first_geq(const float* __restrict__ prefix, uint64_t n, float target,
+                            unsigned long long* __restrict__ out) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n && prefix[e] >= target) atomicMin(out, (unsigned long long)e);
+}
+
+__global__ void k_copy_row_if(const float* __restrict__ vpad, uint64_t n, uint32_t dp,
+                              const unsigned long long* __restrict__ idx, float* __restrict__ dst) {
+    const uint64_t i = *idx;
+    if (i >= n) return;
+    for (uint32_t d = threadIdx.x; d < dp; d += blockDim.x) dst[d] = vpad[i * dp + d];
+}
+
+// Lloyd update (cpp:122-141): per (cluster, dim), sum members in input order,
+// then divide by the count; empty clusters keep their centroid.
+__global__ void k_centroid_update(const float* __restrict__ vpad, uint32_t dp, const uint32_t* __restrict__ order,
+                                  const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ counts,
+                                  uint32_t dim, float* __restrict__ cent) {
+    const uint32_t c = blockIdx.y;
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t cnt = counts[c];
+    if (d >= dim || cnt == 0) return;
+    const uint32_t off = offsets[c];
+    float s = 0.0f;
+    for (uint32_t j = 0; j < cnt; ++j) s = s + vpad[(uint64_t)order[off + j] * dp + d];
+    cent[(uint64_t)c * dp + d] = s / (float)cnt;
+}
+
+__global__ void k_iota(uint32_t* __restrict__ out, uint64_t n) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) out[e] = (uint32_t)e;
+}
+
+__global__ void k_slots_from_order(const uint32_t* __restrict__ sorted_keys, uint64_t n,
+                                   const uint64_t* __restrict__ group_start,
+                                   const uint64_t* __restrict__ base_slot, uint64_t* __restrict__ dest) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t l = sorted_keys[j];
+    dest[j] = base_slot[l] == ~0ull ? ~0ull : base_slot[l] + (j - group_start[l]);
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// Counter-based Box-Muller normal draws (synthetic benchmark data only).
+__global__ void k_gen_normal(float* __restrict__ out, uint64_t n, uint64_t seed, uint64_t offset) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t h = splitmix64(splitmix64(seed) ^ (offset + i));
+    const float u1 = ((float)(h >> 40) + 1.0f) * (1.0f / 16777216.0f);       // (0, 1]
+    const float u2 = (float)(h & 0xFFFFFFull) * (1.0f / 16777216.0f);          // [0, 1)
+    out[i] = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+}
+
+// ============================================================================
+// Launchers
+// ============================================================================
+static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+void launch_pad_rows(const float* src, uint64_t n, uint32_t dim, uint32_t dp, float* dst, hipStream_t s) {
+    if (!n) return;
+    k_pad_rows<<<cdiv(n * dp, 256), 256, 0, s>>>(src, n, dim, dp, dst);
+}
+
+void launch_coarse(int metric, const float4* cent, uint32_t nlist, uint32_t d4, const float* qpad, uint32_t B,
+                   float* cd, hipStream_t s) {
+    dim3 grid(cdiv(nlist, 64), cdiv(B, 16));
+    if (metric == kL2) k_coarse<kL2><<<grid, 256, 0, s>>>(cent, nlist, d4, qpad, B, cd);
+    else if (metric == kIP) k_coarse<kIP><<<grid, 256, 0, s>>>(cent, nlist, d4, qpad, B, cd);
+    else k_coarse<kCos><<<grid, 256, 0, s>>>(cent, nlist, d4, qpad, B, cd);
+}
+
+void launch_select(int regs, const float* cd, uint32_t nlist, uint32_t B, uint32_t P, uint32_t* probes,
+                   hipStream_t s) {
+    const uint32_t g = cdiv(B, 4);
+    switch (regs) {
+        case 1: k_select<1><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
+        case 2: k_select<2><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
+        case 4: k_select<4><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
+        case 8: k_select<8><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
+        default: k_select<16><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
+    }
+}
+
+void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint32_t* count_local, uint32_t B,
+                 uint32_t P, uint32_t group, ScanItem* items, uint32_t* counters, uint32_t* sorted_pair,
+                 uint32_t* part_base_sorted, uint32_t* part_base_qp, uint32_t* nseg_qp,
+                 unsigned long long* stats, hipStream_t s) {
+    uint32_t np = 1;
+    while (np < B * P) np <<= 1;
+    k_plan<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, items, counters, sorted_pair,
+                              part_base_sorted, part_base_qp, nseg_qp, stats);
+}
+
+template <int R>
+static void scan_dispatch_metric(int metric, uint32_t grid, const ScanArgs& a, hipStream_t s) {
+    if (metric == kL2) k_scan<R, kL2><<<grid, 256, 0, s>>>(a);
+    else if (metric == kIP) k_scan<R, kIP><<<grid, 256, 0, s>>>(a);
+    else k_scan<R, kCos><<<grid, 256, 0, s>>>(a);
+}
+
+void launch_scan(int metric, int regs, uint32_t grid_items, const float4* arena, const uint64_t* ids,
+                 const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
+                 const ScanItem* items, const uint32_t* counters, const uint32_t* sorted_pair,
+                 const uint32_t* part_base_sorted, uint32_t k, float* part_d, uint64_t* part_i, hipStream_t s) {
+    if (!grid_items) return;
+    ScanArgs a{arena, ids, block_off, count_local, qpad, items, counters, sorted_pair, part_base_sorted,
+               part_d, part_i, d4, k};
+    const uint32_t grid = cdiv(grid_items, 4);
+    switch (regs) {
+        case 1: scan_dispatch_metric<1>(metric, grid, a, s); break;
+        case 2: scan_dispatch_metric<2>(metric, grid, a, s); break;
+        case 4: scan_dispatch_metric<4>(metric, grid, a, s); break;
+        case 8: scan_dispatch_metric<8>(metric, grid, a, s); break;
+        default: scan_dispatch_metric<16>(metric, grid, a, s); break;
+    }
+}
+
+void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const uint32_t* nseg_qp,
+                       const uint32_t* part_base_qp, const float* part_d, const uint64_t* part_i, uint32_t BP,
+                       uint32_t k, float* slot_d, uint64_t* slot_i, hipStream_t s) {
+    const uint32_t g = cdiv(BP, 4);
+    if (!g) return;
+#define VDB_SLOT(R) k_slot_merge<R><<<g, 256, 0, s>>>(probes, count_global, nseg_qp, part_base_qp, part_d, part_i, BP, k, slot_d, slot_i)
+    switch (regs) {
+        case 1: VDB_SLOT(1); break;
+        case 2: VDB_SLOT(2); break;
+        case 4: VDB_SLOT(4); break;
+        case 8: VDB_SLOT(8); break;
+        default: VDB_SLOT(16); break;
+    }
+#undef VDB_SLOT
+}
+
+void launch_query_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const float* slot_d,
+                        const uint64_t* slot_i, const float* carry_d, const uint64_t* carry_i, uint32_t B,
+                        uint32_t P, uint32_t k, int stale, float* out_d, uint64_t* out_i, hipStream_t s) {
+    const uint32_t g = cdiv(B, 4);
+    if (!g) return;
+#define VDB_QM(R) k_query_merge<R><<<g, 256, 0, s>>>(probes, count_global, slot_d, slot_i, carry_d, carry_i, B, P, k, stale, out_d, out_i)
+    switch (regs) {
+        case 1: VDB_QM(1); break;
+        case 2: VDB_QM(2); break;
+        case 4: VDB_QM(4); break;
+        case 8: VDB_QM(8); break;
+        default: VDB_QM(16); break;
+    }
+#undef VDB_QM
+}
+
+void launch_carry(const uint32_t* probes, const uint32_t* count_global, uint32_t B, uint32_t P, uint32_t k,
+                  const float* slot_d, const uint64_t* slot_i, float* carry_d, uint64_t* carry_i, hipStream_t s) {
+    if (!P || !B) return;
+    k_carry<<<P, 64, 0, s>>>(probes, count_global, B, P, k, slot_d, slot_i, carry_d, carry_i);
+}
+
+void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint32_t nranks, uint32_t n, uint32_t k,
+                       float* out_d, uint64_t* out_i, hipStream_t s) {
+    const uint32_t g = cdiv(n, 4);
+    if (!g) return;
+#define VDB_RM(R) k_rank_merge<R><<<g, 256, 0, s>>>(d, i, nranks, n, k, out_d, out_i)
+    switch (regs) {
+        case 1: VDB_RM(1); break;
+        case 2: VDB_RM(2); break;
+        case 4: VDB_RM(4); break;
+        case 8: VDB_RM(8); break;
+        default: VDB_RM(16); break;
+    }
+#undef VDB_RM
+}
+
+void launch_fill_empty(uint64_t n, float* d, uint64_t* i, hipStream_t s) {
+    if (!n) return;
+    k_fill_empty<<<cdiv(n, 256), 256, 0, s>>>(n, d, i);
+}
+
+void launch_interleave(const float* rows, uint64_t n, uint32_t dp, float4* blocks, hipStream_t s) {
+    if (!n) return;
+    const uint32_t d4 = dp / 4;
+    const uint64_t total = (n + 63) / 64 * d4 * 64;
+    k_interleave<<<cdiv(total, 256), 256, 0, s>>>(rows, n, d4, blocks);
+}
+
+void launch_scatter_rows(const float* rows, const uint64_t* row_ids, const uint32_t* order, uint64_t n, uint32_t dp,
+                         const uint64_t* dest_slot, float4* arena, uint64_t* arena_ids, hipStream_t s) {
+    if (!n) return;
+    const uint32_t d4 = dp / 4;
+    k_scatter_rows<<<cdiv(n * d4, 256), 256, 0, s>>>(rows, row_ids, order, n, d4, dest_slot, arena, arena_ids);
+}
+
+void launch_copy_lists(const float4* old_arena, const uint64_t* old_ids, const uint64_t* old_off,
+                       const uint64_t* new_off, const uint32_t* nblocks, uint32_t nlist, uint32_t d4,
+                       float4* new_arena, uint64_t* new_ids, hipStream_t s) {
+    if (!nlist) return;
+    dim3 grid(16, nlist);
+    k_copy_lists<<<grid, 256, 0, s>>>(old_arena, old_ids, old_off, new_off, nblocks, d4, new_arena, new_ids);
+}
+
+void launch_export_list(const float4* arena, const uint64_t* ids, uint64_t block_off, uint32_t count, uint32_t dim,
+                        uint32_t d4, float* out, uint64_t* out_ids, hipStream_t s) {
+    if (!count) return;
+    k_export_list<<<cdiv((uint64_t)count * dim, 256), 256, 0, s>>>(arena, ids, block_off, count, dim, d4, out,
+                                                                   out_ids);
+}
+
+void launch_assign(int metric, const float* vpad, uint64_t n, uint32_t dp, const float4* cent, uint32_t nlist,
+                   uint32_t* out, hipStream_t s) {
+    if (!n) return;
+    const uint32_t grid = cdiv(n, 32);
+    const uint32_t d4 = dp / 4;
+    if (metric == kL2) k_assign<kL2><<<grid, 256, 0, s>>>(vpad, n, d4, cent, nlist, out);
+    else if (metric == kIP) k_assign<kIP><<<grid, 256, 0, s>>>(vpad, n, d4, cent, nlist, out);
+    else k_assign<kCos><<<grid, 256, 0, s>>>(vpad, n, d4, cent, nlist, out);
+}
+
+void launch_histogram(const uint32_t* keys, uint64_t n, uint32_t* counts, hipStream_t s) {
+    if (!n) return;
+    k_histogram<<<cdiv(n, 256), 256, 0, s>>>(keys, n, counts);
+}
+
+void launch_mindist_init(float* mind, uint64_t n, hipStream_t s) {
+    if (!n) return;
+    k_fill_f32<<<cdiv(n, 256), 256, 0, s>>>(mind, n, FLT_MAX);
+}
+
+void launch_mindist_update(const float4* v_il, uint64_t n, uint32_t d4, const float* crow, float* mind,
+                           hipStream_t s) {
+    if (!n) return;
+    k_mindist_update<<<cdiv((n + 63) / 64, 4), 256, 0, s>>>(v_il, n, d4, crow, mind);
+}
+
+void launch_serial_prefix(const float* mind, uint64_t n, float* prefix, float* total, hipStream_t s) {
+    k_serial_prefix<<<1, 64, 0, s>>>(mind, n, prefix, total);
+}
+
+void launch_first_geq(const float* prefix, uint64_t n, float target, unsigned long long* out, hipStream_t s) {
+    if (!n) return;
+    k_first_geq<<<cdiv(n, 256), 256, 0, s>>>(prefix, n, target, out);
+}
+
+void launch_copy_row_if(const float* vpad, uint64_t n, uint32_t dp, const unsigned long long* idx, float* dst_row,
+                        hipStream_t s) {
+    k_copy_row_if<<<1, 256, 0, s>>>(vpad, n, dp, idx, dst_row);
+}
+
+void launch_centroid_update(const float* vpad, uint32_t dp, const uint32_t* order, const uint32_t* offsets,
+                            const uint32_t* counts, uint32_t nlist, uint32_t dim, float* cent_rm, hipStream_t s) {
+    dim3 grid(cdiv(dim, 256), nlist);
+    k_centroid_update<<<grid, 256, 0, s>>>(vpad, dp, order, offsets, counts, dim, cent_rm);
+}
+
+void launch_iota(uint32_t* out, uint64_t n, hipStream_t s) {
+    if (!n) return;
+    k_iota<<<cdiv(n, 256), 256, 0, s>>>(out, n);
+}
+
+void launch_slots_from_order(const uint32_t* sorted_keys, uint64_t n, const uint64_t* group_start,
+                             const uint64_t* base_slot, uint64_t* dest, hipStream_t s) {
+    if (!n) return;
+    k_slots_from_order<<<cdiv(n, 256), 256, 0, s>>>(sorted_keys, n, group_start, base_slot, dest);
+}
+
+void launch_gen_normal(float* out, uint64_t n, uint64_t seed, uint64_t offset, hipStream_t s) {
+    if (!n) return;
+    k_gen_normal<<<cdiv(n, 256), 256, 0, s>>>(out, n, seed, offset);
+}
+
+hipError_t radix_sort_pairs(void* temp, size_t& temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                            const uint32_t* vals_in, uint32_t* vals_out, uint64_t n, int end_bit, hipStream_t s) {
+    return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (int)n, 0,
+                                              end_bit, s);
+}
+
+}  // namespace vdbk

@@ -1,0 +1,101 @@
+// kernels.hpp — launchers for the gfx950 IVF-Flat kernels (kernels.hip).
+//
+// HBM layouts (DESIGN.md "Data layout"):
+//   * list arena: vectors in blocks of 64, each block [D4][64 lanes][float4]
+//     (D4 = ceil(dim/4), zero-padded dims), so one wave-instruction reads 1 KiB
+//     contiguous; ids [block*64 + lane] uint64.
+//   * centroids: the same interleaved layout (coarse step), plus a zero-padded
+//     row-major copy [nlist][Dp] (training).
+//   * queries: zero-padded row-major [B][Dp], Dp = 4*D4. Zero pads add +0.0f to
+//     sums that can never be -0.0f, so distances keep the reference's bits.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vdbk {
+
+constexpr int kSegBlocks = 8;              // 64-vector blocks per scan work item
+constexpr int kSegVectors = kSegBlocks * 64;
+constexpr int kPlanMaxPairs = 8192;        // batch * nprobe per plan launch
+constexpr int kMaxK = 1024;                // top-k capacity (16 registers x 64 lanes)
+
+struct ScanItem {
+    uint32_t list;
+    uint32_t seg;
+    uint32_t pair_start;
+    uint32_t npairs;
+};
+
+// Number of lane registers for a list of capacity k, and the query-group size the
+// scan kernel uses for that register count.
+inline int topk_regs(uint32_t k) {
+    int r = 1;
+    while (r * 64 < (int)k) r <<= 1;
+    return r;
+}
+inline int scan_group(int regs) { return regs == 1 ? 4 : (regs == 2 ? 2 : 1); }
+
+// ---- search ----
+void launch_pad_rows(const float* src, uint64_t n, uint32_t dim, uint32_t dp, float* dst, hipStream_t s);
+void launch_coarse(int metric, const float4* cent_il, uint32_t nlist, uint32_t d4, const float* qpad,
+                   uint32_t B, float* cd, hipStream_t s);
+void launch_select(int regs, const float* cd, uint32_t nlist, uint32_t B, uint32_t P, uint32_t* probes,
+                   hipStream_t s);
+void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint32_t* count_local,
+                 uint32_t B, uint32_t P, uint32_t group, ScanItem* items, uint32_t* counters,
+                 uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp,
+                 uint32_t* nseg_qp, unsigned long long* stats, hipStream_t s);
+void launch_scan(int metric, int regs, uint32_t grid_items, const float4* arena, const uint64_t* ids,
+                 const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
+                 const ScanItem* items, const uint32_t* counters, const uint32_t* sorted_pair,
+                 const uint32_t* part_base_sorted, uint32_t k, float* part_d, uint64_t* part_i,
+                 hipStream_t s);
+void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
+                       const uint32_t* nseg_qp, const uint32_t* part_base_qp, const float* part_d,
+                       const uint64_t* part_i, uint32_t BP, uint32_t k, float* slot_d, uint64_t* slot_i,
+                       hipStream_t s);
+void launch_query_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const float* slot_d,
+                        const uint64_t* slot_i, const float* carry_d, const uint64_t* carry_i,
+                        uint32_t B, uint32_t P, uint32_t k, int stale, float* out_d, uint64_t* out_i,
+                        hipStream_t s);
+void launch_carry(const uint32_t* probes, const uint32_t* count_global, uint32_t B, uint32_t P, uint32_t k,
+                  const float* slot_d, const uint64_t* slot_i, float* carry_d, uint64_t* carry_i,
+                  hipStream_t s);
+void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint32_t nranks, uint32_t n, uint32_t k,
+                       float* out_d, uint64_t* out_i, hipStream_t s);
+void launch_fill_empty(uint64_t n, float* d, uint64_t* i, hipStream_t s);
+
+// ---- build (train / add / layout) ----
+void launch_interleave(const float* rows, uint64_t n, uint32_t dp, float4* blocks, hipStream_t s);
+void launch_scatter_rows(const float* rows, const uint64_t* row_ids, const uint32_t* order, uint64_t n,
+                         uint32_t dp, const uint64_t* dest_slot, float4* arena, uint64_t* arena_ids,
+                         hipStream_t s);
+void launch_copy_lists(const float4* old_arena, const uint64_t* old_ids, const uint64_t* old_off,
+                       const uint64_t* new_off, const uint32_t* nblocks, uint32_t nlist, uint32_t d4,
+                       float4* new_arena, uint64_t* new_ids, hipStream_t s);
+void launch_export_list(const float4* arena, const uint64_t* ids, uint64_t block_off, uint32_t count,
+                        uint32_t dim, uint32_t d4, float* out, uint64_t* out_ids, hipStream_t s);
+void launch_assign(int metric, const float* vpad, uint64_t n, uint32_t dp, const float4* cent_il,
+                   uint32_t nlist, uint32_t* out, hipStream_t s);
+void launch_histogram(const uint32_t* keys, uint64_t n, uint32_t* counts, hipStream_t s);
+void launch_mindist_init(float* mind, uint64_t n, hipStream_t s);
+void launch_mindist_update(const float4* v_il, uint64_t n, uint32_t d4, const float* centroid_row,
+                           float* mind, hipStream_t s);
+void launch_serial_prefix(const float* mind, uint64_t n, float* prefix, float* total, hipStream_t s);
+void launch_first_geq(const float* prefix, uint64_t n, float target, unsigned long long* out, hipStream_t s);
+void launch_copy_row_if(const float* vpad, uint64_t n, uint32_t dp, const unsigned long long* idx,
+                        float* dst_row, hipStream_t s);
+void launch_centroid_update(const float* vpad, uint32_t dp, const uint32_t* order, const uint32_t* offsets,
+                            const uint32_t* counts, uint32_t nlist, uint32_t dim, float* cent_rm,
+                            hipStream_t s);
+void launch_iota(uint32_t* out, uint64_t n, hipStream_t s);
+void launch_slots_from_order(const uint32_t* sorted_keys, uint64_t n, const uint64_t* group_start,
+                             const uint64_t* list_base_slot, uint64_t* dest_slot, hipStream_t s);
+void launch_gen_normal(float* out, uint64_t n, uint64_t seed, uint64_t offset, hipStream_t s);
+
+// Stable key/value radix sort (hipCUB). temp == nullptr queries temp_bytes.
+hipError_t radix_sort_pairs(void* temp, size_t& temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                            const uint32_t* vals_in, uint32_t* vals_out, uint64_t n, int end_bit,
+                            hipStream_t s);
+
+}  // namespace vdbk

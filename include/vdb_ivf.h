@@ -1,0 +1,148 @@
+/*
+ * vdb_ivf.h — C ABI of the MI355X-native IVF-Flat engine (libvdb_ivf.so).
+ *
+ * This is the drop-in boundary for the reference's search path. Each entry point
+ * names the reference interface it replaces (paths relative to the reference
+ * repository, wedevxer/CUDA-AcceleratedVectorDatabaseEngine):
+ *
+ *   vdb_ivf_create        IVFFlatIndex::IVFFlatIndex(const Config&, TransferManager*)   engine/ivf_flat_index.h:44, .cpp:13-33
+ *   vdb_ivf_destroy       IVFFlatIndex::~IVFFlatIndex()                                 engine/ivf_flat_index.h:45, .cpp:36-46
+ *   vdb_ivf_train         IVFFlatIndex::train(const float*, uint64_t)                   engine/ivf_flat_index.h:47, .cpp:49-145
+ *   vdb_ivf_add           IVFFlatIndex::add(const float*, const uint64_t*, uint64_t)    engine/ivf_flat_index.h:49, .cpp:148-202
+ *   vdb_ivf_search        IVFFlatIndex::search(const float*, uint32_t, const SearchParams&, float*, uint64_t*)
+ *                                                                                       engine/ivf_flat_index.h:51-53, .cpp:205-256
+ *   vdb_ivf_warmup        IVFFlatIndex::warmup_lists(const std::vector<uint32_t>&)      engine/ivf_flat_index.h:60
+ *   vdb_ivf_evict         IVFFlatIndex::evict_list(uint32_t)                            engine/ivf_flat_index.h:61
+ *   vdb_ivf_gpu_bytes     IVFFlatIndex::get_gpu_memory_usage()                          engine/ivf_flat_index.h:63, .cpp:707-709
+ *   vdb_ivf_ntotal        IVFFlatIndex::get_total_vectors()                             engine/ivf_flat_index.h:64
+ *
+ * The remaining entry points have no single reference counterpart; they expose the
+ * device-resident and multi-GPU forms of the same path (the reference searches one
+ * query and one list at a time on device 0, ivf_flat_index.cpp:214-255).
+ *
+ * Conventions: every call returns 0 on success and a negative code on failure;
+ * vdb_last_error() then describes the failure (thread-local). Host buffers are
+ * caller-owned and row-major (queries n x dim fp32; outputs n x k). Metric
+ * ordinals follow kernels::Metric (engine/kernels.cuh:24-28): L2 = 0 (squared
+ * L2), InnerProduct = 1 (negated dot), Cosine = 2 (the reference CPU path leaves
+ * its distance at 0.0f, ivf_flat_index.cpp:351-362; mirrored exactly).
+ * Unfilled result slots are (FLT_MAX, UINT64_MAX) as in ivf_flat_index.cpp:513-517.
+ * Results are bit-identical to the reference CPU path (ids and distance bits).
+ * No torch or HIP types appear in these signatures; streams are passed as void*.
+ */
+#ifndef VDB_IVF_H
+#define VDB_IVF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    VDB_OK = 0,
+    VDB_ERR_INVALID_ARGUMENT = -1,
+    VDB_ERR_DEVICE = -2,
+    VDB_ERR_OUT_OF_MEMORY = -3,
+    VDB_ERR_UNSUPPORTED = -4,
+    VDB_ERR_STATE = -5
+};
+
+enum { VDB_METRIC_L2 = 0, VDB_METRIC_INNER_PRODUCT = 1, VDB_METRIC_COSINE = 2 };
+
+typedef struct vdb_ivf vdb_ivf;
+
+/* Mirrors IVFFlatIndex::Config (engine/ivf_flat_index.h:16-22) plus the device. */
+typedef struct vdb_ivf_config {
+    uint32_t dimension;
+    uint32_t nlist;
+    int32_t metric;
+    int32_t use_gpu;          /* accepted for API parity; the engine always runs on the GPU */
+    uint64_t max_gpu_memory;  /* 0 = no cap. The whole index stays HBM-resident (288 GB/GPU). */
+    int32_t device;           /* HIP device ordinal */
+} vdb_ivf_config;
+
+/* Per-handle measurement, filled by vdb_ivf_profile_read (see DESIGN.md "Measurement"). */
+typedef struct vdb_ivf_profile {
+    uint64_t batches;          /* search batches executed since the last reset */
+    uint64_t scan_launches;    /* ivf_scan kernel launches */
+    double scan_ms;            /* summed ivf_scan durations (HIP events on the search stream) */
+    double coarse_ms;          /* summed coarse-quantiser durations (distance + select) */
+    double total_ms;           /* summed per-batch durations (first to last kernel) */
+    uint64_t scan_vectors;     /* sum over batches of sum_{distinct probed local lists} n_l */
+    uint64_t distinct_lists;   /* sum over batches of distinct probed local lists */
+    uint64_t work_items;       /* sum over batches of scan work items */
+    uint64_t scan_bytes;       /* algorithmic bytes read by ivf_scan: 4 * dim * scan_vectors */
+} vdb_ivf_profile;
+
+const char* vdb_last_error(void);
+const char* vdb_version(void);
+int vdb_device_count(int* count);
+
+int vdb_ivf_create(const vdb_ivf_config* config, vdb_ivf** out);
+int vdb_ivf_destroy(vdb_ivf* index);
+
+/* Training (k-means++ seeded with mt19937(42), then 10 Lloyd iterations), exactly
+ * the reference algorithm; distances run on the GPU. */
+int vdb_ivf_train(vdb_ivf* index, const float* vectors, uint64_t n);
+int vdb_ivf_train_device(vdb_ivf* index, const float* d_vectors, uint64_t n);
+int vdb_ivf_set_centroids(vdb_ivf* index, const float* centroids);  /* nlist x dim, host */
+int vdb_ivf_get_centroids(vdb_ivf* index, float* centroids);        /* nlist x dim, host */
+
+/* add: exact nearest-centroid assignment, lists appended in input order. */
+int vdb_ivf_add(vdb_ivf* index, const float* vectors, const uint64_t* ids, uint64_t n);
+int vdb_ivf_add_device(vdb_ivf* index, const float* d_vectors, const uint64_t* d_ids, uint64_t n);
+
+/* search: host buffers in and out (PCIe included). nprobe is clamped to nlist. */
+int vdb_ivf_search(vdb_ivf* index, const float* queries, uint32_t n, uint32_t nprobe, uint32_t k,
+                   float* distances, uint64_t* ids);
+/* search on device buffers, enqueued on `stream` (NULL = the handle's stream),
+ * asynchronous. When a shard is set (vdb_ivf_set_shard with world > 1) the outputs
+ * are this rank's partial results, to be combined with vdb_merge_ranks_device. */
+int vdb_ivf_search_device(vdb_ivf* index, const float* d_queries, uint32_t n, uint32_t nprobe,
+                          uint32_t k, float* d_distances, uint64_t* d_ids, void* stream);
+
+/* Multi-GPU: restrict this handle to the lists rank `rank` owns out of `world`
+ * (size-balanced LPT over list lengths, identical on every rank), and free the
+ * rest of the list arena. Emptiness of non-owned lists is still tracked. */
+int vdb_ivf_set_shard(vdb_ivf* index, uint32_t rank, uint32_t world);
+/* Combine per-rank partials gathered as [nranks][n][k] into final [n][k]. */
+int vdb_merge_ranks_device(const float* d_dist, const uint64_t* d_ids, uint32_t nranks, uint32_t n,
+                           uint32_t k, float* d_out_dist, uint64_t* d_out_ids, void* stream);
+/* Host-only: the LPT owner of every list for `world` ranks (no GPU needed). */
+int vdb_shard_plan(const uint64_t* list_sizes, uint32_t nlist, uint32_t world, uint32_t* owner);
+
+/* List residency (the whole index is HBM-resident; these keep the API). */
+int vdb_ivf_warmup(vdb_ivf* index, const uint32_t* lists, uint32_t n);
+int vdb_ivf_evict(vdb_ivf* index, uint32_t list);
+
+uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* index);
+uint64_t vdb_ivf_ntotal(const vdb_ivf* index);
+int vdb_ivf_list_sizes(const vdb_ivf* index, uint64_t* sizes);  /* nlist entries */
+/* Copy list `list` out row-major (count x dim) with its ids, in add order. */
+int vdb_ivf_get_list(vdb_ivf* index, uint32_t list, float* vectors, uint64_t* ids);
+
+/* Queries per internal batch (default 256; bounded so batch * nprobe <= 8192). */
+int vdb_ivf_set_batch(vdb_ivf* index, uint32_t batch);
+/* Reference quirk A1: an empty probed list leaves the previous query's
+ * slot content in the merge. 1 (default) reproduces it; 0 drops empty slots. */
+int vdb_ivf_set_stale_slots(vdb_ivf* index, int enable);
+
+int vdb_ivf_profile_enable(vdb_ivf* index, int enable);
+int vdb_ivf_profile_reset(vdb_ivf* index);
+int vdb_ivf_profile_read(vdb_ivf* index, vdb_ivf_profile* out);  /* synchronises the stream */
+
+/* Wait for all work the handle enqueued on its own stream. */
+int vdb_ivf_synchronize(vdb_ivf* index);
+/* The handle's stream (hipStream_t as void*). */
+void* vdb_ivf_stream(vdb_ivf* index);
+
+/* Deterministic N(0,1) fp32 generator on the device (synthetic benchmark data):
+ * element e of the stream (seed, offset + i) is written to d_out[i]. */
+int vdb_gen_normal_device(float* d_out, uint64_t n, uint64_t seed, uint64_t offset, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VDB_IVF_H */

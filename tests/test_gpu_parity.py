@@ -1,0 +1,254 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle.
+
+Bar: ids bit-exact and distance BITS equal to the reference CPU
+path's restatement (oracle/cpu_ref.cpp) on the same inputs. Configurations follow
+the reference's own tests: simple_test.cpp:111-165 (D=64, nlist=16, N=1000, Q=10,
+train 100, nprobe=4, k=5) and the ctest args of gpu_vs_cpu_test
+(test/CMakeLists.txt:56: N=10000, Q=100, D=64, nlist=32, nprobe=8, k=10).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import load_vdb
+
+vdb = load_vdb()
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def assert_same(D, I, Dr, Ir):
+    assert I.shape == Ir.shape
+    bad = np.argwhere(I != Ir)
+    assert bad.size == 0, f"ids differ at {bad[:5].tolist()}: gpu {I[tuple(bad[0])]} ref {Ir[tuple(bad[0])]}"
+    badd = np.argwhere(bits(D) != bits(Dr))
+    assert badd.size == 0, f"dist bits differ at {badd[:5].tolist()}: gpu {D[tuple(badd[0])]!r} ref {Dr[tuple(badd[0])]!r}"
+
+
+def build_pair(X, ids, dim, nlist, metric=0, train=None):
+    """Train+add on both the GPU engine and the oracle; returns (gpu, oracle)."""
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, vdb.Metric(metric)))
+    o = oracle.OracleIndex(dim, nlist, metric)
+    T = X if train is None else train
+    g.train(T)
+    o.train(T)
+    g.add(X, ids)
+    o.add(X, ids)
+    return g, o
+
+
+def mirror_from_oracle(o, dim, nlist, metric=0):
+    """GPU index with the oracle's centroids and the same add() input order."""
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, vdb.Metric(metric)))
+    g.centroids = o.centroids
+    return g
+
+
+def test_simple_test_config():
+    # simple_test.cpp:111-165: mt19937(42) database then queries.
+    flat = oracle.gen_normal(42, (1000 + 10) * 64)
+    X, Q = flat[:64000].reshape(1000, 64), flat[64000:].reshape(10, 64)
+    ids = np.arange(1000, dtype=np.uint64)
+    g, o = build_pair(X, ids, 64, 16, train=X[:100])
+    assert np.array_equal(bits(g.centroids), bits(o.centroids)), "train() centroids differ"
+    for l in range(16):
+        gv, gi = g.get_list(l)
+        ov, oi = o.get_list(l)
+        assert np.array_equal(gi, oi), f"list {l} membership/order differs"
+        assert np.array_equal(bits(gv), bits(ov))
+    D, I = g.search(Q, nprobe=4, k=5)
+    Dr, Ir = o.search(Q, 4, 5)
+    assert_same(D, I, Dr, Ir)
+    # validity rules of simple_test.cpp:186 / gpu_vs_cpu_test.cpp:209-219
+    assert np.all((I < 1000) | (I == np.iinfo(np.uint64).max))
+    assert g.get_total_vectors() == 1000
+
+
+def test_gpu_vs_cpu_ctest_config():
+    X, Q, ids = oracle.reference_test_data(10000, 100, 64)
+    g, o = build_pair(X, ids, 64, 32)
+    assert np.array_equal(bits(g.centroids), bits(o.centroids))
+    D, I = g.search(Q, nprobe=8, k=10)
+    Dr, Ir = o.search(Q, 8, 10)
+    assert_same(D, I, Dr, Ir)
+    assert np.all(np.isfinite(D)) and np.all(D >= 0)
+
+
+@pytest.mark.parametrize("metric", [0, 1, 2])
+def test_metrics_given_centroids(metric):
+    X, Q, ids = oracle.reference_test_data(6000, 50, 32, seed=7)
+    o = oracle.OracleIndex(32, 24, metric)
+    o.centroids = X[::250][:24]
+    o.add(X, ids)
+    g = mirror_from_oracle(o, 32, 24, metric)
+    g.add(X, ids)
+    for l in range(24):
+        assert np.array_equal(g.get_list(l)[1], o.get_list(l)[1]), f"assignment differs for list {l}"
+    D, I = g.search(Q, nprobe=5, k=10)
+    Dr, Ir = o.search(Q, 5, 10)
+    assert_same(D, I, Dr, Ir)
+
+
+def test_train_inner_product():
+    X, Q, ids = oracle.reference_test_data(3000, 20, 16, seed=3)
+    g, o = build_pair(X, ids, 16, 12, metric=1)
+    assert np.array_equal(bits(g.centroids), bits(o.centroids))
+    assert_same(*g.search(Q, nprobe=3, k=7), *o.search(Q, 3, 7))
+
+
+@pytest.mark.parametrize("dim", [1, 3, 67, 130])
+def test_odd_dimensions(dim):
+    X, Q, ids = oracle.reference_test_data(2500, 30, dim, seed=dim)
+    g, o = build_pair(X, ids, dim, 10, train=X[:500])
+    assert np.array_equal(bits(g.centroids), bits(o.centroids))
+    assert_same(*g.search(Q, nprobe=3, k=10), *o.search(Q, 3, 10))
+
+
+@pytest.mark.parametrize("k", [1, 64, 65, 100, 1000])
+def test_k_range(k):
+    X, Q, ids = oracle.reference_test_data(5000, 20, 24, seed=11)
+    o = oracle.OracleIndex(24, 8, 0)
+    o.centroids = X[:8]
+    o.add(X, ids)
+    g = mirror_from_oracle(o, 24, 8)
+    g.add(X, ids)
+    assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))
+
+
+def test_bruteforce_nprobe_equals_nlist():
+    X, Q, ids = oracle.reference_test_data(4000, 25, 20, seed=5)
+    o = oracle.OracleIndex(20, 128, 0)
+    o.centroids = X[:128]
+    o.add(X, ids)
+    g = mirror_from_oracle(o, 20, 128)
+    g.add(X, ids)
+    D, I = g.search(Q, nprobe=128, k=10)
+    assert_same(D, I, *o.search(Q, 128, 10))
+    # nprobe = nlist is exact brute force under (dist, id) order
+    import oracle.np_ref as npr
+    full = npr.distances(0, Q, X)
+    for q in range(Q.shape[0]):
+        order = np.lexsort((ids, full[q]))[:10]
+        assert np.array_equal(I[q], ids[order])
+
+
+def test_nprobe_above_nlist_clamps():
+    X, Q, ids = oracle.reference_test_data(2000, 10, 8, seed=9)
+    o = oracle.OracleIndex(8, 6, 0)
+    o.centroids = X[:6]
+    o.add(X, ids)
+    g = mirror_from_oracle(o, 8, 6)
+    g.add(X, ids)
+    assert_same(*g.search(Q, nprobe=50, k=5), *o.search(Q, 50, 5))
+
+
+def test_empty_lists_stale_slots():
+    """Reference quirk A1: an empty probed list leaves the previous query's slot."""
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((3000, 16)).astype(np.float32)
+    Q = rng.standard_normal((300, 16)).astype(np.float32)
+    ids = np.arange(3000, dtype=np.uint64)
+    C = np.concatenate([X[:10], 6.0 + rng.standard_normal((6, 16)).astype(np.float32) * 0.1])
+    C[10:] *= np.where(rng.random((6, 1)) < 0.5, -1, 1).astype(np.float32)
+    o = oracle.OracleIndex(16, 16, 0)
+    o.centroids = C
+    o.add(X, ids)
+    assert any(o.list_count(l) == 0 for l in range(16)), "fixture must contain empty lists"
+    g = mirror_from_oracle(o, 16, 16)
+    g.add(X, ids)
+    for batch in (7, 64, 256):          # carry across internal batches of one call
+        g.set_batch(batch)
+        assert_same(*g.search(Q, nprobe=12, k=8), *o.search(Q, 12, 8))
+    # with stale slots disabled, empty lists contribute nothing: compare with numpy
+    # restatement after dropping the stale behaviour isn't defined by the reference,
+    # so only check validity here.
+    g.set_stale_slots(False)
+    D, I = g.search(Q, nprobe=12, k=8)
+    assert np.all(np.diff(D, axis=1) >= 0)
+
+
+def test_duplicate_ids_and_vectors():
+    rng = np.random.default_rng(1)
+    base = rng.standard_normal((500, 12)).astype(np.float32)
+    X = np.concatenate([base, base[:200], base[100:300]])            # exact duplicate vectors
+    ids = np.concatenate([np.arange(500), np.arange(200), np.arange(1000, 1200)]).astype(np.uint64)  # dup ids
+    Q = np.concatenate([base[:20], rng.standard_normal((20, 12)).astype(np.float32)])
+    o = oracle.OracleIndex(12, 5, 0)
+    o.centroids = base[:5]
+    o.add(X, ids)
+    g = mirror_from_oracle(o, 12, 5)
+    g.add(X, ids)
+    for k in (1, 5, 30):
+        assert_same(*g.search(Q, nprobe=2, k=k), *o.search(Q, 2, k))
+
+
+def test_incremental_add():
+    X, Q, ids = oracle.reference_test_data(3000, 20, 16, seed=21)
+    o = oracle.OracleIndex(16, 10, 0)
+    o.centroids = X[:10]
+    g = mirror_from_oracle(o, 16, 10)
+    for a, b in ((0, 1000), (1000, 1001), (1001, 3000)):
+        o.add(X[a:b], ids[a:b])
+        g.add(X[a:b], ids[a:b])
+    for l in range(10):
+        assert np.array_equal(g.get_list(l)[1], o.get_list(l)[1])
+    assert_same(*g.search(Q, nprobe=4, k=10), *o.search(Q, 4, 10))
+
+
+def test_benchmark_kat_self_query():
+    """bench/benchmark.cpp:130-138 re-seeds mt19937(42) for queries, so query i == vector i:
+    the top-1 must be (i, 0.0f) for every i < N (known answer)."""
+    n, d = 1000, 64
+    X = oracle.gen_normal(42, n * d).reshape(n, d)
+    Q = oracle.gen_normal(42, 50 * d).reshape(50, d)
+    ids = np.arange(n, dtype=np.uint64)
+    g, o = build_pair(X, ids, d, 32)
+    D, I = g.search(Q, nprobe=5, k=10)
+    assert np.array_equal(I[:, 0], np.arange(50, dtype=np.uint64))
+    assert np.all(bits(D[:, 0]) == 0)
+    assert_same(D, I, *o.search(Q, 5, 10))
+
+
+def test_empty_index_and_degenerate_calls():
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(8, 4))
+    Q = np.ones((3, 8), np.float32)
+    D, I = g.search(Q, nprobe=2, k=4)
+    assert np.all(I == np.iinfo(np.uint64).max) and np.all(D == np.finfo(np.float32).max)
+    D, I = g.search(Q, nprobe=0, k=4)
+    assert np.all(I == np.iinfo(np.uint64).max)
+    D, I = g.search(np.zeros((0, 8), np.float32), nprobe=2, k=4)
+    assert D.shape == (0, 4)
+    with pytest.raises(ValueError):
+        vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(0, 4))
+
+
+def test_two_shards_merge_equals_single():
+    import torch
+    X, Q, ids = oracle.reference_test_data(8000, 40, 32, seed=4)
+    o = oracle.OracleIndex(32, 20, 0)
+    o.centroids = X[:20]
+    o.add(X, ids)
+    Dr, Ir = o.search(Q, 6, 10)
+    parts_d, parts_i = [], []
+    for r in range(2):
+        g = mirror_from_oracle(o, 32, 20)
+        g.add(X, ids)
+        g.set_shard(r, 2)
+        D, I = g.search(Q, nprobe=6, k=10)
+        parts_d.append(D)
+        parts_i.append(I)
+        owner = vdb.shard_plan(g.list_sizes(), 2)
+        Do, Io = o.search_shard(Q, 6, 10, (owner == r).astype(np.uint8))
+        assert_same(D, I, Do, Io)
+    dev = torch.device("cuda:0")
+    pd = torch.from_numpy(np.stack(parts_d)).to(dev)
+    pi = torch.from_numpy(np.stack(parts_i).view(np.int64)).to(dev)
+    od = torch.empty((40, 10), dtype=torch.float32, device=dev)
+    oi = torch.empty((40, 10), dtype=torch.int64, device=dev)
+    vdb.merge_ranks_device(pd.data_ptr(), pi.data_ptr(), 2, 40, 10, od.data_ptr(), oi.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), Dr, Ir)
