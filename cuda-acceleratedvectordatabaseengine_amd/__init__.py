@@ -51,7 +51,7 @@ class Profile(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("scan_launches", ctypes.c_uint64), ("scan_ms", ctypes.c_double),
                 ("coarse_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("scan_vectors", ctypes.c_uint64),
                 ("distinct_lists", ctypes.c_uint64), ("work_items", ctypes.c_uint64),
-                ("scan_bytes", ctypes.c_uint64)]
+                ("scan_bytes", ctypes.c_uint64), ("pair_vectors", ctypes.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -279,6 +279,12 @@ class IVFFlatIndex:
         i = np.empty(n, dtype=np.uint64)
         _check(lib().vdb_ivf_get_list(self._h, list_id, _ptr(v), _ptr(i)))
         return v, i
+
+    def get_list_into(self, list_id: int, vectors: np.ndarray, ids: np.ndarray):
+        """Copy list `list_id` into caller arrays (C-contiguous, sized count x dim / count)."""
+        assert vectors.flags.c_contiguous and ids.flags.c_contiguous
+        assert vectors.dtype == np.float32 and ids.dtype == np.uint64
+        _check(lib().vdb_ivf_get_list(self._h, list_id, _ptr(vectors), _ptr(ids)))
 
     def set_batch(self, batch: int):
         _check(lib().vdb_ivf_set_batch(self._h, batch))

@@ -124,12 +124,16 @@ struct vdb_ivf {
     uint32_t rank = 0, world = 1;
     uint32_t batch = 256;
     int stale = 1;
+    bool wide_scan = true;
 
     // search workspace
     DevBuf<float> qpad, cd, part_d, slot_d, carry_d, out_d, qin;
     DevBuf<uint64_t> part_i, slot_i, carry_i, out_i;
-    DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters;
-    DevBuf<vdbk::ScanItem> items;
+    DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters, l1base;
+    DevBuf<uint2> l1_items;
+    DevBuf<float> l1_d;
+    DevBuf<uint64_t> l1_i;
+    DevBuf<vdbk::ScanItem> items, items_w;
     DevBuf<unsigned long long> stats;
 
     bool prof = false;
@@ -367,9 +371,11 @@ struct vdb_ivf {
     void ensure_workspace(uint32_t B, uint32_t P, uint32_t k, hipStream_t s) {
         const size_t BP = (size_t)B * P;
         const size_t max_items = (size_t)B * nseg_prefix[P];
-        const bool grow = qpad.cap < (size_t)B * dp || cd.cap < (size_t)B * nlist || probes.cap < BP ||
+        const size_t max_l1 = max_items / vdbk::kMergeFan + BP;
+        const size_t max_wide = max_items / 4 + (size_t)BP * 8 + 8;
+        const bool grow = items_w.cap < max_wide || qpad.cap < (size_t)B * dp || cd.cap < (size_t)B * nlist || probes.cap < BP ||
                           items.cap < max_items || part_d.cap < max_items * k || slot_d.cap < BP * k ||
-                          carry_d.cap < (size_t)P * k;
+                          carry_d.cap < (size_t)P * k || l1_items.cap < max_l1 || l1_d.cap < max_l1 * k;
         if (!grow) return;
         HIPCHECK(hipStreamSynchronize(s));
         HIPCHECK(hipStreamSynchronize(stream));
@@ -380,8 +386,13 @@ struct vdb_ivf {
         pbqp.ensure(BP);
         sorted_pair.ensure(BP);
         pbs.ensure(BP);
-        counters.ensure(2);
+        counters.ensure(4);
+        l1base.ensure(BP);
+        l1_items.ensure(max_l1);
+        l1_d.ensure(max_l1 * k);
+        l1_i.ensure(max_l1 * k);
         items.ensure(max_items);
+        items_w.ensure(max_wide);
         part_d.ensure(max_items * k);
         part_i.ensure(max_items * k);
         slot_d.ensure(BP * k);
@@ -402,21 +413,26 @@ struct vdb_ivf {
         EventSet* ev = prof ? &next_events() : nullptr;
         if (ev) HIPCHECK(hipEventRecord(ev->begin, s));
 
-        vdbk::launch_pad_rows(d_q, B, dim, dp, qpad.ensure((size_t)B * dp), s);
-        vdbk::launch_coarse(metric, cent_il.p, nlist, d4, qpad.p, B, cd.ensure((size_t)B * nlist), s);
-        vdbk::launch_select(regs_p, cd.p, nlist, B, P, probes.ensure(BP), s);
+        vdbk::launch_pad_rows(d_q, B, dim, dp, qpad.p, s);
+        vdbk::launch_coarse(metric, cent_il.p, nlist, d4, qpad.p, B, cd.p, s);
+        vdbk::launch_select(regs_p, cd.p, nlist, B, P, probes.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
-        vdbk::launch_plan(probes.p, d_nseg.p, d_count_local.p, B, P, group, items.ensure(max_items),
-                          counters.ensure(2), sorted_pair.ensure(BP), pbs.ensure(BP), pbqp.ensure(BP),
-                          nseg_qp.ensure(BP), stats.ensure(4), s);
-        part_d.ensure(max_items * k);
-        part_i.ensure(max_items * k);
+        const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
+        const uint64_t max_wide = max_items / 4 + (uint64_t)BP * 8 + 8;
+        const bool wide = regs_k == 1 && wide_scan;
+        vdbk::launch_plan(probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? 1 : 0, items.p, items_w.p,
+                          counters.p, sorted_pair.p, pbs.p, pbqp.p, nseg_qp.p, l1base.p, l1_items.p, stats.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
+        if (wide)
+            vdbk::launch_scan_wide(metric, (uint32_t)max_wide, arena.p, arena_ids.p, d_block_off.p, d_count_local.p,
+                                   qpad.p, d4, items_w.p, counters.p, sorted_pair.p, pbs.p, k, part_d.p, part_i.p, s);
         vdbk::launch_scan(metric, regs_k, (uint32_t)max_items, arena.p, arena_ids.p, d_block_off.p, d_count_local.p,
                           qpad.p, d4, items.p, counters.p, sorted_pair.p, pbs.p, k, part_d.p, part_i.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_end, s));
-        vdbk::launch_slot_merge(regs_k, probes.p, d_count_global.p, nseg_qp.p, pbqp.p, part_d.p, part_i.p, BP, k,
-                                slot_d.ensure((size_t)BP * k), slot_i.ensure((size_t)BP * k), s);
+        vdbk::launch_merge_partials(regs_k, (uint32_t)max_l1, probes.p, d_count_global.p, nseg_qp.p, pbqp.p, l1base.p,
+                                    l1_items.p, counters.p, part_d.p, part_i.p, k, l1_d.p, l1_i.p, s);
+        vdbk::launch_slot_merge(regs_k, probes.p, d_count_global.p, nseg_qp.p, pbqp.p, l1base.p, part_d.p, part_i.p,
+                                l1_d.p, l1_i.p, BP, k, slot_d.p, slot_i.p, s);
         vdbk::launch_query_merge(regs_k, probes.p, d_count_global.p, slot_d.p, slot_i.p, carry_d.p, carry_i.p, B, P, k,
                                  stale, out_d_, out_i_, s);
         if (stale) vdbk::launch_carry(probes.p, d_count_global.p, B, P, k, slot_d.p, slot_i.p, carry_d.p, carry_i.p, s);
@@ -436,8 +452,8 @@ struct vdb_ivf {
         }
         require(P <= (uint32_t)vdbk::kMaxK, "nprobe above 1024 is not supported", VDB_ERR_UNSUPPORTED);
         if (!stats.p) {
-            stats.ensure(4);
-            HIPCHECK(hipMemsetAsync(stats.p, 0, 32, s));
+            stats.ensure(8);
+            HIPCHECK(hipMemsetAsync(stats.p, 0, 64, s));
         }
         const uint32_t bmax = std::max<uint32_t>(1, std::min<uint32_t>(batch, vdbk::kPlanMaxPairs / P));
         ensure_workspace(std::min(bmax, n), P, k, s);
@@ -722,7 +738,7 @@ int vdb_ivf_profile_reset(vdb_ivf* h) {
         h->set_device();
         HIPCHECK(hipDeviceSynchronize());
         h->events_used = 0;
-        HIPCHECK(hipMemsetAsync(h->stats.ensure(4), 0, 32, h->stream));
+        HIPCHECK(hipMemsetAsync(h->stats.ensure(8), 0, 64, h->stream));
         HIPCHECK(hipStreamSynchronize(h->stream));
     });
 }
@@ -745,13 +761,14 @@ int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
             p.total_ms += c;
             p.scan_launches++;
         }
-        unsigned long long st[4] = {0, 0, 0, 0};
-        if (h->stats.p) HIPCHECK(hipMemcpy(st, h->stats.p, 32, hipMemcpyDeviceToHost));
+        unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (h->stats.p) HIPCHECK(hipMemcpy(st, h->stats.p, 64, hipMemcpyDeviceToHost));
         p.distinct_lists = st[0];
         p.scan_vectors = st[1];
         p.work_items = st[2];
         p.batches = st[3];
         p.scan_bytes = st[1] * (uint64_t)h->dim * 4;
+        p.pair_vectors = st[4];
         *out = p;
     });
 }

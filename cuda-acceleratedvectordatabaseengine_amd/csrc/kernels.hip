@@ -16,6 +16,10 @@
 #include "kernels.hpp"
 #include "wave_topk.hpp"
 
+#ifndef VDB_NARROW_CHUNK
+#define VDB_NARROW_CHUNK 4
+#endif
+
 namespace vdbk {
 
 enum { kL2 = 0, kIP = 1, kCos = 2 };
@@ -50,16 +54,21 @@ __device__ __forceinline__ uint32_t wave_index() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
+// Grid-stride helpers. An HSA dispatch packet holds the grid size in work-items as
+// 32 bits, so every element-wise launch caps its grid (launch_grid) and strides.
+__device__ __forceinline__ uint64_t gtid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ uint64_t gstride() { return (uint64_t)gridDim.x * blockDim.x; }
+
 // ============================================================================
 // Query padding: [n][dim] -> [n][dp] with +0.0f pads.
 // ============================================================================
-__global__ void k_pad_rows(const float* __restrict__ src, uint64_t n, uint32_t dim, uint32_t dp,
+__global__ void ivf_pad_queries(const float* __restrict__ src, uint64_t n, uint32_t dim, uint32_t dp,
                            float* __restrict__ dst) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n * dp) return;
-    const uint64_t r = e / dp;
-    const uint32_t c = (uint32_t)(e - r * dp);
-    dst[e] = c < dim ? src[r * dim + c] : 0.0f;
+    for (uint64_t e = gtid(); e < n * dp; e += gstride()) {
+        const uint64_t r = e / dp;
+        const uint32_t c = (uint32_t)(e - r * dp);
+        dst[e] = c < dim ? src[r * dim + c] : 0.0f;
+    }
 }
 
 // ============================================================================
@@ -68,7 +77,7 @@ __global__ void k_pad_rows(const float* __restrict__ src, uint64_t n, uint32_t d
 // 4 queries whose dims are wave-uniform (scalar loads). Exact sequential sums.
 // ============================================================================
 template <int M>
-__global__ __launch_bounds__(256) void k_coarse(const float4* __restrict__ cent, uint32_t nlist, uint32_t d4,
+__global__ __launch_bounds__(256) void ivf_coarse_distances(const float4* __restrict__ cent, uint32_t nlist, uint32_t d4,
                                                 const float* __restrict__ qpad, uint32_t B,
                                                 float* __restrict__ cd) {
     constexpr int G = 4;
@@ -103,7 +112,7 @@ __global__ __launch_bounds__(256) void k_coarse(const float4* __restrict__ cent,
 // (dist, list_id) — partial_sort on std::pair (cpp:324-333). One wave per query.
 // ============================================================================
 template <int R>
-__global__ __launch_bounds__(256) void k_select(const float* __restrict__ cd, uint32_t nlist, uint32_t B,
+__global__ __launch_bounds__(256) void ivf_select_probes(const float* __restrict__ cd, uint32_t nlist, uint32_t B,
                                                 uint32_t P, uint32_t* __restrict__ probes) {
     const uint32_t q = blockIdx.x * 4 + wave_index();
     if (q >= B) return;
@@ -164,23 +173,64 @@ __device__ uint32_t plan_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
     return res;
 }
 
-__global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ probes,
-                                               const uint32_t* __restrict__ nseg_local,
-                                               const uint32_t* __restrict__ count_local, uint32_t B,
-                                               uint32_t P, uint32_t NP, uint32_t G, ScanItem* __restrict__ items,
-                                               uint32_t* __restrict__ counters,
-                                               uint32_t* __restrict__ sorted_pair,
-                                               uint32_t* __restrict__ part_base_sorted,
-                                               uint32_t* __restrict__ part_base_qp,
-                                               uint32_t* __restrict__ nseg_qp,
-                                               unsigned long long* __restrict__ stats) {
+// Query groups of one list with m (query, probe) pairs. With wide items enabled
+// (top-k in one register), pairs go in groups of kWideGroup; a trailing group of
+// <= kNarrowMax pairs becomes a narrow item. Otherwise groups of gn pairs.
+struct ListGroups {
+    uint32_t wide, narrow, full;
+};
+__device__ __forceinline__ ListGroups list_groups(uint32_t m, uint32_t gn, bool wide) {
+    ListGroups g;
+    if (wide) {
+        g.full = m / kWideGroup;
+        const uint32_t rem = m % kWideGroup;
+        g.wide = g.full + (rem > (uint32_t)kNarrowMax ? 1u : 0u);
+        g.narrow = (rem > 0 && rem <= (uint32_t)kNarrowMax) ? 1u : 0u;
+    } else {
+        g.full = 0;
+        g.wide = 0;
+        g.narrow = (m + gn - 1) / gn;
+    }
+    return g;
+}
+
+// Wide items per group of a list with ns segments: quads of 4 segments, padded
+// to a multiple of 8 (see the emission loop in ivf_plan_probes).
+__device__ __forceinline__ uint32_t wide_span(uint32_t ns) { return ((ns + 3) / 4 + 7) / 8 * 8; }
+
+// Last index d in [0, n) with base[d] <= x (base non-decreasing, base[0] == 0).
+__device__ __forceinline__ uint32_t find_owner(const uint32_t* base, uint32_t n, uint32_t x) {
+    uint32_t lo = 0, hi = n;  // answer in [lo, hi)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (base[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restrict__ probes,
+                                                        const uint32_t* __restrict__ nseg_local,
+                                                        const uint32_t* __restrict__ count_local, uint32_t B,
+                                                        uint32_t P, uint32_t NP, uint32_t gn, uint32_t wide_on,
+                                                        ScanItem* __restrict__ items_n, ScanItem* __restrict__ items_w,
+                                                        uint32_t* __restrict__ counters,
+                                                        uint32_t* __restrict__ sorted_pair,
+                                                        uint32_t* __restrict__ part_base_sorted,
+                                                        uint32_t* __restrict__ part_base_qp,
+                                                        uint32_t* __restrict__ nseg_qp,
+                                                        uint32_t* __restrict__ l1base_qp,
+                                                        uint2* __restrict__ l1_items,
+                                                        unsigned long long* __restrict__ stats) {
     __shared__ uint32_t keys[kPlanMaxPairs];
     __shared__ uint32_t starts[kPlanMaxPairs + 1];
-    __shared__ uint32_t ibase[kPlanMaxPairs];
+    __shared__ uint32_t base_n[kPlanMaxPairs];
+    __shared__ uint32_t base_w[kPlanMaxPairs];
     __shared__ uint32_t sh[33];
     __shared__ uint32_t s_nvalid;
     const uint32_t tid = threadIdx.x;
     const uint32_t BP = B * P;
+    const bool wide = wide_on != 0;
 
     if (tid == 0) s_nvalid = 0;
     for (uint32_t i = tid; i < NP; i += blockDim.x) {
@@ -221,84 +271,121 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t* __restrict__ prob
     const uint32_t c0 = min(nvalid, tid * per), c1 = min(nvalid, c0 + per);
     auto list_of = [&](uint32_t s) { return keys[s] >> 13; };
     auto is_head = [&](uint32_t s) { return s == 0 || list_of(s - 1) != list_of(s); };
+    auto fan_of = [&](uint32_t ns) { return ns > (uint32_t)kMergeFan ? (ns + kMergeFan - 1) / kMergeFan : 0u; };
 
-    uint32_t hsum = 0, nsum = 0;
+    uint32_t hsum = 0, nsum = 0, fsum = 0;
+    unsigned long long vsum = 0;
     for (uint32_t s = c0; s < c1; ++s) {
         hsum += is_head(s) ? 1u : 0u;
-        nsum += nseg_local[list_of(s)];
+        const uint32_t ns = nseg_local[list_of(s)];
+        nsum += ns;
+        fsum += fan_of(ns);
+        vsum += count_local[list_of(s)];
     }
-    uint32_t nd, nparts;
+    if (vsum) atomicAdd(&stats[4], vsum);
+    uint32_t nd, nparts, nl1;
     const uint32_t dl_base = plan_excl_scan(hsum, sh, nd);
     const uint32_t pb_base = plan_excl_scan(nsum, sh, nparts);
+    const uint32_t fb_base = plan_excl_scan(fsum, sh, nl1);
     {
         int cur = (int)dl_base - 1;
-        uint32_t pb = pb_base;
+        uint32_t pb = pb_base, fb = fb_base;
         for (uint32_t s = c0; s < c1; ++s) {
             const uint32_t l = list_of(s);
             if (is_head(s)) starts[++cur] = s;
             const uint32_t i = keys[s] & 8191u;
+            const uint32_t ns = nseg_local[l];
             sorted_pair[s] = ((i / P) << 16) | (i % P);
             part_base_sorted[s] = pb;
             part_base_qp[i] = pb;
-            pb += nseg_local[l];
+            l1base_qp[i] = fb;
+            const uint32_t nf = fan_of(ns);
+            for (uint32_t j = 0; j < nf; ++j) l1_items[fb + j] = make_uint2(i, j);
+            pb += ns;
+            fb += nf;
         }
     }
     if (tid == 0) starts[nd] = nvalid;
     __syncthreads();
 
-    uint32_t isum = 0;
+    // Item counts per list: narrow = groups x segments, wide = groups x segment quads.
+    uint32_t nsum_n = 0, nsum_w = 0;
     {
         int cur = (int)dl_base - 1;
         for (uint32_t s = c0; s < c1; ++s) {
             if (!is_head(s)) continue;
             ++cur;
-            const uint32_t m = starts[cur + 1] - starts[cur];
-            isum += ((m + G - 1) / G) * nseg_local[list_of(s)];
+            const uint32_t ns = nseg_local[list_of(s)];
+            const ListGroups g = list_groups(starts[cur + 1] - starts[cur], gn, wide);
+            nsum_n += g.narrow * ns;
+            nsum_w += g.wide * wide_span(ns);
         }
     }
-    uint32_t nitems;
-    const uint32_t ib_base = plan_excl_scan(isum, sh, nitems);
+    uint32_t n_narrow, n_wide;
+    const uint32_t bn_base = plan_excl_scan(nsum_n, sh, n_narrow);
+    const uint32_t bw_base = plan_excl_scan(nsum_w, sh, n_wide);
     {
         int cur = (int)dl_base - 1;
-        uint32_t ib = ib_base;
+        uint32_t bn = bn_base, bw = bw_base;
         for (uint32_t s = c0; s < c1; ++s) {
             if (!is_head(s)) continue;
             ++cur;
             const uint32_t l = list_of(s);
-            const uint32_t m = starts[cur + 1] - starts[cur];
-            ibase[cur] = ib;
-            ib += ((m + G - 1) / G) * nseg_local[l];
+            const uint32_t ns = nseg_local[l];
+            const ListGroups g = list_groups(starts[cur + 1] - starts[cur], gn, wide);
+            base_n[cur] = bn;
+            base_w[cur] = bw;
+            bn += g.narrow * ns;
+            bw += g.wide * wide_span(ns);
             atomicAdd(&stats[1], (unsigned long long)count_local[l]);
         }
     }
     __syncthreads();
-    {
-        int cur = (int)dl_base - 1;
-        for (uint32_t s = c0; s < c1; ++s) {
-            if (is_head(s)) ++cur;
-            const uint32_t rank = s - starts[cur];
-            if (rank % G) continue;
-            const uint32_t l = list_of(s);
-            const uint32_t m = starts[cur + 1] - starts[cur];
-            const uint32_t ng = (m + G - 1) / G;
-            const uint32_t gi = rank / G;
-            const uint32_t gs = min(G, m - rank);
-            const uint32_t ns = nseg_local[l];
-            for (uint32_t seg = 0; seg < ns; ++seg) {
-                ScanItem it;
-                it.list = l;
-                it.seg = seg;
-                it.pair_start = s;
-                it.npairs = gs;
-                items[ibase[cur] + seg * ng + gi] = it;
-            }
-        }
+
+    // Emit items in parallel. Narrow items of a list are ordered (segment, group)
+    // and wide ones (segment quad, group): the groups re-reading one stretch of the
+    // list are adjacent, so they run side by side and share L2.
+    for (uint32_t x = tid; x < n_narrow; x += blockDim.x) {
+        const uint32_t dl = find_owner(base_n, nd, x);
+        const uint32_t off = x - base_n[dl];
+        const uint32_t st = starts[dl], m = starts[dl + 1] - st;
+        const uint32_t l = list_of(st);
+        const ListGroups g = list_groups(m, gn, wide);
+        const uint32_t gi = off % g.narrow, seg = off / g.narrow;
+        ScanItem it;
+        it.list = l;
+        it.seg = seg;
+        it.pair_start = st + (wide ? g.full * kWideGroup : gi * gn);
+        it.npairs = wide ? m - g.full * kWideGroup : min(gn, m - gi * gn);
+        items_n[x] = it;
+    }
+    // Wide items: one workgroup each. Within a list, item x -> (r = x % 8,
+    // group = (x / 8) % ng, chunk = x / (8 ng)), quad = chunk * 8 + r: every group
+    // of a quad shares x % 8, i.e. one XCD under round-robin dispatch, so the
+    // group re-reads of those 4 segments hit that XCD's L2 (placement only ever
+    // affects speed). Padding items (quad past the list) exit at once.
+    for (uint32_t x = tid; x < n_wide; x += blockDim.x) {
+        const uint32_t dl = find_owner(base_w, nd, x);
+        const uint32_t off = x - base_w[dl];
+        const uint32_t st = starts[dl], m = starts[dl + 1] - st;
+        const uint32_t l = list_of(st);
+        const ListGroups g = list_groups(m, gn, wide);
+        const uint32_t r = off & 7u, gi = (off >> 3) % g.wide, chunk = (off >> 3) / g.wide;
+        const uint32_t quad = chunk * 8 + r;
+        ScanItem it;
+        it.list = l;
+        it.seg = quad;
+        it.pair_start = st + gi * kWideGroup;
+        it.npairs = quad * 4 < nseg_local[l] ? min((uint32_t)kWideGroup, m - gi * kWideGroup) : 0u;
+        items_w[x] = it;
     }
     if (tid == 0) {
-        counters[0] = nitems;
+        counters[0] = n_narrow;
         counters[1] = nparts;
+        counters[2] = nl1;
+        counters[3] = n_wide;
         atomicAdd(&stats[0], (unsigned long long)nd);
-        atomicAdd(&stats[2], (unsigned long long)nitems);
+        atomicAdd(&stats[2], (unsigned long long)(n_narrow + n_wide));
         atomicAdd(&stats[3], 1ull);
     }
 }
@@ -317,6 +404,7 @@ struct ScanArgs {
     const uint32_t* __restrict__ count;
     const float* __restrict__ qpad;
     const ScanItem* __restrict__ items;
+    const ScanItem* __restrict__ items_w;
     const uint32_t* __restrict__ counters;
     const uint32_t* __restrict__ sorted_pair;
     const uint32_t* __restrict__ part_base_sorted;
@@ -325,6 +413,8 @@ struct ScanArgs {
     uint32_t d4;
     uint32_t k;
 };
+
+constexpr int kNarrowChunk = VDB_NARROW_CHUNK;
 
 template <int R, int G, int M>
 __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) {
@@ -336,14 +426,16 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
     const uint32_t nb = (nv + 63) >> 6;
     const uint32_t d4 = a.d4;
     const int k = (int)a.k;
+    const int np = (int)it.npairs;  // <= G; slots g >= np recompute query np-1 and are dropped
 
     const float4* q[G];
     uint32_t part[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        const uint32_t pr = a.sorted_pair[it.pair_start + g];
+        const int gg = g < np ? g : np - 1;
+        const uint32_t pr = a.sorted_pair[it.pair_start + gg];
         q[g] = (const float4*)(a.qpad + (size_t)(pr >> 16) * d4 * 4);
-        part[g] = a.part_base_sorted[it.pair_start + g] + it.seg;
+        part[g] = a.part_base_sorted[it.pair_start + gg] + it.seg;
     }
     WaveTopK<R> tk[G];
     float kd[G];
@@ -360,11 +452,25 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
         float acc[G];
 #pragma unroll
         for (int g = 0; g < G; ++g) acc[g] = 0.0f;
-#pragma unroll 8
-        for (uint32_t t = 0; t < d4; ++t) {
-            const float4 x = vb[(size_t)t * 64];
+        // Hold kChunkTiles float4 of this lane's vector in registers and sweep every
+        // query of the group over them: one HBM read feeds G distance chains, each
+        // still summed in d order.
+        uint32_t t0 = 0;
+        for (; t0 + kNarrowChunk <= d4; t0 += kNarrowChunk) {
+            float4 x[kNarrowChunk];
 #pragma unroll
-            for (int g = 0; g < G; ++g) acc[g] = acc4<M>(acc[g], q[g][t], x);
+            for (int t = 0; t < kNarrowChunk; ++t) x[t] = vb[(size_t)(t0 + t) * 64];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float4* qg = q[g] + t0;
+#pragma unroll
+                for (int t = 0; t < kNarrowChunk; ++t) acc[g] = acc4<M>(acc[g], qg[t], x[t]);
+            }
+        }
+        for (; t0 < d4; ++t0) {
+            const float4 x = vb[(size_t)t0 * 64];
+#pragma unroll
+            for (int g = 0; g < G; ++g) acc[g] = acc4<M>(acc[g], q[g][t0], x);
         }
         const bool valid = j * 64 + lane < nv;
         bool want[G];
@@ -372,17 +478,19 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             acc[g] = dist_finish<M>(acc[g]);
-            want[g] = valid && acc[g] <= kd[g];
+            want[g] = g < np && valid && acc[g] <= kd[g];
             any |= want[g];
         }
         if (__ballot(any)) {
             const uint64_t vid = valid ? a.ids[(b0 + j) * 64 + lane] : kNoId;
 #pragma unroll
-            for (int g = 0; g < G; ++g) offer_lanes<R>(tk[g], want[g], acc[g], vid, k, kd[g], ki[g]);
+            for (int g = 0; g < G; ++g)
+                if (g < np) offer_lanes<R>(tk[g], want[g], acc[g], vid, k, kd[g], ki[g]);
         }
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
+        if (g >= np) break;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int e = r * 64 + lane;
@@ -395,17 +503,227 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
 }
 
 template <int R, int M>
-__global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
-    constexpr int GMAX = (R == 1) ? 4 : (R == 2 ? 2 : 1);
-    const uint32_t idx = blockIdx.x * 4 + wave_index();
-    if (idx >= a.counters[0]) return;
-    const ScanItem it = a.items[idx];
-    switch (it.npairs) {
-        case 1: scan_item<R, 1, M>(a, it); break;
-        case 2: if constexpr (GMAX >= 2) scan_item<R, 2, M>(a, it); break;
-        case 3: if constexpr (GMAX >= 3) scan_item<R, 3, M>(a, it); break;
-        case 4: if constexpr (GMAX >= 4) scan_item<R, 4, M>(a, it); break;
-        default: break;
+__global__ __launch_bounds__(256) void ivf_scan(ScanArgs a) {
+    constexpr int GMAX = scan_group_max(R);
+    const uint32_t n_items = a.counters[0];
+    for (uint32_t idx = blockIdx.x * 4 + wave_index(); idx < n_items; idx += gridDim.x * 4) {
+        const ScanItem it = a.items[idx];
+        switch (it.npairs) {
+            case 1: scan_item<R, 1, M>(a, it); break;
+            case 2: if constexpr (GMAX >= 2) scan_item<R, 2, M>(a, it); break;
+            case 3: if constexpr (GMAX >= 3) scan_item<R, 3, M>(a, it); break;
+            case 4: if constexpr (GMAX >= 4) scan_item<R, 4, M>(a, it); break;
+            default: break;
+        }
+    }
+}
+
+// ============================================================================
+// ivf_scan_wide: hub lists probed by many queries of the batch. One workgroup =
+// one group of 5..16 (query, probe) pairs of one list x 4 consecutive segments
+// (one per wave). The group's queries are staged once in LDS as interleaved
+// pairs (q[2p][d], q[2p+1][d]) and read by broadcast; each lane keeps 32 dims of
+// its list vector in registers and runs two queries per packed instruction
+// (v_pk_add_f32 / v_pk_mul_f32 round each half exactly like the scalar ops).
+// ============================================================================
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int M>
+__device__ __forceinline__ f2 dist_term2(f2 acc, f2 q, float x) {
+    const f2 xx = {x, x};
+    if constexpr (M == kL2) {
+        const f2 diff = q - xx;
+        return acc + diff * diff;
+    } else if constexpr (M == kIP) {
+        return acc + q * xx;
+    } else {
+        return acc;
+    }
+}
+
+template <int M>
+__device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds);
+
+template <int M>
+__global__ __launch_bounds__(256) void ivf_scan_wide(ScanArgs a) {
+    constexpr int GP = kWideGroup / 2;
+    extern __shared__ __attribute__((aligned(16))) float4 qlds[];  // [GP][d4][2] float4
+    const uint32_t d4 = a.d4;
+    const uint32_t n_items = a.counters[3];
+    for (uint32_t idx = blockIdx.x; idx < n_items; idx += gridDim.x) {
+        const ScanItem it = a.items_w[idx];
+        const int np = (int)it.npairs;
+        if (np == 0) continue;  // XCD-alignment padding (block-uniform)
+        // Stage the group's queries: pair p, tile t -> (qa.x, qb.x, qa.y, qb.y), (qa.z, qb.z, qa.w, qb.w).
+        for (uint32_t e = threadIdx.x; e < GP * d4; e += blockDim.x) {
+            const uint32_t p = e / d4, t = e - p * d4;
+            const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
+            const float4 qa = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + ga] >> 16) * d4 * 4))[t];
+            const float4 qb = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + gb] >> 16) * d4 * 4))[t];
+            qlds[(p * d4 + t) * 2 + 0] = make_float4(qa.x, qb.x, qa.y, qb.y);
+            qlds[(p * d4 + t) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
+        }
+        __syncthreads();
+        scan_wide_wave<M>(a, it, qlds);
+        __syncthreads();  // qlds is restaged by the next item
+    }
+}
+
+template <int M>
+__device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds) {
+    constexpr int G = kWideGroup, GP = kWideGroup / 2;
+    const uint32_t d4 = a.d4;
+    const int np = (int)it.npairs;
+    const int lane = lane_id();
+    const uint32_t count = a.count[it.list];
+    const uint32_t nseg = (count + kSegVectors - 1) / kSegVectors;
+    const uint32_t seg = it.seg * 4 + wave_index();
+    if (seg >= nseg) return;  // this wave idles until the block's next item
+    const uint64_t b0 = a.block_off[it.list] + (uint64_t)seg * kSegBlocks;
+    const uint32_t v0 = seg * kSegVectors;
+    const uint32_t nv = min(count - v0, (uint32_t)kSegVectors);
+    const uint32_t nb = (nv + 63) >> 6;
+    const int k = (int)a.k;
+
+    WaveTopK<1> tk[G];
+    float kd[G];
+    uint64_t ki[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        tk[g].init();
+        kd[g] = __builtin_inff();
+        ki[g] = kNoId;
+    }
+    for (uint32_t j = 0; j < nb; ++j) {
+        const float4* vb = a.arena + (b0 + j) * d4 * 64 + lane;
+        f2 acc[GP];
+#pragma unroll
+        for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
+        uint32_t t0 = 0;
+        for (; t0 + kChunkTiles <= d4; t0 += kChunkTiles) {
+            float4 x[kChunkTiles];
+#pragma unroll
+            for (int t = 0; t < kChunkTiles; ++t) x[t] = vb[(size_t)(t0 + t) * 64];
+#pragma unroll
+            for (int p = 0; p < GP; ++p) {
+                const float4* qp = qlds + ((size_t)p * d4 + t0) * 2;
+#pragma unroll
+                for (int t = 0; t < kChunkTiles; ++t) {
+                    const float4 lo = qp[2 * t], hi = qp[2 * t + 1];
+                    acc[p] = dist_term2<M>(acc[p], f2{lo.x, lo.y}, x[t].x);
+                    acc[p] = dist_term2<M>(acc[p], f2{lo.z, lo.w}, x[t].y);
+                    acc[p] = dist_term2<M>(acc[p], f2{hi.x, hi.y}, x[t].z);
+                    acc[p] = dist_term2<M>(acc[p], f2{hi.z, hi.w}, x[t].w);
+                }
+            }
+        }
+        for (; t0 < d4; ++t0) {
+            const float4 x = vb[(size_t)t0 * 64];
+#pragma unroll
+            for (int p = 0; p < GP; ++p) {
+                const float4 lo = qlds[((size_t)p * d4 + t0) * 2], hi = qlds[((size_t)p * d4 + t0) * 2 + 1];
+                acc[p] = dist_term2<M>(acc[p], f2{lo.x, lo.y}, x.x);
+                acc[p] = dist_term2<M>(acc[p], f2{lo.z, lo.w}, x.y);
+                acc[p] = dist_term2<M>(acc[p], f2{hi.x, hi.y}, x.z);
+                acc[p] = dist_term2<M>(acc[p], f2{hi.z, hi.w}, x.w);
+            }
+        }
+        const bool valid = j * 64 + lane < nv;
+        float dist[G];
+        bool want[G];
+        bool any = false;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            dist[g] = dist_finish<M>((g & 1) ? acc[g >> 1].y : acc[g >> 1].x);
+            want[g] = g < np && valid && dist[g] <= kd[g];
+            any |= want[g];
+        }
+        if (__ballot(any)) {
+            const uint64_t vid = valid ? a.ids[(b0 + j) * 64 + lane] : kNoId;
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                if (g < np) offer_lanes<1>(tk[g], want[g], dist[g], vid, k, kd[g], ki[g]);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        if (g >= np) break;
+        const uint32_t part = a.part_base_sorted[it.pair_start + g] + seg;
+        if (lane < k) {
+            a.part_d[(size_t)part * k + lane] = tk[g].d[0];
+            a.part_i[(size_t)part * k + lane] = tk[g].id[0];
+        }
+    }
+}
+
+// ============================================================================
+// Level-1 partial merge: one wave folds <= kMergeFan segment partials of one
+// (query, probe) pair into one (multiset top-min(k, n_l), cpp:368-377), so a list
+// of millions of vectors is never merged by a single wave.
+// ============================================================================
+template <int R>
+__device__ __forceinline__ void merge_partial_item(const uint32_t* __restrict__ probes,
+                                                   const uint32_t* __restrict__ count_global,
+                                                   const uint32_t* __restrict__ nseg_qp,
+                                                   const uint32_t* __restrict__ part_base_qp,
+                                                   const uint32_t* __restrict__ l1base_qp, const uint2 w,
+                                                   const float* __restrict__ part_d,
+                                                   const uint64_t* __restrict__ part_i, uint32_t k,
+                                                   float* __restrict__ l1_d, uint64_t* __restrict__ l1_i);
+
+template <int R>
+__global__ __launch_bounds__(256) void ivf_merge_partials(const uint32_t* __restrict__ probes,
+                                                          const uint32_t* __restrict__ count_global,
+                                                          const uint32_t* __restrict__ nseg_qp,
+                                                          const uint32_t* __restrict__ part_base_qp,
+                                                          const uint32_t* __restrict__ l1base_qp,
+                                                          const uint2* __restrict__ l1_items,
+                                                          const uint32_t* __restrict__ counters,
+                                                          const float* __restrict__ part_d,
+                                                          const uint64_t* __restrict__ part_i, uint32_t k,
+                                                          float* __restrict__ l1_d, uint64_t* __restrict__ l1_i) {
+    const uint32_t n_items = counters[2];
+    for (uint32_t idx = blockIdx.x * 4 + wave_index(); idx < n_items; idx += gridDim.x * 4)
+        merge_partial_item<R>(probes, count_global, nseg_qp, part_base_qp, l1base_qp, l1_items[idx], part_d, part_i, k,
+                              l1_d, l1_i);
+}
+
+template <int R>
+__device__ __forceinline__ void merge_partial_item(const uint32_t* __restrict__ probes,
+                                                   const uint32_t* __restrict__ count_global,
+                                                   const uint32_t* __restrict__ nseg_qp,
+                                                   const uint32_t* __restrict__ part_base_qp,
+                                                   const uint32_t* __restrict__ l1base_qp, const uint2 w,
+                                                   const float* __restrict__ part_d,
+                                                   const uint64_t* __restrict__ part_i, uint32_t k,
+                                                   float* __restrict__ l1_d, uint64_t* __restrict__ l1_i) {
+    const uint32_t i = w.x, j = w.y;
+    const int lane = lane_id();
+    const uint32_t ns = nseg_qp[i];
+    const uint32_t cnt = min((uint32_t)kMergeFan, ns - j * kMergeFan);
+    const size_t base = ((size_t)part_base_qp[i] + (size_t)j * kMergeFan) * k;
+    const int kk = (int)min(k, count_global[probes[i]]);
+    WaveTopK<R> tk;
+    tk.init();
+    float kd = __builtin_inff();
+    uint64_t ki = kNoId;
+    const uint32_t n = cnt * k;
+    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        const bool valid = c < n;
+        const float d = valid ? part_d[base + c] : __builtin_inff();
+        const uint64_t id = valid ? part_i[base + c] : kNoId;
+        offer_lanes<R>(tk, valid && d <= kd, d, id, kk, kd, ki);
+    }
+    float* od = l1_d + ((size_t)l1base_qp[i] + j) * k;
+    uint64_t* oi = l1_i + ((size_t)l1base_qp[i] + j) * k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < (int)k) {
+            od[e] = e < kk ? tk.d[r] : __builtin_inff();
+            oi[e] = e < kk ? tk.id[r] : kNoId;
+        }
     }
 }
 
@@ -414,13 +732,16 @@ __global__ __launch_bounds__(256) void k_scan(ScanArgs a) {
 // search_list_cpu's partial_sort yields for the whole list (cpp:368-377).
 // ============================================================================
 template <int R>
-__global__ __launch_bounds__(256) void k_slot_merge(const uint32_t* __restrict__ probes,
-                                                    const uint32_t* __restrict__ count_global,
-                                                    const uint32_t* __restrict__ nseg_qp,
-                                                    const uint32_t* __restrict__ part_base_qp,
-                                                    const float* __restrict__ part_d,
-                                                    const uint64_t* __restrict__ part_i, uint32_t BP, uint32_t k,
-                                                    float* __restrict__ slot_d, uint64_t* __restrict__ slot_i) {
+__global__ __launch_bounds__(256) void ivf_merge_slots(const uint32_t* __restrict__ probes,
+                                                       const uint32_t* __restrict__ count_global,
+                                                       const uint32_t* __restrict__ nseg_qp,
+                                                       const uint32_t* __restrict__ part_base_qp,
+                                                       const uint32_t* __restrict__ l1base_qp,
+                                                       const float* __restrict__ part_d,
+                                                       const uint64_t* __restrict__ part_i,
+                                                       const float* __restrict__ l1_d,
+                                                       const uint64_t* __restrict__ l1_i, uint32_t BP, uint32_t k,
+                                                       float* __restrict__ slot_d, uint64_t* __restrict__ slot_i) {
     const uint32_t i = blockIdx.x * 4 + wave_index();
     if (i >= BP) return;
     const int lane = lane_id();
@@ -434,11 +755,22 @@ __global__ __launch_bounds__(256) void k_slot_merge(const uint32_t* __restrict__
         }
         return;
     }
-    const size_t base = (size_t)part_base_qp[i] * k;
-    if (ns == 1) {
+    const float* sd;
+    const uint64_t* si;
+    uint32_t nin;
+    if (ns <= (uint32_t)kMergeFan) {
+        sd = part_d + (size_t)part_base_qp[i] * k;
+        si = part_i + (size_t)part_base_qp[i] * k;
+        nin = ns;
+    } else {
+        sd = l1_d + (size_t)l1base_qp[i] * k;
+        si = l1_i + (size_t)l1base_qp[i] * k;
+        nin = (ns + kMergeFan - 1) / kMergeFan;
+    }
+    if (nin == 1) {
         for (uint32_t e = lane; e < k; e += 64) {
-            od[e] = part_d[base + e];
-            oi[e] = part_i[base + e];
+            od[e] = sd[e];
+            oi[e] = si[e];
         }
         return;
     }
@@ -447,12 +779,12 @@ __global__ __launch_bounds__(256) void k_slot_merge(const uint32_t* __restrict__
     tk.init();
     float kd = __builtin_inff();
     uint64_t ki = kNoId;
-    const uint32_t n = ns * k;
+    const uint32_t n = nin * k;
     for (uint32_t c0 = 0; c0 < n; c0 += 64) {
         const uint32_t c = c0 + lane;
         const bool valid = c < n;
-        const float d = valid ? part_d[base + c] : __builtin_inff();
-        const uint64_t id = valid ? part_i[base + c] : kNoId;
+        const float d = valid ? sd[c] : __builtin_inff();
+        const uint64_t id = valid ? si[c] : kNoId;
         offer_lanes<R>(tk, valid && d <= kd, d, id, kk, kd, ki);
     }
 #pragma unroll
@@ -504,7 +836,7 @@ __device__ __forceinline__ void write_final(const WaveTopK<R>& tk, uint32_t k, f
 // lists, cpp:210-233) into the unique-id top-k.
 // ============================================================================
 template <int R>
-__global__ __launch_bounds__(256) void k_query_merge(const uint32_t* __restrict__ probes,
+__global__ __launch_bounds__(256) void ivf_merge_query(const uint32_t* __restrict__ probes,
                                                      const uint32_t* __restrict__ count_global,
                                                      const float* __restrict__ slot_d,
                                                      const uint64_t* __restrict__ slot_i,
@@ -548,7 +880,7 @@ __global__ __launch_bounds__(256) void k_query_merge(const uint32_t* __restrict_
 }
 
 // Slot content that survives into the next batch of the same search call.
-__global__ void k_carry(const uint32_t* __restrict__ probes, const uint32_t* __restrict__ count_global,
+__global__ void ivf_carry_slots(const uint32_t* __restrict__ probes, const uint32_t* __restrict__ count_global,
                         uint32_t B, uint32_t P, uint32_t k, const float* __restrict__ slot_d,
                         const uint64_t* __restrict__ slot_i, float* __restrict__ carry_d,
                         uint64_t* __restrict__ carry_i) {
@@ -574,7 +906,7 @@ __global__ void k_carry(const uint32_t* __restrict__ probes, const uint32_t* __r
 
 // Final combine of per-rank partials [nranks][n][k] (list-sharded multi-GPU).
 template <int R>
-__global__ __launch_bounds__(256) void k_rank_merge(const float* __restrict__ d, const uint64_t* __restrict__ ids,
+__global__ __launch_bounds__(256) void ivf_merge_ranks(const float* __restrict__ d, const uint64_t* __restrict__ ids,
                                                     uint32_t nranks, uint32_t n, uint32_t k,
                                                     float* __restrict__ out_d, uint64_t* __restrict__ out_i) {
     const uint32_t q = blockIdx.x * 4 + wave_index();
@@ -588,9 +920,8 @@ __global__ __launch_bounds__(256) void k_rank_merge(const float* __restrict__ d,
     write_final<R>(tk, k, out_d + (size_t)q * k, out_i + (size_t)q * k);
 }
 
-__global__ void k_fill_empty(uint64_t n, float* __restrict__ d, uint64_t* __restrict__ i) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) {
+__global__ void ivf_fill_empty(uint64_t n, float* __restrict__ d, uint64_t* __restrict__ i) {
+    for (uint64_t e = gtid(); e < n; e += gstride()) {
         d[e] = FLT_MAX;
         i[e] = kNoId;
     }
@@ -601,35 +932,35 @@ __global__ void k_fill_empty(uint64_t n, float* __restrict__ d, uint64_t* __rest
 // k-means++ seeding and Lloyd update (train, cpp:49-145).
 // ============================================================================
 // rows [n][dp] -> interleaved blocks [ceil(n/64)][d4][64] float4 (tail lanes zero).
-__global__ void k_interleave(const float* __restrict__ rows, uint64_t n, uint32_t d4, float4* __restrict__ out) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (block, t, lane)
+__global__ void ivf_interleave_rows(const float* __restrict__ rows, uint64_t n, uint32_t d4, float4* __restrict__ out) {
     const uint64_t nb = (n + 63) / 64;
-    if (e >= nb * d4 * 64) return;
-    const uint32_t lane = e & 63;
-    const uint64_t bt = e >> 6;
-    const uint64_t b = bt / d4;
-    const uint32_t t = (uint32_t)(bt - b * d4);
-    const uint64_t r = b * 64 + lane;
-    out[e] = r < n ? ((const float4*)(rows + r * (uint64_t)d4 * 4))[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (uint64_t e = gtid(); e < nb * d4 * 64; e += gstride()) {  // (block, t, lane)
+        const uint32_t lane = e & 63;
+        const uint64_t bt = e >> 6;
+        const uint64_t b = bt / d4;
+        const uint32_t t = (uint32_t)(bt - b * d4);
+        const uint64_t r = b * 64 + lane;
+        out[e] = r < n ? ((const float4*)(rows + r * (uint64_t)d4 * 4))[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 }
 
-__global__ void k_scatter_rows(const float* __restrict__ rows, const uint64_t* __restrict__ row_ids,
+__global__ void ivf_scatter_rows(const float* __restrict__ rows, const uint64_t* __restrict__ row_ids,
                                const uint32_t* __restrict__ order, uint64_t n, uint32_t d4,
                                const uint64_t* __restrict__ dest_slot, float4* __restrict__ arena,
                                uint64_t* __restrict__ arena_ids) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (j, t)
-    if (e >= n * d4) return;
-    const uint64_t j = e / d4;
-    const uint32_t t = (uint32_t)(e - j * d4);
-    const uint64_t slot = dest_slot[j];
-    if (slot == ~0ull) return;  // list stored on another shard
-    const uint64_t row = order[j];
-    arena[((slot >> 6) * d4 + t) * 64 + (slot & 63)] = ((const float4*)(rows + row * (uint64_t)d4 * 4))[t];
-    if (t == 0) arena_ids[slot] = row_ids[row];
+    for (uint64_t e = gtid(); e < n * d4; e += gstride()) {  // (j, t)
+        const uint64_t j = e / d4;
+        const uint32_t t = (uint32_t)(e - j * d4);
+        const uint64_t slot = dest_slot[j];
+        if (slot == ~0ull) continue;  // list stored on another shard
+        const uint64_t row = order[j];
+        arena[((slot >> 6) * d4 + t) * 64 + (slot & 63)] = ((const float4*)(rows + row * (uint64_t)d4 * 4))[t];
+        if (t == 0) arena_ids[slot] = row_ids[row];
+    }
 }
 
 // Move each list's first nblocks[l] blocks from old_off[l] to new_off[l].
-__global__ void k_copy_lists(const float4* __restrict__ old_arena, const uint64_t* __restrict__ old_ids,
+__global__ void ivf_copy_lists(const float4* __restrict__ old_arena, const uint64_t* __restrict__ old_ids,
                              const uint64_t* __restrict__ old_off, const uint64_t* __restrict__ new_off,
                              const uint32_t* __restrict__ nblocks, uint32_t d4, float4* __restrict__ new_arena,
                              uint64_t* __restrict__ new_ids) {
@@ -644,28 +975,39 @@ __global__ void k_copy_lists(const float4* __restrict__ old_arena, const uint64_
         new_ids[new_off[l] * 64 + e] = old_ids[old_off[l] * 64 + e];
 }
 
-__global__ void k_export_list(const float4* __restrict__ arena, const uint64_t* __restrict__ ids,
+__global__ void ivf_export_list(const float4* __restrict__ arena, const uint64_t* __restrict__ ids,
                               uint64_t block_off, uint32_t count, uint32_t dim, uint32_t d4,
                               float* __restrict__ out, uint64_t* __restrict__ out_ids) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (v, d)
-    if (e >= (uint64_t)count * dim) return;
-    const uint32_t v = (uint32_t)(e / dim), d = (uint32_t)(e - (uint64_t)v * dim);
-    const float* blk = (const float*)(arena + ((block_off + (v >> 6)) * d4 + (d >> 2)) * 64 + (v & 63));
-    out[e] = blk[d & 3];
-    if (d == 0 && out_ids) out_ids[v] = ids[(block_off << 6) + v];
+    for (uint64_t e = gtid(); e < (uint64_t)count * dim; e += gstride()) {  // (v, d)
+        const uint32_t v = (uint32_t)(e / dim), d = (uint32_t)(e - (uint64_t)v * dim);
+        const float* blk = (const float*)(arena + ((block_off + (v >> 6)) * d4 + (d >> 2)) * 64 + (v & 63));
+        out[e] = blk[d & 3];
+        if (d == 0 && out_ids) out_ids[v] = ids[(block_off << 6) + v];
+    }
 }
+
+template <int M, int G>
+__device__ __forceinline__ void assign_group(const float* __restrict__ vpad, uint64_t n, uint32_t d4,
+                                             const float4* __restrict__ cent, uint32_t nlist,
+                                             uint32_t* __restrict__ out, uint64_t v0, int lane);
 
 // Exact argmin over centroids with the reference's strict '<' (lowest index wins
 // ties; a distance must beat FLT_MAX to count, else list 0). Lane = centroid,
 // 8 row vectors per wave whose dims are wave-uniform.
 template <int M>
-__global__ __launch_bounds__(256) void k_assign(const float* __restrict__ vpad, uint64_t n, uint32_t d4,
+__global__ __launch_bounds__(256) void ivf_assign(const float* __restrict__ vpad, uint64_t n, uint32_t d4,
                                                 const float4* __restrict__ cent, uint32_t nlist,
                                                 uint32_t* __restrict__ out) {
     constexpr int G = 8;
     const int lane = lane_id();
-    const uint64_t v0 = ((uint64_t)blockIdx.x * 4 + wave_index()) * G;
-    if (v0 >= n) return;
+    for (uint64_t v0 = ((uint64_t)blockIdx.x * 4 + wave_index()) * G; v0 < n; v0 += (uint64_t)gridDim.x * 4 * G)
+        assign_group<M, G>(vpad, n, d4, cent, nlist, out, v0, lane);
+}
+
+template <int M, int G>
+__device__ __forceinline__ void assign_group(const float* __restrict__ vpad, uint64_t n, uint32_t d4,
+                                             const float4* __restrict__ cent, uint32_t nlist,
+                                             uint32_t* __restrict__ out, uint64_t v0, int lane) {
     const float4* q[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) q[g] = (const float4*)(vpad + min(v0 + g, n - 1) * (uint64_t)d4 * 4);
@@ -715,39 +1057,37 @@ __global__ __launch_bounds__(256) void k_assign(const float* __restrict__ vpad, 
     }
 }
 
-__global__ void k_histogram(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ counts) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) atomicAdd(&counts[keys[e]], 1u);
+__global__ void ivf_histogram(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ counts) {
+    for (uint64_t e = gtid(); e < n; e += gstride()) atomicAdd(&counts[keys[e]], 1u);
 }
 
-__global__ void k_fill_f32(float* __restrict__ p, uint64_t n, float v) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) p[e] = v;
+__global__ void ivf_fill_f32(float* __restrict__ p, uint64_t n, float v) {
+    for (uint64_t e = gtid(); e < n; e += gstride()) p[e] = v;
 }
 
 // k-means++: min_dist[v] = std::min(min_dist[v], L2(v, newest centroid)) (cpp:68-84).
 // Lane = training vector (interleaved copy); centroid dims are wave-uniform.
-__global__ __launch_bounds__(256) void k_mindist_update(const float4* __restrict__ v_il, uint64_t n, uint32_t d4,
+__global__ __launch_bounds__(256) void kmeanspp_mindist(const float4* __restrict__ v_il, uint64_t n, uint32_t d4,
                                                         const float* __restrict__ crow,
                                                         float* __restrict__ mind) {
-    const uint64_t blk = (uint64_t)blockIdx.x * 4 + wave_index();
     const int lane = lane_id();
-    if (blk * 64 >= n) return;
-    const float4* vb = v_il + blk * d4 * 64 + lane;
     const float4* c4 = (const float4*)crow;
-    float acc = 0.0f;
+    for (uint64_t blk = (uint64_t)blockIdx.x * 4 + wave_index(); blk * 64 < n; blk += (uint64_t)gridDim.x * 4) {
+        const float4* vb = v_il + blk * d4 * 64 + lane;
+        float acc = 0.0f;
 #pragma unroll 8
-    for (uint32_t t = 0; t < d4; ++t) acc = acc4<kL2>(acc, vb[(size_t)t * 64], c4[t]);
-    const uint64_t v = blk * 64 + lane;
-    if (v < n) {
-        const float m = mind[v];
-        mind[v] = (acc < m) ? acc : m;  // std::min(m, acc)
+        for (uint32_t t = 0; t < d4; ++t) acc = acc4<kL2>(acc, vb[(size_t)t * 64], c4[t]);
+        const uint64_t v = blk * 64 + lane;
+        if (v < n) {
+            const float m = mind[v];
+            mind[v] = (acc < m) ? acc : m;  // std::min(m, acc)
+        }
     }
 }
 
 // The serial float sum of cpp:87 and the cumsum of cpp:95-96 produce the same
 // running values; one wave walks them in order, lane j latching element j.
-__global__ void k_serial_prefix(const float* __restrict__ mind, uint64_t n, float* __restrict__ prefix,
+__global__ void kmeanspp_serial_prefix(const float* __restrict__ mind, uint64_t n, float* __restrict__ prefix,
                                 float* __restrict__ total) {
     const int lane = lane_id();
     float s = 0.0f;
@@ -766,13 +1106,13 @@ __global__ void k_serial_prefix(const float* __restrict__ mind, uint64_t n, floa
 }
 
 // First v with cumsum >= target (cpp:95-103); n if none.
-__global__ void k_first_geq(const float* __restrict__ prefix, uint64_t n, float target,
+__global__ void kmeanspp_pick(const float* __restrict__ prefix, uint64_t n, float target,
                             unsigned long long* __restrict__ out) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n && prefix[e] >= target) atomicMin(out, (unsigned long long)e);
+    for (uint64_t e = gtid(); e < n; e += gstride())
+        if (prefix[e] >= target) atomicMin(out, (unsigned long long)e);
 }
 
-__global__ void k_copy_row_if(const float* __restrict__ vpad, uint64_t n, uint32_t dp,
+__global__ void kmeanspp_copy_row(const float* __restrict__ vpad, uint64_t n, uint32_t dp,
                               const unsigned long long* __restrict__ idx, float* __restrict__ dst) {
     const uint64_t i = *idx;
     if (i >= n) return;
@@ -781,7 +1121,7 @@ __global__ void k_copy_row_if(const float* __restrict__ vpad, uint64_t n, uint32
 
 // Lloyd update (cpp:122-141): per (cluster, dim), sum members in input order,
 // then divide by the count; empty clusters keep their centroid.
-__global__ void k_centroid_update(const float* __restrict__ vpad, uint32_t dp, const uint32_t* __restrict__ order,
+__global__ void lloyd_update(const float* __restrict__ vpad, uint32_t dp, const uint32_t* __restrict__ order,
                                   const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ counts,
                                   uint32_t dim, float* __restrict__ cent) {
     const uint32_t c = blockIdx.y;
@@ -794,18 +1134,17 @@ __global__ void k_centroid_update(const float* __restrict__ vpad, uint32_t dp, c
     cent[(uint64_t)c * dp + d] = s / (float)cnt;
 }
 
-__global__ void k_iota(uint32_t* __restrict__ out, uint64_t n) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) out[e] = (uint32_t)e;
+__global__ void ivf_iota(uint32_t* __restrict__ out, uint64_t n) {
+    for (uint64_t e = gtid(); e < n; e += gstride()) out[e] = (uint32_t)e;
 }
 
-__global__ void k_slots_from_order(const uint32_t* __restrict__ sorted_keys, uint64_t n,
+__global__ void ivf_slots_from_order(const uint32_t* __restrict__ sorted_keys, uint64_t n,
                                    const uint64_t* __restrict__ group_start,
                                    const uint64_t* __restrict__ base_slot, uint64_t* __restrict__ dest) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const uint32_t l = sorted_keys[j];
-    dest[j] = base_slot[l] == ~0ull ? ~0ull : base_slot[l] + (j - group_start[l]);
+    for (uint64_t j = gtid(); j < n; j += gstride()) {
+        const uint32_t l = sorted_keys[j];
+        dest[j] = base_slot[l] == ~0ull ? ~0ull : base_slot[l] + (j - group_start[l]);
+    }
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -816,60 +1155,98 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 }
 
 // Counter-based Box-Muller normal draws (synthetic benchmark data only).
-__global__ void k_gen_normal(float* __restrict__ out, uint64_t n, uint64_t seed, uint64_t offset) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t h = splitmix64(splitmix64(seed) ^ (offset + i));
-    const float u1 = ((float)(h >> 40) + 1.0f) * (1.0f / 16777216.0f);       // (0, 1]
-    const float u2 = (float)(h & 0xFFFFFFull) * (1.0f / 16777216.0f);          // [0, 1)
-    out[i] = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+__global__ void synth_gen_normal(float* __restrict__ out, uint64_t n, uint64_t seed, uint64_t offset) {
+    const uint64_t sk = splitmix64(seed);
+    for (uint64_t i = gtid(); i < n; i += gstride()) {
+        const uint64_t h = splitmix64(sk ^ (offset + i));
+        const float u1 = ((float)(h >> 40) + 1.0f) * (1.0f / 16777216.0f);       // (0, 1]
+        const float u2 = (float)(h & 0xFFFFFFull) * (1.0f / 16777216.0f);          // [0, 1)
+        out[i] = sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+    }
 }
 
 // ============================================================================
 // Launchers
 // ============================================================================
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+// Blocks for an element-wise launch of n items: at most 2^20 blocks of 256 (2^28 work-items).
+static inline uint32_t launch_grid(uint64_t n, uint32_t block = 256) {
+    const uint64_t b = (n + block - 1) / block;
+    return (uint32_t)(b < (1ull << 20) ? (b ? b : 1) : (1ull << 20));
+}
 
 void launch_pad_rows(const float* src, uint64_t n, uint32_t dim, uint32_t dp, float* dst, hipStream_t s) {
     if (!n) return;
-    k_pad_rows<<<cdiv(n * dp, 256), 256, 0, s>>>(src, n, dim, dp, dst);
+    ivf_pad_queries<<<launch_grid(n * dp), 256, 0, s>>>(src, n, dim, dp, dst);
 }
 
 void launch_coarse(int metric, const float4* cent, uint32_t nlist, uint32_t d4, const float* qpad, uint32_t B,
                    float* cd, hipStream_t s) {
     dim3 grid(cdiv(nlist, 64), cdiv(B, 16));
-    if (metric == kL2) k_coarse<kL2><<<grid, 256, 0, s>>>(cent, nlist, d4, qpad, B, cd);
-    else if (metric == kIP) k_coarse<kIP><<<grid, 256, 0, s>>>(cent, nlist, d4, qpad, B, cd);
-    else k_coarse<kCos><<<grid, 256, 0, s>>>(cent, nlist, d4, qpad, B, cd);
+    if (metric == kL2) ivf_coarse_distances<kL2><<<grid, 256, 0, s>>>(cent, nlist, d4, qpad, B, cd);
+    else if (metric == kIP) ivf_coarse_distances<kIP><<<grid, 256, 0, s>>>(cent, nlist, d4, qpad, B, cd);
+    else ivf_coarse_distances<kCos><<<grid, 256, 0, s>>>(cent, nlist, d4, qpad, B, cd);
 }
 
 void launch_select(int regs, const float* cd, uint32_t nlist, uint32_t B, uint32_t P, uint32_t* probes,
                    hipStream_t s) {
     const uint32_t g = cdiv(B, 4);
     switch (regs) {
-        case 1: k_select<1><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
-        case 2: k_select<2><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
-        case 4: k_select<4><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
-        case 8: k_select<8><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
-        default: k_select<16><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
+        case 1: ivf_select_probes<1><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
+        case 2: ivf_select_probes<2><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
+        case 4: ivf_select_probes<4><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
+        case 8: ivf_select_probes<8><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
+        default: ivf_select_probes<16><<<g, 256, 0, s>>>(cd, nlist, B, P, probes); break;
     }
 }
 
 void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint32_t* count_local, uint32_t B,
-                 uint32_t P, uint32_t group, ScanItem* items, uint32_t* counters, uint32_t* sorted_pair,
-                 uint32_t* part_base_sorted, uint32_t* part_base_qp, uint32_t* nseg_qp,
-                 unsigned long long* stats, hipStream_t s) {
+                 uint32_t P, uint32_t group, int wide, ScanItem* items, ScanItem* items_w, uint32_t* counters,
+                 uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp, uint32_t* nseg_qp,
+                 uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats, hipStream_t s) {
     uint32_t np = 1;
     while (np < B * P) np <<= 1;
-    k_plan<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, items, counters, sorted_pair,
-                              part_base_sorted, part_base_qp, nseg_qp, stats);
+    ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, wide ? 1u : 0u, items,
+                                       items_w, counters, sorted_pair, part_base_sorted, part_base_qp, nseg_qp,
+                                       l1base_qp, l1_items, stats);
+}
+
+void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes, const uint32_t* count_global,
+                           const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
+                           const uint2* l1_items, const uint32_t* counters, const float* part_d,
+                           const uint64_t* part_i, uint32_t k, float* l1_d, uint64_t* l1_i, hipStream_t s) {
+    const uint32_t g = launch_grid(grid_items, 4);
+    if (!grid_items) return;
+#define VDB_MP(R) ivf_merge_partials<R><<<g, 256, 0, s>>>(probes, count_global, nseg_qp, part_base_qp, l1base_qp, l1_items, counters, part_d, part_i, k, l1_d, l1_i)
+    switch (regs) {
+        case 1: VDB_MP(1); break;
+        case 2: VDB_MP(2); break;
+        case 4: VDB_MP(4); break;
+        case 8: VDB_MP(8); break;
+        default: VDB_MP(16); break;
+    }
+#undef VDB_MP
 }
 
 template <int R>
 static void scan_dispatch_metric(int metric, uint32_t grid, const ScanArgs& a, hipStream_t s) {
-    if (metric == kL2) k_scan<R, kL2><<<grid, 256, 0, s>>>(a);
-    else if (metric == kIP) k_scan<R, kIP><<<grid, 256, 0, s>>>(a);
-    else k_scan<R, kCos><<<grid, 256, 0, s>>>(a);
+    if (metric == kL2) ivf_scan<R, kL2><<<grid, 256, 0, s>>>(a);
+    else if (metric == kIP) ivf_scan<R, kIP><<<grid, 256, 0, s>>>(a);
+    else ivf_scan<R, kCos><<<grid, 256, 0, s>>>(a);
+}
+
+void launch_scan_wide(int metric, uint32_t grid_items, const float4* arena, const uint64_t* ids,
+                      const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
+                      const ScanItem* items_w, const uint32_t* counters, const uint32_t* sorted_pair,
+                      const uint32_t* part_base_sorted, uint32_t k, float* part_d, uint64_t* part_i, hipStream_t s) {
+    if (!grid_items) return;
+    ScanArgs a{arena, ids, block_off, count_local, qpad, nullptr, items_w, counters, sorted_pair, part_base_sorted,
+               part_d, part_i, d4, k};
+    const size_t lds = (size_t)(kWideGroup / 2) * d4 * 2 * sizeof(float4);
+    const uint32_t grid = launch_grid(grid_items, 1);
+    if (metric == kL2) ivf_scan_wide<kL2><<<grid, 256, lds, s>>>(a);
+    else if (metric == kIP) ivf_scan_wide<kIP><<<grid, 256, lds, s>>>(a);
+    else ivf_scan_wide<kCos><<<grid, 256, lds, s>>>(a);
 }
 
 void launch_scan(int metric, int regs, uint32_t grid_items, const float4* arena, const uint64_t* ids,
@@ -877,9 +1254,9 @@ void launch_scan(int metric, int regs, uint32_t grid_items, const float4* arena,
                  const ScanItem* items, const uint32_t* counters, const uint32_t* sorted_pair,
                  const uint32_t* part_base_sorted, uint32_t k, float* part_d, uint64_t* part_i, hipStream_t s) {
     if (!grid_items) return;
-    ScanArgs a{arena, ids, block_off, count_local, qpad, items, counters, sorted_pair, part_base_sorted,
+    ScanArgs a{arena, ids, block_off, count_local, qpad, items, nullptr, counters, sorted_pair, part_base_sorted,
                part_d, part_i, d4, k};
-    const uint32_t grid = cdiv(grid_items, 4);
+    const uint32_t grid = launch_grid(grid_items, 4);
     switch (regs) {
         case 1: scan_dispatch_metric<1>(metric, grid, a, s); break;
         case 2: scan_dispatch_metric<2>(metric, grid, a, s); break;
@@ -890,11 +1267,12 @@ void launch_scan(int metric, int regs, uint32_t grid_items, const float4* arena,
 }
 
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const uint32_t* nseg_qp,
-                       const uint32_t* part_base_qp, const float* part_d, const uint64_t* part_i, uint32_t BP,
-                       uint32_t k, float* slot_d, uint64_t* slot_i, hipStream_t s) {
+                       const uint32_t* part_base_qp, const uint32_t* l1base_qp, const float* part_d,
+                       const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i, uint32_t BP, uint32_t k,
+                       float* slot_d, uint64_t* slot_i, hipStream_t s) {
     const uint32_t g = cdiv(BP, 4);
     if (!g) return;
-#define VDB_SLOT(R) k_slot_merge<R><<<g, 256, 0, s>>>(probes, count_global, nseg_qp, part_base_qp, part_d, part_i, BP, k, slot_d, slot_i)
+#define VDB_SLOT(R) ivf_merge_slots<R><<<g, 256, 0, s>>>(probes, count_global, nseg_qp, part_base_qp, l1base_qp, part_d, part_i, l1_d, l1_i, BP, k, slot_d, slot_i)
     switch (regs) {
         case 1: VDB_SLOT(1); break;
         case 2: VDB_SLOT(2); break;
@@ -910,7 +1288,7 @@ void launch_query_merge(int regs, const uint32_t* probes, const uint32_t* count_
                         uint32_t P, uint32_t k, int stale, float* out_d, uint64_t* out_i, hipStream_t s) {
     const uint32_t g = cdiv(B, 4);
     if (!g) return;
-#define VDB_QM(R) k_query_merge<R><<<g, 256, 0, s>>>(probes, count_global, slot_d, slot_i, carry_d, carry_i, B, P, k, stale, out_d, out_i)
+#define VDB_QM(R) ivf_merge_query<R><<<g, 256, 0, s>>>(probes, count_global, slot_d, slot_i, carry_d, carry_i, B, P, k, stale, out_d, out_i)
     switch (regs) {
         case 1: VDB_QM(1); break;
         case 2: VDB_QM(2); break;
@@ -924,14 +1302,14 @@ void launch_query_merge(int regs, const uint32_t* probes, const uint32_t* count_
 void launch_carry(const uint32_t* probes, const uint32_t* count_global, uint32_t B, uint32_t P, uint32_t k,
                   const float* slot_d, const uint64_t* slot_i, float* carry_d, uint64_t* carry_i, hipStream_t s) {
     if (!P || !B) return;
-    k_carry<<<P, 64, 0, s>>>(probes, count_global, B, P, k, slot_d, slot_i, carry_d, carry_i);
+    ivf_carry_slots<<<P, 64, 0, s>>>(probes, count_global, B, P, k, slot_d, slot_i, carry_d, carry_i);
 }
 
 void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint32_t nranks, uint32_t n, uint32_t k,
                        float* out_d, uint64_t* out_i, hipStream_t s) {
     const uint32_t g = cdiv(n, 4);
     if (!g) return;
-#define VDB_RM(R) k_rank_merge<R><<<g, 256, 0, s>>>(d, i, nranks, n, k, out_d, out_i)
+#define VDB_RM(R) ivf_merge_ranks<R><<<g, 256, 0, s>>>(d, i, nranks, n, k, out_d, out_i)
     switch (regs) {
         case 1: VDB_RM(1); break;
         case 2: VDB_RM(2); break;
@@ -944,21 +1322,21 @@ void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint32_t nra
 
 void launch_fill_empty(uint64_t n, float* d, uint64_t* i, hipStream_t s) {
     if (!n) return;
-    k_fill_empty<<<cdiv(n, 256), 256, 0, s>>>(n, d, i);
+    ivf_fill_empty<<<launch_grid(n), 256, 0, s>>>(n, d, i);
 }
 
 void launch_interleave(const float* rows, uint64_t n, uint32_t dp, float4* blocks, hipStream_t s) {
     if (!n) return;
     const uint32_t d4 = dp / 4;
     const uint64_t total = (n + 63) / 64 * d4 * 64;
-    k_interleave<<<cdiv(total, 256), 256, 0, s>>>(rows, n, d4, blocks);
+    ivf_interleave_rows<<<launch_grid(total), 256, 0, s>>>(rows, n, d4, blocks);
 }
 
 void launch_scatter_rows(const float* rows, const uint64_t* row_ids, const uint32_t* order, uint64_t n, uint32_t dp,
                          const uint64_t* dest_slot, float4* arena, uint64_t* arena_ids, hipStream_t s) {
     if (!n) return;
     const uint32_t d4 = dp / 4;
-    k_scatter_rows<<<cdiv(n * d4, 256), 256, 0, s>>>(rows, row_ids, order, n, d4, dest_slot, arena, arena_ids);
+    ivf_scatter_rows<<<launch_grid(n * d4), 256, 0, s>>>(rows, row_ids, order, n, d4, dest_slot, arena, arena_ids);
 }
 
 void launch_copy_lists(const float4* old_arena, const uint64_t* old_ids, const uint64_t* old_off,
@@ -966,76 +1344,76 @@ void launch_copy_lists(const float4* old_arena, const uint64_t* old_ids, const u
                        float4* new_arena, uint64_t* new_ids, hipStream_t s) {
     if (!nlist) return;
     dim3 grid(16, nlist);
-    k_copy_lists<<<grid, 256, 0, s>>>(old_arena, old_ids, old_off, new_off, nblocks, d4, new_arena, new_ids);
+    ivf_copy_lists<<<grid, 256, 0, s>>>(old_arena, old_ids, old_off, new_off, nblocks, d4, new_arena, new_ids);
 }
 
 void launch_export_list(const float4* arena, const uint64_t* ids, uint64_t block_off, uint32_t count, uint32_t dim,
                         uint32_t d4, float* out, uint64_t* out_ids, hipStream_t s) {
     if (!count) return;
-    k_export_list<<<cdiv((uint64_t)count * dim, 256), 256, 0, s>>>(arena, ids, block_off, count, dim, d4, out,
+    ivf_export_list<<<launch_grid((uint64_t)count * dim), 256, 0, s>>>(arena, ids, block_off, count, dim, d4, out,
                                                                    out_ids);
 }
 
 void launch_assign(int metric, const float* vpad, uint64_t n, uint32_t dp, const float4* cent, uint32_t nlist,
                    uint32_t* out, hipStream_t s) {
     if (!n) return;
-    const uint32_t grid = cdiv(n, 32);
+    const uint32_t grid = launch_grid(n, 32);
     const uint32_t d4 = dp / 4;
-    if (metric == kL2) k_assign<kL2><<<grid, 256, 0, s>>>(vpad, n, d4, cent, nlist, out);
-    else if (metric == kIP) k_assign<kIP><<<grid, 256, 0, s>>>(vpad, n, d4, cent, nlist, out);
-    else k_assign<kCos><<<grid, 256, 0, s>>>(vpad, n, d4, cent, nlist, out);
+    if (metric == kL2) ivf_assign<kL2><<<grid, 256, 0, s>>>(vpad, n, d4, cent, nlist, out);
+    else if (metric == kIP) ivf_assign<kIP><<<grid, 256, 0, s>>>(vpad, n, d4, cent, nlist, out);
+    else ivf_assign<kCos><<<grid, 256, 0, s>>>(vpad, n, d4, cent, nlist, out);
 }
 
 void launch_histogram(const uint32_t* keys, uint64_t n, uint32_t* counts, hipStream_t s) {
     if (!n) return;
-    k_histogram<<<cdiv(n, 256), 256, 0, s>>>(keys, n, counts);
+    ivf_histogram<<<launch_grid(n), 256, 0, s>>>(keys, n, counts);
 }
 
 void launch_mindist_init(float* mind, uint64_t n, hipStream_t s) {
     if (!n) return;
-    k_fill_f32<<<cdiv(n, 256), 256, 0, s>>>(mind, n, FLT_MAX);
+    ivf_fill_f32<<<launch_grid(n), 256, 0, s>>>(mind, n, FLT_MAX);
 }
 
 void launch_mindist_update(const float4* v_il, uint64_t n, uint32_t d4, const float* crow, float* mind,
                            hipStream_t s) {
     if (!n) return;
-    k_mindist_update<<<cdiv((n + 63) / 64, 4), 256, 0, s>>>(v_il, n, d4, crow, mind);
+    kmeanspp_mindist<<<launch_grid((n + 63) / 64, 4), 256, 0, s>>>(v_il, n, d4, crow, mind);
 }
 
 void launch_serial_prefix(const float* mind, uint64_t n, float* prefix, float* total, hipStream_t s) {
-    k_serial_prefix<<<1, 64, 0, s>>>(mind, n, prefix, total);
+    kmeanspp_serial_prefix<<<1, 64, 0, s>>>(mind, n, prefix, total);
 }
 
 void launch_first_geq(const float* prefix, uint64_t n, float target, unsigned long long* out, hipStream_t s) {
     if (!n) return;
-    k_first_geq<<<cdiv(n, 256), 256, 0, s>>>(prefix, n, target, out);
+    kmeanspp_pick<<<launch_grid(n), 256, 0, s>>>(prefix, n, target, out);
 }
 
 void launch_copy_row_if(const float* vpad, uint64_t n, uint32_t dp, const unsigned long long* idx, float* dst_row,
                         hipStream_t s) {
-    k_copy_row_if<<<1, 256, 0, s>>>(vpad, n, dp, idx, dst_row);
+    kmeanspp_copy_row<<<1, 256, 0, s>>>(vpad, n, dp, idx, dst_row);
 }
 
 void launch_centroid_update(const float* vpad, uint32_t dp, const uint32_t* order, const uint32_t* offsets,
                             const uint32_t* counts, uint32_t nlist, uint32_t dim, float* cent_rm, hipStream_t s) {
     dim3 grid(cdiv(dim, 256), nlist);
-    k_centroid_update<<<grid, 256, 0, s>>>(vpad, dp, order, offsets, counts, dim, cent_rm);
+    lloyd_update<<<grid, 256, 0, s>>>(vpad, dp, order, offsets, counts, dim, cent_rm);
 }
 
 void launch_iota(uint32_t* out, uint64_t n, hipStream_t s) {
     if (!n) return;
-    k_iota<<<cdiv(n, 256), 256, 0, s>>>(out, n);
+    ivf_iota<<<launch_grid(n), 256, 0, s>>>(out, n);
 }
 
 void launch_slots_from_order(const uint32_t* sorted_keys, uint64_t n, const uint64_t* group_start,
                              const uint64_t* base_slot, uint64_t* dest, hipStream_t s) {
     if (!n) return;
-    k_slots_from_order<<<cdiv(n, 256), 256, 0, s>>>(sorted_keys, n, group_start, base_slot, dest);
+    ivf_slots_from_order<<<launch_grid(n), 256, 0, s>>>(sorted_keys, n, group_start, base_slot, dest);
 }
 
 void launch_gen_normal(float* out, uint64_t n, uint64_t seed, uint64_t offset, hipStream_t s) {
     if (!n) return;
-    k_gen_normal<<<cdiv(n, 256), 256, 0, s>>>(out, n, seed, offset);
+    synth_gen_normal<<<launch_grid(n), 256, 0, s>>>(out, n, seed, offset);
 }
 
 hipError_t radix_sort_pairs(void* temp, size_t& temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,

@@ -16,6 +16,10 @@ namespace vdbk {
 
 constexpr int kSegBlocks = 8;              // 64-vector blocks per scan work item
 constexpr int kSegVectors = kSegBlocks * 64;
+constexpr int kChunkTiles = 8;             // float4 of a list vector held in registers (32 dims)
+constexpr int kMergeFan = 32;              // segment partials folded per level-1 merge wave
+constexpr int kWideGroup = 8;              // pairs per wide scan item (hub lists)
+constexpr int kNarrowMax = 4;              // pairs per narrow scan item
 constexpr int kPlanMaxPairs = 8192;        // batch * nprobe per plan launch
 constexpr int kMaxK = 1024;                // top-k capacity (16 registers x 64 lanes)
 
@@ -33,7 +37,8 @@ inline int topk_regs(uint32_t k) {
     while (r * 64 < (int)k) r <<= 1;
     return r;
 }
-inline int scan_group(int regs) { return regs == 1 ? 4 : (regs == 2 ? 2 : 1); }
+__host__ __device__ constexpr int scan_group_max(int regs) { return regs == 1 ? 4 : (regs == 2 ? 2 : 1); }
+inline int scan_group(int regs) { return scan_group_max(regs); }
 
 // ---- search ----
 void launch_pad_rows(const float* src, uint64_t n, uint32_t dim, uint32_t dp, float* dst, hipStream_t s);
@@ -42,18 +47,27 @@ void launch_coarse(int metric, const float4* cent_il, uint32_t nlist, uint32_t d
 void launch_select(int regs, const float* cd, uint32_t nlist, uint32_t B, uint32_t P, uint32_t* probes,
                    hipStream_t s);
 void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint32_t* count_local,
-                 uint32_t B, uint32_t P, uint32_t group, ScanItem* items, uint32_t* counters,
-                 uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp,
-                 uint32_t* nseg_qp, unsigned long long* stats, hipStream_t s);
+                 uint32_t B, uint32_t P, uint32_t group, int wide, ScanItem* items, ScanItem* items_w,
+                 uint32_t* counters, uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp,
+                 uint32_t* nseg_qp, uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats,
+                 hipStream_t s);
+void launch_scan_wide(int metric, uint32_t grid_items, const float4* arena, const uint64_t* ids,
+                      const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
+                      const ScanItem* items_w, const uint32_t* counters, const uint32_t* sorted_pair,
+                      const uint32_t* part_base_sorted, uint32_t k, float* part_d, uint64_t* part_i, hipStream_t s);
+void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes, const uint32_t* count_global,
+                           const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
+                           const uint2* l1_items, const uint32_t* counters, const float* part_d,
+                           const uint64_t* part_i, uint32_t k, float* l1_d, uint64_t* l1_i, hipStream_t s);
 void launch_scan(int metric, int regs, uint32_t grid_items, const float4* arena, const uint64_t* ids,
                  const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
                  const ScanItem* items, const uint32_t* counters, const uint32_t* sorted_pair,
                  const uint32_t* part_base_sorted, uint32_t k, float* part_d, uint64_t* part_i,
                  hipStream_t s);
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
-                       const uint32_t* nseg_qp, const uint32_t* part_base_qp, const float* part_d,
-                       const uint64_t* part_i, uint32_t BP, uint32_t k, float* slot_d, uint64_t* slot_i,
-                       hipStream_t s);
+                       const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
+                       const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,
+                       uint32_t BP, uint32_t k, float* slot_d, uint64_t* slot_i, hipStream_t s);
 void launch_query_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const float* slot_d,
                         const uint64_t* slot_i, const float* carry_d, const uint64_t* carry_i,
                         uint32_t B, uint32_t P, uint32_t k, int stale, float* out_d, uint64_t* out_i,

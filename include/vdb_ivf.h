@@ -74,6 +74,7 @@ typedef struct vdb_ivf_profile {
     uint64_t distinct_lists;   /* sum over batches of distinct probed local lists */
     uint64_t work_items;       /* sum over batches of scan work items */
     uint64_t scan_bytes;       /* algorithmic bytes read by ivf_scan: 4 * dim * scan_vectors */
+    uint64_t pair_vectors;     /* sum over batches and (query, probe) pairs of n_l: distances computed */
 } vdb_ivf_profile;
 
 const char* vdb_last_error(void);

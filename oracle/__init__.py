@@ -62,6 +62,7 @@ def lib():
             "oracle_get_list": (None, [vp, ctypes.c_uint32, _f32p, _u64p]),
             "oracle_set_list": (None, [vp, ctypes.c_uint32, _f32p, _u64p, ctypes.c_uint64]),
             "oracle_total_vectors": (ctypes.c_uint64, [vp]),
+            "oracle_list_resize": (None, [vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(_f32p), ctypes.POINTER(_u64p)]),
             "oracle_gen_normal": (None, [ctypes.c_uint32, ctypes.c_uint64, _f32p]),
         }
         for name, (res, args) in sig.items():
@@ -175,6 +176,17 @@ class OracleIndex:
         v = np.ascontiguousarray(vectors, dtype=np.float32).reshape(-1, self.dim)
         i = np.ascontiguousarray(ids, dtype=np.uint64)
         lib().oracle_set_list(self._h, l, _p(v, _f32p), _p(i, _u64p), v.shape[0])
+
+    def list_buffers(self, l: int, count: int):
+        """Resize list l to `count` vectors and return writable numpy views of its
+        storage (vectors (count, dim) f32, ids (count,) u64) to fill in place."""
+        vp, ip = _f32p(), _u64p()
+        lib().oracle_list_resize(self._h, l, count, ctypes.byref(vp), ctypes.byref(ip))
+        if count == 0:
+            return np.empty((0, self.dim), np.float32), np.empty(0, np.uint64)
+        v = np.ctypeslib.as_array(vp, shape=(count, self.dim))
+        i = np.ctypeslib.as_array(ip, shape=(count,))
+        return v, i
 
     @property
     def total_vectors(self) -> int:

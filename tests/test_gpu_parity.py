@@ -252,3 +252,42 @@ def test_two_shards_merge_equals_single():
                            torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), Dr, Ir)
+
+
+@pytest.mark.parametrize("k", [10, 64, 65])
+def test_hub_lists_wide_items(k):
+    """Skewed lists probed by every query of the batch: wide scan items (groups of
+    8 queries), XCD-alignment padding items and two-level partial merges."""
+    rng = np.random.default_rng(7)
+    X = rng.standard_normal((40000, 48)).astype(np.float32)
+    Q = rng.standard_normal((130, 48)).astype(np.float32)
+    ids = rng.permutation(40000).astype(np.uint64)
+    C = np.zeros((6, 48), np.float32)                     # centroid 0 at the origin takes most vectors
+    C[1:] = 3.0 * rng.standard_normal((5, 48)).astype(np.float32)
+    o = oracle.OracleIndex(48, 6, 0)
+    o.centroids = C
+    o.add(X, ids)
+    assert max(o.list_count(l) for l in range(6)) > 32 * 512, "need > kMergeFan segments in one list"
+    g = mirror_from_oracle(o, 48, 6)
+    g.add(X, ids)
+    for batch in (64, 130):
+        g.set_batch(batch)
+        assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))
+
+
+def test_launches_beyond_2_32_workitems():
+    """HSA grid sizes are 32-bit in work-items: element-wise launchers must stride.
+    (10M x 768 = 7.7e9 floats once left the tail of the synthetic data unwritten.)"""
+    import torch
+    n = (1 << 32) + 4096
+    dev = torch.device("cuda:0")
+    buf = torch.zeros(n, dtype=torch.float32, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    vdb.gen_normal_device(buf.data_ptr(), n, seed=5, offset=0, stream=s)
+    tail = torch.empty(4096, dtype=torch.float32, device=dev)
+    vdb.gen_normal_device(tail.data_ptr(), 4096, seed=5, offset=n - 4096, stream=s)
+    torch.cuda.synchronize()
+    assert torch.equal(buf[-4096:], tail)
+    assert int((buf[-(1 << 20):] == 0).sum()) < 16
+    del buf
+    torch.cuda.empty_cache()
