@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -314,10 +315,17 @@ struct vdb_ivf {
         if (n == 0) return;
         DevBuf<float> tmp;
         const float* vpad = padded_rows(d_v, n, tmp);
-        DevBuf<uint32_t> asg, skeys, order, counts;
+        DevBuf<uint32_t> asg;
         assign(vpad, n, asg.ensure(n));
-        group_by_key(asg.p, n, skeys, order);
-        std::vector<uint32_t> added = key_counts(asg.p, n, counts);
+        append(vpad, d_ids, asg.p, n);
+    }
+
+    // Append rows to the given lists, keeping input order within each list
+    // (cpp:160-192). `asg` holds one list id per row (device).
+    void append(const float* vpad, const uint64_t* d_ids, const uint32_t* asg, uint64_t n) {
+        DevBuf<uint32_t> skeys, order, counts;
+        group_by_key(asg, n, skeys, order);
+        std::vector<uint32_t> added = key_counts(asg, n, counts);
 
         std::vector<uint64_t> new_count(count);
         for (uint32_t l = 0; l < nlist; ++l) new_count[l] += added[l];
@@ -336,7 +344,7 @@ struct vdb_ivf {
         HIPCHECK(hipGetLastError());
         count = new_count;
         total += n;
-        upload_directory();
+        upload_directory();  // also waits for the stream before tmp buffers go
     }
 
     void set_shard(uint32_t r, uint32_t w) {
@@ -590,6 +598,105 @@ int vdb_ivf_add_device(vdb_ivf* h, const float* d_v, const uint64_t* d_ids, uint
     });
 }
 
+int vdb_ivf_add_to_lists(vdb_ivf* h, const float* v, const uint64_t* ids, const uint32_t* lists, uint64_t n) {
+    return guarded([&] {
+        require(h && ((v && ids && lists) || n == 0), "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        if (n == 0) return;
+        for (uint64_t i = 0; i < n; ++i) require(lists[i] < h->nlist, "list id out of range");
+        DevBuf<float> dv, tmp;
+        DevBuf<uint64_t> di;
+        DevBuf<uint32_t> dl;
+        HIPCHECK(hipMemcpyAsync(dv.ensure(n * h->dim), v, n * h->dim * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHECK(hipMemcpyAsync(di.ensure(n), ids, n * 8, hipMemcpyHostToDevice, h->stream));
+        HIPCHECK(hipMemcpyAsync(dl.ensure(n), lists, n * 4, hipMemcpyHostToDevice, h->stream));
+        h->append(h->padded_rows(dv.p, n, tmp), di.p, dl.p, n);
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+// Index file: "VDBIVF01", u32 dim, u32 nlist, i32 metric, u32 reserved, centroids
+// f32[nlist][dim], then per list: u64 count, u64 ids[count], f32 vectors[count][dim].
+int vdb_ivf_save(vdb_ivf* h, const char* path) {
+    return guarded([&] {
+        require(h && path, "null argument");
+        require(h->world == 1, "save a sharded handle from every rank's full copy instead", VDB_ERR_STATE);
+        FILE* f = std::fopen(path, "wb");
+        require(f != nullptr, std::string("cannot open ") + path, VDB_ERR_STATE);
+        auto put = [&](const void* p, size_t b) {
+            if (b && std::fwrite(p, 1, b, f) != b) {
+                std::fclose(f);
+                throw VdbError(VDB_ERR_STATE, "short write");
+            }
+        };
+        const uint32_t hdr[4] = {h->dim, h->nlist, (uint32_t)h->metric, 0};
+        put("VDBIVF01", 8);
+        put(hdr, sizeof(hdr));
+        std::vector<float> c((size_t)h->nlist * h->dim);
+        if (vdb_ivf_get_centroids(h, c.data()) != VDB_OK) {
+            std::fclose(f);
+            throw VdbError(VDB_ERR_DEVICE, g_last_error);
+        }
+        put(c.data(), c.size() * 4);
+        for (uint32_t l = 0; l < h->nlist; ++l) {
+            const uint64_t cnt = h->count[l];
+            std::vector<float> v(cnt * h->dim);
+            std::vector<uint64_t> ids(cnt);
+            if (cnt && vdb_ivf_get_list(h, l, v.data(), ids.data()) != VDB_OK) {
+                std::fclose(f);
+                throw VdbError(VDB_ERR_DEVICE, g_last_error);
+            }
+            put(&cnt, 8);
+            put(ids.data(), cnt * 8);
+            put(v.data(), v.size() * 4);
+        }
+        std::fclose(f);
+    });
+}
+
+int vdb_ivf_load(vdb_ivf* h, const char* path) {
+    return guarded([&] {
+        require(h && path, "null argument");
+        FILE* f = std::fopen(path, "rb");
+        require(f != nullptr, std::string("cannot open ") + path, VDB_ERR_STATE);
+        auto get = [&](void* p, size_t b) {
+            if (b && std::fread(p, 1, b, f) != b) {
+                std::fclose(f);
+                throw VdbError(VDB_ERR_STATE, "truncated index file");
+            }
+        };
+        char magic[8];
+        uint32_t hdr[4];
+        get(magic, 8);
+        get(hdr, sizeof(hdr));
+        if (std::memcmp(magic, "VDBIVF01", 8) != 0 || hdr[0] != h->dim || hdr[1] != h->nlist ||
+            (int)hdr[2] != h->metric) {
+            std::fclose(f);
+            throw VdbError(VDB_ERR_INVALID_ARGUMENT, "index file does not match this index's configuration");
+        }
+        std::vector<float> c((size_t)h->nlist * h->dim);
+        get(c.data(), c.size() * 4);
+        std::vector<float> vs;
+        std::vector<uint64_t> is;
+        std::vector<uint32_t> ls;
+        for (uint32_t l = 0; l < h->nlist; ++l) {
+            uint64_t cnt = 0;
+            get(&cnt, 8);
+            const size_t o = is.size();
+            is.resize(o + cnt);
+            vs.resize((o + cnt) * h->dim);
+            get(is.data() + o, cnt * 8);
+            get(vs.data() + o * h->dim, cnt * h->dim * 4);
+            ls.insert(ls.end(), cnt, l);
+        }
+        std::fclose(f);
+        int rc = vdb_ivf_set_centroids(h, c.data());
+        if (rc == VDB_OK) rc = vdb_ivf_add_to_lists(h, vs.data(), is.data(), ls.data(), is.size());
+        if (rc != VDB_OK) throw VdbError(rc, g_last_error);
+    });
+}
+
 int vdb_ivf_search(vdb_ivf* h, const float* q, uint32_t n, uint32_t nprobe, uint32_t k, float* dist,
                    uint64_t* ids) {
     return guarded([&] {
@@ -680,6 +787,8 @@ uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* h) {
 }
 
 uint64_t vdb_ivf_ntotal(const vdb_ivf* h) { return h ? h->total : 0; }
+uint32_t vdb_ivf_dimension(const vdb_ivf* h) { return h ? h->dim : 0; }
+uint32_t vdb_ivf_nlist(const vdb_ivf* h) { return h ? h->nlist : 0; }
 
 int vdb_ivf_list_sizes(const vdb_ivf* h, uint64_t* sizes) {
     return guarded([&] {

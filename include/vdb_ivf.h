@@ -95,6 +95,15 @@ int vdb_ivf_get_centroids(vdb_ivf* index, float* centroids);        /* nlist x d
 int vdb_ivf_add(vdb_ivf* index, const float* vectors, const uint64_t* ids, uint64_t n);
 int vdb_ivf_add_device(vdb_ivf* index, const float* d_vectors, const uint64_t* d_ids, uint64_t n);
 
+/* Append rows to explicitly given lists (no assignment), input order kept per list.
+ * Used by vdb_ivf_load and for indexes whose assignment was computed elsewhere. */
+int vdb_ivf_add_to_lists(vdb_ivf* index, const float* vectors, const uint64_t* ids, const uint32_t* lists,
+                         uint64_t n);
+/* Persist / restore centroids and lists (IVFFlatIndex::save/load, engine/ivf_flat_index.h:66-67,
+ * declared but never defined in the reference; this engine's own file format). */
+int vdb_ivf_save(vdb_ivf* index, const char* path);
+int vdb_ivf_load(vdb_ivf* index, const char* path);
+
 /* search: host buffers in and out (PCIe included). nprobe is clamped to nlist. */
 int vdb_ivf_search(vdb_ivf* index, const float* queries, uint32_t n, uint32_t nprobe, uint32_t k,
                    float* distances, uint64_t* ids);
@@ -120,6 +129,8 @@ int vdb_ivf_evict(vdb_ivf* index, uint32_t list);
 
 uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* index);
 uint64_t vdb_ivf_ntotal(const vdb_ivf* index);
+uint32_t vdb_ivf_dimension(const vdb_ivf* index);
+uint32_t vdb_ivf_nlist(const vdb_ivf* index);
 int vdb_ivf_list_sizes(const vdb_ivf* index, uint64_t* sizes);  /* nlist entries */
 /* Copy list `list` out row-major (count x dim) with its ids, in add order. */
 int vdb_ivf_get_list(vdb_ivf* index, uint32_t list, float* vectors, uint64_t* ids);

@@ -291,3 +291,41 @@ def test_launches_beyond_2_32_workitems():
     assert int((buf[-(1 << 20):] == 0).sum()) < 16
     del buf
     torch.cuda.empty_cache()
+
+
+GOLDEN_DIR = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden")
+
+
+@pytest.mark.parametrize("name", ["simple_test", "gpu_vs_cpu_ctest", "benchmark_small", "inner_product",
+                                  "empty_lists_dups"])
+def test_golden_fixture_on_gpu(name):
+    import os
+    f = np.load(os.path.join(GOLDEN_DIR, name + ".npz"))
+    dim, nlist, train_n, nprobe, k, metric = (int(x) for x in f["params"])
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, vdb.Metric(metric)))
+    if train_n:
+        g.train(f["X"][:train_n])
+        assert np.array_equal(bits(g.centroids), bits(f["centroids"]))
+    else:
+        g.centroids = f["centroids"]
+    g.add(f["X"], f["ids"])
+    assert np.array_equal(g.list_sizes(), f["list_sizes"])
+    assert_same(*g.search(f["Q"], nprobe=nprobe, k=k), f["D"], f["I"])
+
+
+def test_save_load_round_trip(tmp_path):
+    X, Q, ids = oracle.reference_test_data(4000, 30, 40, seed=31)
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(40, 12))
+    g.train(X[:1000])
+    g.add(X, ids)
+    D, I = g.search(Q, nprobe=4, k=10)
+    lib = vdb.lib()
+    path = str(tmp_path / "idx.ivf").encode()
+    import ctypes
+    lib.vdb_ivf_save.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    lib.vdb_ivf_load.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    assert lib.vdb_ivf_save(g._h, path) == 0
+    h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(40, 12))
+    assert lib.vdb_ivf_load(h._h, path) == 0
+    assert np.array_equal(h.list_sizes(), g.list_sizes())
+    assert_same(*h.search(Q, nprobe=4, k=10), D, I)
