@@ -380,7 +380,7 @@ struct vdb_ivf {
         const size_t BP = (size_t)B * P;
         const size_t max_items = (size_t)B * nseg_prefix[P];
         const size_t max_l1 = max_items / vdbk::kMergeFan + BP;
-        const size_t max_wide = max_items / 4 + (size_t)BP * 8 + 8;
+        const size_t max_wide = max_items / 4 + BP + 1;
         const bool grow = items_w.cap < max_wide || qpad.cap < (size_t)B * dp || cd.cap < (size_t)B * nlist || probes.cap < BP ||
                           items.cap < max_items || part_d.cap < max_items * k || slot_d.cap < BP * k ||
                           carry_d.cap < (size_t)P * k || l1_items.cap < max_l1 || l1_d.cap < max_l1 * k;
@@ -426,16 +426,14 @@ struct vdb_ivf {
         vdbk::launch_select(regs_p, cd.p, nlist, B, P, probes.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
         const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
-        const uint64_t max_wide = max_items / 4 + (uint64_t)BP * 8 + 8;
-        const bool wide = regs_k == 1 && wide_scan;
+        const uint64_t max_wide = max_items / 4 + BP + 1;
+        const bool wide = regs_k == 1 && wide_scan && vdbk::scan_wide_fits(d4, k);
         vdbk::launch_plan(probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? 1 : 0, items.p, items_w.p,
                           counters.p, sorted_pair.p, pbs.p, pbqp.p, nseg_qp.p, l1base.p, l1_items.p, stats.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
-        if (wide)
-            vdbk::launch_scan_wide(metric, (uint32_t)max_wide, arena.p, arena_ids.p, d_block_off.p, d_count_local.p,
-                                   qpad.p, d4, items_w.p, counters.p, sorted_pair.p, pbs.p, k, part_d.p, part_i.p, s);
-        vdbk::launch_scan(metric, regs_k, (uint32_t)max_items, arena.p, arena_ids.p, d_block_off.p, d_count_local.p,
-                          qpad.p, d4, items.p, counters.p, sorted_pair.p, pbs.p, k, part_d.p, part_i.p, s);
+        vdbk::launch_scan(metric, regs_k, wide ? 1 : 0, (uint32_t)(max_wide + (max_items + 3) / 4), arena.p, arena_ids.p,
+                          d_block_off.p, d_count_local.p, qpad.p, d4, items.p, items_w.p, counters.p, sorted_pair.p,
+                          pbs.p, k, part_d.p, part_i.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_end, s));
         vdbk::launch_merge_partials(regs_k, (uint32_t)max_l1, probes.p, d_count_global.p, nseg_qp.p, pbqp.p, l1base.p,
                                     l1_items.p, counters.p, part_d.p, part_i.p, k, l1_d.p, l1_i.p, s);

@@ -173,30 +173,24 @@ __device__ uint32_t plan_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
     return res;
 }
 
-// Query groups of one list with m (query, probe) pairs. With wide items enabled
-// (top-k in one register), pairs go in groups of kWideGroup; a trailing group of
-// <= kNarrowMax pairs becomes a narrow item. Otherwise groups of gn pairs.
+// Query groups of one list with m (query, probe) pairs and ns segments. A list of at
+// least kWideMinSeg segments (with top-k in one register) is scanned by wide items:
+// ceil(m / kWideGroup) balanced groups x ceil(ns / 4) segment quads, so each list is
+// read ceil(m / 16) times per batch. Other lists: narrow items of <= gn pairs x ns.
 struct ListGroups {
-    uint32_t wide, narrow, full;
+    uint32_t wide, narrow;
 };
-__device__ __forceinline__ ListGroups list_groups(uint32_t m, uint32_t gn, bool wide) {
+__device__ __forceinline__ ListGroups list_groups(uint32_t m, uint32_t ns, uint32_t gn, bool wide) {
     ListGroups g;
-    if (wide) {
-        g.full = m / kWideGroup;
-        const uint32_t rem = m % kWideGroup;
-        g.wide = g.full + (rem > (uint32_t)kNarrowMax ? 1u : 0u);
-        g.narrow = (rem > 0 && rem <= (uint32_t)kNarrowMax) ? 1u : 0u;
+    if (wide && ns >= (uint32_t)kWideMinSeg) {
+        g.wide = (m + kWideGroup - 1) / kWideGroup;
+        g.narrow = 0;
     } else {
-        g.full = 0;
         g.wide = 0;
         g.narrow = (m + gn - 1) / gn;
     }
     return g;
 }
-
-// Wide items per group of a list with ns segments: quads of 4 segments, padded
-// to a multiple of 8 (see the emission loop in ivf_plan_probes).
-__device__ __forceinline__ uint32_t wide_span(uint32_t ns) { return ((ns + 3) / 4 + 7) / 8 * 8; }
 
 // Last index d in [0, n) with base[d] <= x (base non-decreasing, base[0] == 0).
 __device__ __forceinline__ uint32_t find_owner(const uint32_t* base, uint32_t n, uint32_t x) {
@@ -316,9 +310,9 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
             if (!is_head(s)) continue;
             ++cur;
             const uint32_t ns = nseg_local[list_of(s)];
-            const ListGroups g = list_groups(starts[cur + 1] - starts[cur], gn, wide);
+            const ListGroups g = list_groups(starts[cur + 1] - starts[cur], ns, gn, wide);
             nsum_n += g.narrow * ns;
-            nsum_w += g.wide * wide_span(ns);
+            nsum_w += g.wide * ((ns + 3) / 4);
         }
     }
     uint32_t n_narrow, n_wide;
@@ -332,51 +326,45 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
             ++cur;
             const uint32_t l = list_of(s);
             const uint32_t ns = nseg_local[l];
-            const ListGroups g = list_groups(starts[cur + 1] - starts[cur], gn, wide);
+            const ListGroups g = list_groups(starts[cur + 1] - starts[cur], ns, gn, wide);
             base_n[cur] = bn;
             base_w[cur] = bw;
             bn += g.narrow * ns;
-            bw += g.wide * wide_span(ns);
+            bw += g.wide * ((ns + 3) / 4);
             atomicAdd(&stats[1], (unsigned long long)count_local[l]);
         }
     }
     __syncthreads();
 
-    // Emit items in parallel. Narrow items of a list are ordered (segment, group)
-    // and wide ones (segment quad, group): the groups re-reading one stretch of the
-    // list are adjacent, so they run side by side and share L2.
+    // Emit items in parallel. Items of one list are ordered (segment or quad, group):
+    // the groups re-reading one stretch of the list are adjacent in the grid.
     for (uint32_t x = tid; x < n_narrow; x += blockDim.x) {
         const uint32_t dl = find_owner(base_n, nd, x);
         const uint32_t off = x - base_n[dl];
         const uint32_t st = starts[dl], m = starts[dl + 1] - st;
         const uint32_t l = list_of(st);
-        const ListGroups g = list_groups(m, gn, wide);
+        const ListGroups g = list_groups(m, nseg_local[l], gn, wide);
         const uint32_t gi = off % g.narrow, seg = off / g.narrow;
         ScanItem it;
         it.list = l;
         it.seg = seg;
-        it.pair_start = st + (wide ? g.full * kWideGroup : gi * gn);
-        it.npairs = wide ? m - g.full * kWideGroup : min(gn, m - gi * gn);
+        it.pair_start = st + gi * gn;
+        it.npairs = min(gn, m - gi * gn);
         items_n[x] = it;
     }
-    // Wide items: one workgroup each. Within a list, item x -> (r = x % 8,
-    // group = (x / 8) % ng, chunk = x / (8 ng)), quad = chunk * 8 + r: every group
-    // of a quad shares x % 8, i.e. one XCD under round-robin dispatch, so the
-    // group re-reads of those 4 segments hit that XCD's L2 (placement only ever
-    // affects speed). Padding items (quad past the list) exit at once.
     for (uint32_t x = tid; x < n_wide; x += blockDim.x) {
         const uint32_t dl = find_owner(base_w, nd, x);
         const uint32_t off = x - base_w[dl];
         const uint32_t st = starts[dl], m = starts[dl + 1] - st;
         const uint32_t l = list_of(st);
-        const ListGroups g = list_groups(m, gn, wide);
-        const uint32_t r = off & 7u, gi = (off >> 3) % g.wide, chunk = (off >> 3) / g.wide;
-        const uint32_t quad = chunk * 8 + r;
+        const ListGroups g = list_groups(m, nseg_local[l], gn, wide);
+        const uint32_t gi = off % g.wide, quad = off / g.wide;
+        const uint32_t p0 = gi * m / g.wide, p1 = (gi + 1) * m / g.wide;  // balanced groups
         ScanItem it;
         it.list = l;
         it.seg = quad;
-        it.pair_start = st + gi * kWideGroup;
-        it.npairs = quad * 4 < nseg_local[l] ? min((uint32_t)kWideGroup, m - gi * kWideGroup) : 0u;
+        it.pair_start = st + p0;
+        it.npairs = p1 - p0;
         items_w[x] = it;
     }
     if (tid == 0) {
@@ -502,30 +490,6 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
     }
 }
 
-template <int R, int M>
-__global__ __launch_bounds__(256) void ivf_scan(ScanArgs a) {
-    constexpr int GMAX = scan_group_max(R);
-    const uint32_t n_items = a.counters[0];
-    for (uint32_t idx = blockIdx.x * 4 + wave_index(); idx < n_items; idx += gridDim.x * 4) {
-        const ScanItem it = a.items[idx];
-        switch (it.npairs) {
-            case 1: scan_item<R, 1, M>(a, it); break;
-            case 2: if constexpr (GMAX >= 2) scan_item<R, 2, M>(a, it); break;
-            case 3: if constexpr (GMAX >= 3) scan_item<R, 3, M>(a, it); break;
-            case 4: if constexpr (GMAX >= 4) scan_item<R, 4, M>(a, it); break;
-            default: break;
-        }
-    }
-}
-
-// ============================================================================
-// ivf_scan_wide: hub lists probed by many queries of the batch. One workgroup =
-// one group of 5..16 (query, probe) pairs of one list x 4 consecutive segments
-// (one per wave). The group's queries are staged once in LDS as interleaved
-// pairs (q[2p][d], q[2p+1][d]) and read by broadcast; each lane keeps 32 dims of
-// its list vector in registers and runs two queries per packed instruction
-// (v_pk_add_f32 / v_pk_mul_f32 round each half exactly like the scalar ops).
-// ============================================================================
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 template <int M>
@@ -541,37 +505,36 @@ __device__ __forceinline__ f2 dist_term2(f2 acc, f2 q, float x) {
     }
 }
 
-template <int M>
-__device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds);
-
-template <int M>
-__global__ __launch_bounds__(256) void ivf_scan_wide(ScanArgs a) {
-    constexpr int GP = kWideGroup / 2;
-    extern __shared__ __attribute__((aligned(16))) float4 qlds[];  // [GP][d4][2] float4
-    const uint32_t d4 = a.d4;
-    const uint32_t n_items = a.counters[3];
-    for (uint32_t idx = blockIdx.x; idx < n_items; idx += gridDim.x) {
-        const ScanItem it = a.items_w[idx];
-        const int np = (int)it.npairs;
-        if (np == 0) continue;  // XCD-alignment padding (block-uniform)
-        // Stage the group's queries: pair p, tile t -> (qa.x, qb.x, qa.y, qb.y), (qa.z, qb.z, qa.w, qb.w).
-        for (uint32_t e = threadIdx.x; e < GP * d4; e += blockDim.x) {
-            const uint32_t p = e / d4, t = e - p * d4;
-            const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
-            const float4 qa = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + ga] >> 16) * d4 * 4))[t];
-            const float4 qb = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + gb] >> 16) * d4 * 4))[t];
-            qlds[(p * d4 + t) * 2 + 0] = make_float4(qa.x, qb.x, qa.y, qb.y);
-            qlds[(p * d4 + t) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
-        }
-        __syncthreads();
-        scan_wide_wave<M>(a, it, qlds);
-        __syncthreads();  // qlds is restaged by the next item
+// Top-k list of one query kept in LDS: k (dist, id) entries, ascending. Loads it
+// into the lane-distributed form (lanes >= k empty), offers the lanes in `mask`,
+// stores it back and returns the new k-th distance. Shared by every query slot
+// (runtime index) so the rare insertion path exists once in the code.
+__device__ __noinline__ float lds_topk_offer(float* sd, uint64_t* si, int k, uint64_t mask, float cd, uint64_t cid) {
+    const int lane = lane_id();
+    WaveTopK<1> tk;
+    tk.d[0] = lane < k ? sd[lane] : __builtin_inff();
+    tk.id[0] = lane < k ? si[lane] : kNoId;
+    float kd;
+    uint64_t ki;
+    tk.at(k - 1, kd, ki);
+    offer_lanes<1>(tk, ((mask >> lane) & 1ull) != 0, cd, cid, k, kd, ki);
+    if (lane < k) {
+        sd[lane] = tk.d[0];
+        si[lane] = tk.id[0];
     }
+    return kd;
 }
 
-template <int M>
-__device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds) {
-    constexpr int G = kWideGroup, GP = kWideGroup / 2;
+// One wave of a wide item: segment it.seg * 4 + wave of list it.list against GP
+// query pairs read from LDS as interleaved pairs (q[2p][d], q[2p+1][d]). Each lane
+// keeps kChunkTiles float4 of its list vector in registers and runs two queries per
+// packed instruction (v_pk_add_f32 / v_pk_mul_f32 round each half exactly like the
+// scalar ops); every query's sum still runs in d order. Per query only the k-th
+// distance lives in registers; the top-k lists live in LDS (tk_d / tk_i).
+template <int GP, int M>
+__device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds, float* tk_d,
+                                               uint64_t* tk_i) {
+    constexpr int G = 2 * GP;
     const uint32_t d4 = a.d4;
     const int np = (int)it.npairs;
     const int lane = lane_id();
@@ -585,15 +548,13 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
     const uint32_t nb = (nv + 63) >> 6;
     const int k = (int)a.k;
 
-    WaveTopK<1> tk[G];
-    float kd[G];
-    uint64_t ki[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        tk[g].init();
-        kd[g] = __builtin_inff();
-        ki[g] = kNoId;
+    for (int e = lane; e < G * k; e += 64) {
+        tk_d[e] = __builtin_inff();
+        tk_i[e] = kNoId;
     }
+    float kd[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) kd[g] = __builtin_inff();
     for (uint32_t j = 0; j < nb; ++j) {
         const float4* vb = a.arena + (b0 + j) * d4 * 64 + lane;
         f2 acc[GP];
@@ -629,29 +590,88 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
             }
         }
         const bool valid = j * 64 + lane < nv;
-        float dist[G];
-        bool want[G];
-        bool any = false;
+        uint64_t vid = kNoId;
+        bool have_id = false;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            dist[g] = dist_finish<M>((g & 1) ? acc[g >> 1].y : acc[g >> 1].x);
-            want[g] = g < np && valid && dist[g] <= kd[g];
-            any |= want[g];
-        }
-        if (__ballot(any)) {
-            const uint64_t vid = valid ? a.ids[(b0 + j) * 64 + lane] : kNoId;
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-                if (g < np) offer_lanes<1>(tk[g], want[g], dist[g], vid, k, kd[g], ki[g]);
+            if (g >= np) break;
+            const float dist = dist_finish<M>((g & 1) ? acc[g >> 1].y : acc[g >> 1].x);
+            const uint64_t mask = __ballot(valid && dist <= kd[g]);
+            if (mask) {
+                if (!have_id) {
+                    vid = valid ? a.ids[(b0 + j) * 64 + lane] : kNoId;
+                    have_id = true;
+                }
+                kd[g] = lds_topk_offer(tk_d + g * k, tk_i + g * k, k, mask, dist, vid);
+            }
         }
     }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        if (g >= np) break;
+    for (int g = 0; g < np; ++g) {
         const uint32_t part = a.part_base_sorted[it.pair_start + g] + seg;
         if (lane < k) {
-            a.part_d[(size_t)part * k + lane] = tk[g].d[0];
-            a.part_i[(size_t)part * k + lane] = tk[g].id[0];
+            a.part_d[(size_t)part * k + lane] = tk_d[g * k + lane];
+            a.part_i[(size_t)part * k + lane] = tk_i[g * k + lane];
+        }
+    }
+}
+
+// One wave-item of a narrow list (<= 4 pairs of one segment).
+template <int R, int M>
+__device__ __forceinline__ void scan_narrow(const ScanArgs& a, const ScanItem it) {
+    constexpr int GMAX = scan_group_max(R);
+    switch (it.npairs) {
+        case 1: scan_item<R, 1, M>(a, it); break;
+        case 2: if constexpr (GMAX >= 2) scan_item<R, 2, M>(a, it); break;
+        case 3: if constexpr (GMAX >= 3) scan_item<R, 3, M>(a, it); break;
+        case 4: if constexpr (GMAX >= 4) scan_item<R, 4, M>(a, it); break;
+        default: break;
+    }
+}
+
+// ivf_scan: the fine scan (search_list_cpu, cpp:347-370) of one batch in ONE launch.
+// Workgroup b < n_wide takes wide item b (a large list: 4 segments x up to 16 of its
+// queries, staged once in LDS); the remaining workgroups take 4 narrow items each
+// (small lists, one segment x <= 4 queries per wave, queries via scalar loads).
+template <int R, int M>
+__global__ __launch_bounds__(256) void ivf_scan(ScanArgs a) {
+    // Dynamic LDS (wide items, R == 1): [kWideGroup/2][d4][2] float4 of staged query
+    // pairs, then per wave kWideGroup x k top-k ids (u64) and distances (f32).
+    extern __shared__ __attribute__((aligned(16))) float4 qlds[];
+    const uint32_t d4 = a.d4;
+    uint64_t* tk_i = (uint64_t*)(qlds + (size_t)(kWideGroup / 2) * d4 * 2) + (size_t)wave_index() * kWideGroup * a.k;
+    float* tk_d = (float*)((uint64_t*)(qlds + (size_t)(kWideGroup / 2) * d4 * 2) + (size_t)4 * kWideGroup * a.k) +
+                  (size_t)wave_index() * kWideGroup * a.k;
+    const uint32_t n_wide = a.counters[3], n_narrow = a.counters[0];
+    const uint32_t nblocks = n_wide + (n_narrow + 3) / 4;
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        if (b >= n_wide) {
+            const uint32_t idx = (b - n_wide) * 4 + wave_index();
+            if (idx < n_narrow) scan_narrow<R, M>(a, a.items[idx]);
+            continue;
+        }
+        if constexpr (R == 1) {
+            const ScanItem it = a.items_w[b];
+            const int np = (int)it.npairs;
+            const int gp = (np + 1) / 2;
+            const int gpv = gp <= 1 ? 1 : gp <= 2 ? 2 : gp <= 3 ? 3 : gp <= 4 ? 4 : gp <= 6 ? 6 : 8;
+            for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
+                const uint32_t p = e / d4, t = e - p * d4;
+                const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
+                const float4 qa = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + ga] >> 16) * d4 * 4))[t];
+                const float4 qb = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + gb] >> 16) * d4 * 4))[t];
+                qlds[(p * d4 + t) * 2 + 0] = make_float4(qa.x, qb.x, qa.y, qb.y);
+                qlds[(p * d4 + t) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
+            }
+            __syncthreads();
+            switch (gpv) {
+                case 1: scan_wide_wave<1, M>(a, it, qlds, tk_d, tk_i); break;
+                case 2: scan_wide_wave<2, M>(a, it, qlds, tk_d, tk_i); break;
+                case 3: scan_wide_wave<3, M>(a, it, qlds, tk_d, tk_i); break;
+                case 4: scan_wide_wave<4, M>(a, it, qlds, tk_d, tk_i); break;
+                case 6: scan_wide_wave<6, M>(a, it, qlds, tk_d, tk_i); break;
+                default: scan_wide_wave<8, M>(a, it, qlds, tk_d, tk_i); break;
+            }
+            __syncthreads();  // qlds is restaged by the next wide item
         }
     }
 }
@@ -1229,40 +1249,45 @@ void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes
 }
 
 template <int R>
-static void scan_dispatch_metric(int metric, uint32_t grid, const ScanArgs& a, hipStream_t s) {
-    if (metric == kL2) ivf_scan<R, kL2><<<grid, 256, 0, s>>>(a);
-    else if (metric == kIP) ivf_scan<R, kIP><<<grid, 256, 0, s>>>(a);
-    else ivf_scan<R, kCos><<<grid, 256, 0, s>>>(a);
+static void scan_dispatch_metric(int metric, uint32_t grid, size_t lds, const ScanArgs& a, hipStream_t s) {
+    if (metric == kL2) ivf_scan<R, kL2><<<grid, 256, lds, s>>>(a);
+    else if (metric == kIP) ivf_scan<R, kIP><<<grid, 256, lds, s>>>(a);
+    else ivf_scan<R, kCos><<<grid, 256, lds, s>>>(a);
 }
 
-void launch_scan_wide(int metric, uint32_t grid_items, const float4* arena, const uint64_t* ids,
-                      const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
-                      const ScanItem* items_w, const uint32_t* counters, const uint32_t* sorted_pair,
-                      const uint32_t* part_base_sorted, uint32_t k, float* part_d, uint64_t* part_i, hipStream_t s) {
-    if (!grid_items) return;
-    ScanArgs a{arena, ids, block_off, count_local, qpad, nullptr, items_w, counters, sorted_pair, part_base_sorted,
-               part_d, part_i, d4, k};
-    const size_t lds = (size_t)(kWideGroup / 2) * d4 * 2 * sizeof(float4);
-    const uint32_t grid = launch_grid(grid_items, 1);
-    if (metric == kL2) ivf_scan_wide<kL2><<<grid, 256, lds, s>>>(a);
-    else if (metric == kIP) ivf_scan_wide<kIP><<<grid, 256, lds, s>>>(a);
-    else ivf_scan_wide<kCos><<<grid, 256, lds, s>>>(a);
+size_t scan_wide_lds(uint32_t d4, uint32_t k) {
+    return (size_t)(kWideGroup / 2) * d4 * 2 * sizeof(float4) + (size_t)4 * kWideGroup * k * (sizeof(float) + sizeof(uint64_t));
 }
 
-void launch_scan(int metric, int regs, uint32_t grid_items, const float4* arena, const uint64_t* ids,
+bool scan_wide_fits(uint32_t d4, uint32_t k) { return scan_wide_lds(d4, k) <= kLdsBytes; }
+
+void launch_scan(int metric, int regs, int wide, uint32_t grid_blocks, const float4* arena, const uint64_t* ids,
                  const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
-                 const ScanItem* items, const uint32_t* counters, const uint32_t* sorted_pair,
-                 const uint32_t* part_base_sorted, uint32_t k, float* part_d, uint64_t* part_i, hipStream_t s) {
-    if (!grid_items) return;
-    ScanArgs a{arena, ids, block_off, count_local, qpad, items, nullptr, counters, sorted_pair, part_base_sorted,
+                 const ScanItem* items, const ScanItem* items_w, const uint32_t* counters,
+                 const uint32_t* sorted_pair, const uint32_t* part_base_sorted, uint32_t k, float* part_d,
+                 uint64_t* part_i, hipStream_t s) {
+    if (!grid_blocks) return;
+    ScanArgs a{arena, ids, block_off, count_local, qpad, items, items_w, counters, sorted_pair, part_base_sorted,
                part_d, part_i, d4, k};
-    const uint32_t grid = launch_grid(grid_items, 4);
+    size_t lds = 0;
+    if (wide && regs == 1) {
+        static const bool raised = [] {
+            // wide items stage up to 16 queries in LDS: allow the whole 160 KB of a CU
+            hipFuncSetAttribute((const void*)ivf_scan<1, kL2>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+            hipFuncSetAttribute((const void*)ivf_scan<1, kIP>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+            hipFuncSetAttribute((const void*)ivf_scan<1, kCos>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+            return true;
+        }();
+        (void)raised;
+        lds = scan_wide_lds(d4, k);
+    }
+    const uint32_t grid = launch_grid(grid_blocks, 1);
     switch (regs) {
-        case 1: scan_dispatch_metric<1>(metric, grid, a, s); break;
-        case 2: scan_dispatch_metric<2>(metric, grid, a, s); break;
-        case 4: scan_dispatch_metric<4>(metric, grid, a, s); break;
-        case 8: scan_dispatch_metric<8>(metric, grid, a, s); break;
-        default: scan_dispatch_metric<16>(metric, grid, a, s); break;
+        case 1: scan_dispatch_metric<1>(metric, grid, lds, a, s); break;
+        case 2: scan_dispatch_metric<2>(metric, grid, 0, a, s); break;
+        case 4: scan_dispatch_metric<4>(metric, grid, 0, a, s); break;
+        case 8: scan_dispatch_metric<8>(metric, grid, 0, a, s); break;
+        default: scan_dispatch_metric<16>(metric, grid, 0, a, s); break;
     }
 }
 

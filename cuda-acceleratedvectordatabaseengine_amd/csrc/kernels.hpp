@@ -18,10 +18,12 @@ constexpr int kSegBlocks = 8;              // 64-vector blocks per scan work ite
 constexpr int kSegVectors = kSegBlocks * 64;
 constexpr int kChunkTiles = 8;             // float4 of a list vector held in registers (32 dims)
 constexpr int kMergeFan = 32;              // segment partials folded per level-1 merge wave
-constexpr int kWideGroup = 8;              // pairs per wide scan item (hub lists)
+constexpr int kWideGroup = 16;             // max pairs per wide scan item (large lists)
+constexpr int kWideMinSeg = 4;             // lists with >= 4 segments are scanned by wide items
 constexpr int kNarrowMax = 4;              // pairs per narrow scan item
 constexpr int kPlanMaxPairs = 8192;        // batch * nprobe per plan launch
 constexpr int kMaxK = 1024;                // top-k capacity (16 registers x 64 lanes)
+constexpr size_t kLdsBytes = 160 * 1024;   // LDS per CU (gfx950)
 
 struct ScanItem {
     uint32_t list;
@@ -51,19 +53,18 @@ void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint3
                  uint32_t* counters, uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp,
                  uint32_t* nseg_qp, uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats,
                  hipStream_t s);
-void launch_scan_wide(int metric, uint32_t grid_items, const float4* arena, const uint64_t* ids,
-                      const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
-                      const ScanItem* items_w, const uint32_t* counters, const uint32_t* sorted_pair,
-                      const uint32_t* part_base_sorted, uint32_t k, float* part_d, uint64_t* part_i, hipStream_t s);
 void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes, const uint32_t* count_global,
                            const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                            const uint2* l1_items, const uint32_t* counters, const float* part_d,
                            const uint64_t* part_i, uint32_t k, float* l1_d, uint64_t* l1_i, hipStream_t s);
-void launch_scan(int metric, int regs, uint32_t grid_items, const float4* arena, const uint64_t* ids,
+// One launch for the whole scan of a batch: grid_blocks bounds (wide items + narrow items / 4).
+size_t scan_wide_lds(uint32_t d4, uint32_t k);   // dynamic LDS of a wide-item block
+bool scan_wide_fits(uint32_t d4, uint32_t k);
+void launch_scan(int metric, int regs, int wide, uint32_t grid_blocks, const float4* arena, const uint64_t* ids,
                  const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
-                 const ScanItem* items, const uint32_t* counters, const uint32_t* sorted_pair,
-                 const uint32_t* part_base_sorted, uint32_t k, float* part_d, uint64_t* part_i,
-                 hipStream_t s);
+                 const ScanItem* items, const ScanItem* items_w, const uint32_t* counters,
+                 const uint32_t* sorted_pair, const uint32_t* part_base_sorted, uint32_t k, float* part_d,
+                 uint64_t* part_i, hipStream_t s);
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                        const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,
