@@ -107,6 +107,8 @@ struct vdb_ivf {
     int device = 0;
     uint64_t max_gpu_memory = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;          // narrow-item scan, concurrent with the wide items
+    hipEvent_t fork = nullptr, join = nullptr;
     std::mutex mu;
 
     DevBuf<float> cent_rm;   // [nlist][dp], zero pads
@@ -149,6 +151,9 @@ struct vdb_ivf {
             (void)hipEventDestroy(e.scan_end);
             (void)hipEventDestroy(e.end);
         }
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+        if (side) (void)hipStreamDestroy(side);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -190,12 +195,14 @@ struct vdb_ivf {
         }
         DevBuf<float4> na;
         DevBuf<uint64_t> ni;
-        const size_t vec4 = (size_t)blocks * d4 * 64;
+        // one slack block past the last list: the scan prefetches one chunk and one
+        // block of ids beyond the segment it streams
+        const size_t vec4 = (size_t)(blocks + 1) * d4 * 64;
         na.ensure(vec4);
-        ni.ensure((size_t)blocks * 64);
+        ni.ensure((size_t)(blocks + 1) * 64);
         if (blocks) {
             HIPCHECK(hipMemsetAsync(na.p, 0, vec4 * sizeof(float4), stream));
-            HIPCHECK(hipMemsetAsync(ni.p, 0xFF, (size_t)blocks * 64 * 8, stream));
+            HIPCHECK(hipMemsetAsync(ni.p, 0xFF, (size_t)(blocks + 1) * 64 * 8, stream));
         }
         if (arena_blocks && blocks) {
             DevBuf<uint64_t> doo, dno;
@@ -431,9 +438,19 @@ struct vdb_ivf {
         vdbk::launch_plan(probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? 1 : 0, items.p, items_w.p,
                           counters.p, sorted_pair.p, pbs.p, pbqp.p, nseg_qp.p, l1base.p, l1_items.p, stats.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
-        vdbk::launch_scan(metric, regs_k, wide ? 1 : 0, (uint32_t)(max_wide + (max_items + 3) / 4), arena.p, arena_ids.p,
-                          d_block_off.p, d_count_local.p, qpad.p, d4, items.p, items_w.p, counters.p, sorted_pair.p,
-                          pbs.p, k, part_d.p, part_i.p, s);
+        const vdbk::ScanArgs sa{arena.p, arena_ids.p, d_block_off.p, d_count_local.p, qpad.p, items.p, items_w.p,
+                                counters.p, sorted_pair.p, pbs.p, part_d.p, part_i.p, d4, k};
+        if (wide) {
+            // narrow items on the side stream fill the CUs the wide items leave idle
+            HIPCHECK(hipEventRecord(fork, s));
+            HIPCHECK(hipStreamWaitEvent(side, fork, 0));
+            vdbk::launch_scan_narrow(metric, regs_k, (uint32_t)((max_items + 3) / 4), sa, side);
+            HIPCHECK(hipEventRecord(join, side));
+            vdbk::launch_scan_wide(metric, (uint32_t)max_wide, sa, s);
+            HIPCHECK(hipStreamWaitEvent(s, join, 0));
+        } else {
+            vdbk::launch_scan_narrow(metric, regs_k, (uint32_t)((max_items + 3) / 4), sa, s);
+        }
         if (ev) HIPCHECK(hipEventRecord(ev->scan_end, s));
         vdbk::launch_merge_partials(regs_k, (uint32_t)max_l1, probes.p, d_count_global.p, nseg_qp.p, pbqp.p, l1base.p,
                                     l1_items.p, counters.p, part_d.p, part_i.p, k, l1_d.p, l1_i.p, s);
@@ -495,13 +512,18 @@ int vdb_ivf_create(const vdb_ivf_config* cfg, vdb_ivf** out) {
         try {
             h->dim = cfg->dimension;
             h->nlist = cfg->nlist;
-            h->d4 = (cfg->dimension + 3) / 4;
+            // float4 tiles per vector, zero-padded to whole scan chunks so every chunk
+            // load is unconditional (the +0.0f pad terms leave every sum's bits unchanged)
+            h->d4 = (cfg->dimension + 4 * vdbk::kTileAlign - 1) / (4 * vdbk::kTileAlign) * vdbk::kTileAlign;
             h->dp = h->d4 * 4;
             h->metric = cfg->metric;
             h->device = cfg->device;
             h->max_gpu_memory = cfg->max_gpu_memory;
             h->set_device();
             HIPCHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+            HIPCHECK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+            HIPCHECK(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
+            HIPCHECK(hipEventCreateWithFlags(&h->join, hipEventDisableTiming));
             h->cent_rm.ensure((size_t)h->nlist * h->dp);
             h->cent_il.ensure(cdiv(h->nlist, 64) * h->d4 * 64);
             HIPCHECK(hipMemsetAsync(h->cent_rm.p, 0, (size_t)h->nlist * h->dp * 4, h->stream));  // cpp:22

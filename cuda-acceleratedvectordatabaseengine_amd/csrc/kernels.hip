@@ -385,25 +385,47 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
 // Each query keeps a wave top-k of (dist, id); the segment's top-k becomes one
 // partial result of that (query, probe) pair.
 // ============================================================================
-struct ScanArgs {
-    const float4* __restrict__ arena;
-    const uint64_t* __restrict__ ids;
-    const uint64_t* __restrict__ block_off;
-    const uint32_t* __restrict__ count;
-    const float* __restrict__ qpad;
-    const ScanItem* __restrict__ items;
-    const ScanItem* __restrict__ items_w;
-    const uint32_t* __restrict__ counters;
-    const uint32_t* __restrict__ sorted_pair;
-    const uint32_t* __restrict__ part_base_sorted;
-    float* __restrict__ part_d;
-    uint64_t* __restrict__ part_i;
-    uint32_t d4;
-    uint32_t k;
-};
 
 constexpr int kNarrowChunk = VDB_NARROW_CHUNK;
 
+// Stream nb 64-vector blocks of one list segment through a wave, C float4 per lane
+// at a time, double-buffered: the next chunk is in flight while the current one is
+// consumed (and the next block's ids while a block is consumed), so a wave keeps HBM
+// reads outstanding while it computes. Tiles of consecutive blocks are contiguous
+// ([block][D4][64] float4) and 2C divides D4 (the layout pads D4), so the loads are
+// unconditional: the last prefetch reads one chunk and one id block past the
+// segment, which the arena's slack block keeps in bounds.
+//   compute(x, t0): consume tiles t0 .. t0+C-1 of the current block
+//   finish(j, id):  block j done; id = this lane's id slot in block j
+template <int C>
+__device__ __forceinline__ void load_chunk(float4 (&x)[C], const float4* vb) {
+#pragma unroll
+    for (int t = 0; t < C; ++t) x[t] = vb[(size_t)t * 64];
+}
+
+template <int C, class Compute, class Finish>
+__device__ __forceinline__ void stream_blocks(const float4* __restrict__ base, const uint64_t* __restrict__ ids,
+                                              uint32_t d4, uint32_t nb, Compute&& compute, Finish&& finish) {
+    float4 xa[C], xb[C];
+    const float4* p = base;
+    load_chunk<C>(xa, p);
+    uint64_t id_next = ids[0];
+    for (uint32_t j = 0; j < nb; ++j) {
+        const uint64_t id = id_next;
+        id_next = ids[(size_t)(j + 1) * 64];
+        for (uint32_t t0 = 0; t0 < d4; t0 += 2 * C) {
+            load_chunk<C>(xb, p + (size_t)C * 64);
+            compute(xa, t0);
+            load_chunk<C>(xa, p + (size_t)2 * C * 64);
+            compute(xb, t0 + C);
+            p += (size_t)2 * C * 64;
+        }
+        finish(j, id);
+    }
+}
+
+// One narrow wave-item: one segment of a small list against G <= 4 queries whose
+// dims are wave-uniform scalar loads; each query's top-k lives in registers.
 template <int R, int G, int M>
 __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) {
     const int lane = lane_id();
@@ -428,38 +450,24 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
     WaveTopK<R> tk[G];
     float kd[G];
     uint64_t ki[G];
+    float acc[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         tk[g].init();
         kd[g] = __builtin_inff();
         ki[g] = kNoId;
+        acc[g] = 0.0f;
     }
-
-    for (uint32_t j = 0; j < nb; ++j) {
-        const float4* vb = a.arena + (b0 + j) * d4 * 64 + lane;
-        float acc[G];
+    // one HBM read of a list vector feeds G distance chains, each summed in d order
+    auto compute = [&](const float4(&x)[kNarrowChunk], uint32_t t0) {
 #pragma unroll
-        for (int g = 0; g < G; ++g) acc[g] = 0.0f;
-        // Hold kChunkTiles float4 of this lane's vector in registers and sweep every
-        // query of the group over them: one HBM read feeds G distance chains, each
-        // still summed in d order.
-        uint32_t t0 = 0;
-        for (; t0 + kNarrowChunk <= d4; t0 += kNarrowChunk) {
-            float4 x[kNarrowChunk];
+        for (int g = 0; g < G; ++g) {
+            const float4* qg = q[g] + t0;
 #pragma unroll
-            for (int t = 0; t < kNarrowChunk; ++t) x[t] = vb[(size_t)(t0 + t) * 64];
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const float4* qg = q[g] + t0;
-#pragma unroll
-                for (int t = 0; t < kNarrowChunk; ++t) acc[g] = acc4<M>(acc[g], qg[t], x[t]);
-            }
+            for (int t = 0; t < kNarrowChunk; ++t) acc[g] = acc4<M>(acc[g], qg[t], x[t]);
         }
-        for (; t0 < d4; ++t0) {
-            const float4 x = vb[(size_t)t0 * 64];
-#pragma unroll
-            for (int g = 0; g < G; ++g) acc[g] = acc4<M>(acc[g], q[g][t0], x);
-        }
+    };
+    auto finish = [&](uint32_t j, uint64_t id) {
         const bool valid = j * 64 + lane < nv;
         bool want[G];
         bool any = false;
@@ -470,12 +478,15 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
             any |= want[g];
         }
         if (__ballot(any)) {
-            const uint64_t vid = valid ? a.ids[(b0 + j) * 64 + lane] : kNoId;
+            const uint64_t vid = valid ? id : kNoId;
 #pragma unroll
             for (int g = 0; g < G; ++g)
                 if (g < np) offer_lanes<R>(tk[g], want[g], acc[g], vid, k, kd[g], ki[g]);
         }
-    }
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[g] = 0.0f;
+    };
+    stream_blocks<kNarrowChunk>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         if (g >= np) break;
@@ -492,45 +503,49 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-template <int M>
-__device__ __forceinline__ f2 dist_term2(f2 acc, f2 q, float x) {
-    const f2 xx = {x, x};
+// Packed term for two queries q = (qa, qb) against one list value held in half H of
+// the aligned register pair x (H = 0: x.lo, 1: x.hi). The broadcast is an op_sel on
+// the pair the value was loaded into, so a float4 of list data is consumed in place
+// (the compiler would otherwise copy the odd halves into fresh pairs and, with them,
+// wait on a prefetch it just issued). Sub, mul, add stay separate instructions:
+// each half rounds exactly like the scalar diff = a - b; acc = acc + diff * diff.
+template <int H>
+__device__ __forceinline__ f2 pk_sub_bcast(f2 q, f2 x) {
+    f2 r;
+    if constexpr (H == 0)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(q), "v"(x));
+    else
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(q), "v"(x));
+    return r;
+}
+template <int H>
+__device__ __forceinline__ f2 pk_mul_bcast(f2 q, f2 x) {
+    f2 r;
+    if constexpr (H == 0)
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(q), "v"(x));
+    else
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(q), "v"(x));
+    return r;
+}
+
+template <int M, int H>
+__device__ __forceinline__ f2 dist_term2(f2 acc, f2 q, f2 x) {
     if constexpr (M == kL2) {
-        const f2 diff = q - xx;
+        const f2 diff = pk_sub_bcast<H>(q, x);
         return acc + diff * diff;
     } else if constexpr (M == kIP) {
-        return acc + q * xx;
+        return acc + pk_mul_bcast<H>(q, x);
     } else {
         return acc;
     }
 }
 
-// Top-k list of one query kept in LDS: k (dist, id) entries, ascending. Loads it
-// into the lane-distributed form (lanes >= k empty), offers the lanes in `mask`,
-// stores it back and returns the new k-th distance. Shared by every query slot
-// (runtime index) so the rare insertion path exists once in the code.
-__device__ __noinline__ float lds_topk_offer(float* sd, uint64_t* si, int k, uint64_t mask, float cd, uint64_t cid) {
-    const int lane = lane_id();
-    WaveTopK<1> tk;
-    tk.d[0] = lane < k ? sd[lane] : __builtin_inff();
-    tk.id[0] = lane < k ? si[lane] : kNoId;
-    float kd;
-    uint64_t ki;
-    tk.at(k - 1, kd, ki);
-    offer_lanes<1>(tk, ((mask >> lane) & 1ull) != 0, cd, cid, k, kd, ki);
-    if (lane < k) {
-        sd[lane] = tk.d[0];
-        si[lane] = tk.id[0];
-    }
-    return kd;
-}
-
 // One wave of a wide item: segment it.seg * 4 + wave of list it.list against GP
-// query pairs read from LDS as interleaved pairs (q[2p][d], q[2p+1][d]). Each lane
-// keeps kChunkTiles float4 of its list vector in registers and runs two queries per
-// packed instruction (v_pk_add_f32 / v_pk_mul_f32 round each half exactly like the
-// scalar ops); every query's sum still runs in d order. Per query only the k-th
-// distance lives in registers; the top-k lists live in LDS (tk_d / tk_i).
+// query pairs read from LDS as interleaved pairs (q[2p][d], q[2p+1][d]). Two queries
+// run per packed instruction (v_pk_add_f32 / v_pk_mul_f32 round each half exactly
+// like the scalar ops); every query's sum still runs in d order. Per query only the
+// k-th distance lives in registers; the top-k lists live in LDS (tk_d / tk_i), and
+// the insertion code exists once, looping over the queries that have candidates.
 template <int GP, int M>
 __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds, float* tk_d,
                                                uint64_t* tk_i) {
@@ -553,59 +568,69 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
         tk_i[e] = kNoId;
     }
     float kd[G];
+    f2 acc[GP];
 #pragma unroll
     for (int g = 0; g < G; ++g) kd[g] = __builtin_inff();
-    for (uint32_t j = 0; j < nb; ++j) {
-        const float4* vb = a.arena + (b0 + j) * d4 * 64 + lane;
-        f2 acc[GP];
 #pragma unroll
-        for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
-        uint32_t t0 = 0;
-        for (; t0 + kChunkTiles <= d4; t0 += kChunkTiles) {
-            float4 x[kChunkTiles];
+    for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
+
+    auto compute = [&](const float4(&x)[kChunkTiles], uint32_t t0) {
 #pragma unroll
-            for (int t = 0; t < kChunkTiles; ++t) x[t] = vb[(size_t)(t0 + t) * 64];
+        for (int p = 0; p < GP; ++p) {
+            const float4* qp = qlds + ((size_t)p * d4 + t0) * 2;
 #pragma unroll
-            for (int p = 0; p < GP; ++p) {
-                const float4* qp = qlds + ((size_t)p * d4 + t0) * 2;
-#pragma unroll
-                for (int t = 0; t < kChunkTiles; ++t) {
-                    const float4 lo = qp[2 * t], hi = qp[2 * t + 1];
-                    acc[p] = dist_term2<M>(acc[p], f2{lo.x, lo.y}, x[t].x);
-                    acc[p] = dist_term2<M>(acc[p], f2{lo.z, lo.w}, x[t].y);
-                    acc[p] = dist_term2<M>(acc[p], f2{hi.x, hi.y}, x[t].z);
-                    acc[p] = dist_term2<M>(acc[p], f2{hi.z, hi.w}, x[t].w);
-                }
+            for (int t = 0; t < kChunkTiles; ++t) {
+                const float4 lo = qp[2 * t], hi = qp[2 * t + 1];
+                const f2 xlo = {x[t].x, x[t].y}, xhi = {x[t].z, x[t].w};
+                acc[p] = dist_term2<M, 0>(acc[p], f2{lo.x, lo.y}, xlo);
+                acc[p] = dist_term2<M, 1>(acc[p], f2{lo.z, lo.w}, xlo);
+                acc[p] = dist_term2<M, 0>(acc[p], f2{hi.x, hi.y}, xhi);
+                acc[p] = dist_term2<M, 1>(acc[p], f2{hi.z, hi.w}, xhi);
             }
         }
-        for (; t0 < d4; ++t0) {
-            const float4 x = vb[(size_t)t0 * 64];
-#pragma unroll
-            for (int p = 0; p < GP; ++p) {
-                const float4 lo = qlds[((size_t)p * d4 + t0) * 2], hi = qlds[((size_t)p * d4 + t0) * 2 + 1];
-                acc[p] = dist_term2<M>(acc[p], f2{lo.x, lo.y}, x.x);
-                acc[p] = dist_term2<M>(acc[p], f2{lo.z, lo.w}, x.y);
-                acc[p] = dist_term2<M>(acc[p], f2{hi.x, hi.y}, x.z);
-                acc[p] = dist_term2<M>(acc[p], f2{hi.z, hi.w}, x.w);
-            }
-        }
+    };
+    auto finish = [&](uint32_t j, uint64_t id) {
         const bool valid = j * 64 + lane < nv;
-        uint64_t vid = kNoId;
-        bool have_id = false;
+        uint32_t pend = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            if (g >= np) break;
             const float dist = dist_finish<M>((g & 1) ? acc[g >> 1].y : acc[g >> 1].x);
-            const uint64_t mask = __ballot(valid && dist <= kd[g]);
-            if (mask) {
-                if (!have_id) {
-                    vid = valid ? a.ids[(b0 + j) * 64 + lane] : kNoId;
-                    have_id = true;
-                }
-                kd[g] = lds_topk_offer(tk_d + g * k, tk_i + g * k, k, mask, dist, vid);
-            }
+            if (g < np && __ballot(valid && dist <= kd[g])) pend |= 1u << g;
         }
-    }
+        if (pend) {
+            const uint64_t vid = valid ? id : kNoId;
+            do {
+                const int gs = __builtin_ctz(pend);
+                pend &= pend - 1;
+                float dist = 0.0f, kdg = 0.0f;
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    if (g == gs) {
+                        dist = dist_finish<M>((g & 1) ? acc[g >> 1].y : acc[g >> 1].x);
+                        kdg = kd[g];
+                    }
+                float* sd = tk_d + gs * k;
+                uint64_t* si = tk_i + gs * k;
+                WaveTopK<1> tk;
+                tk.d[0] = lane < k ? sd[lane] : __builtin_inff();
+                tk.id[0] = lane < k ? si[lane] : kNoId;
+                float nkd;
+                uint64_t nki;
+                tk.at(k - 1, nkd, nki);
+                offer_lanes<1>(tk, valid && dist <= kdg, dist, vid, k, nkd, nki);
+                if (lane < k) {
+                    sd[lane] = tk.d[0];
+                    si[lane] = tk.id[0];
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    if (g == gs) kd[g] = nkd;
+            } while (pend);
+        }
+#pragma unroll
+        for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
+    };
+    stream_blocks<kChunkTiles>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
     for (int g = 0; g < np; ++g) {
         const uint32_t part = a.part_base_sorted[it.pair_start + g] + seg;
         if (lane < k) {
@@ -628,51 +653,54 @@ __device__ __forceinline__ void scan_narrow(const ScanArgs& a, const ScanItem it
     }
 }
 
-// ivf_scan: the fine scan (search_list_cpu, cpp:347-370) of one batch in ONE launch.
-// Workgroup b < n_wide takes wide item b (a large list: 4 segments x up to 16 of its
-// queries, staged once in LDS); the remaining workgroups take 4 narrow items each
-// (small lists, one segment x <= 4 queries per wave, queries via scalar loads).
+// ivf_scan_narrow: the fine scan (search_list_cpu, cpp:347-370) of the batch's small
+// lists: each wave takes one narrow item (one segment x <= 4 queries, queries via
+// scalar loads, top-k in registers).
 template <int R, int M>
-__global__ __launch_bounds__(256) void ivf_scan(ScanArgs a) {
-    // Dynamic LDS (wide items, R == 1): [kWideGroup/2][d4][2] float4 of staged query
-    // pairs, then per wave kWideGroup x k top-k ids (u64) and distances (f32).
+__global__ __launch_bounds__(256) void ivf_scan_narrow(ScanArgs a) {
+    const uint32_t n_narrow = a.counters[0];
+    const uint32_t nblocks = (n_narrow + 3) / 4;
+    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        const uint32_t idx = b * 4 + wave_index();
+        if (idx < n_narrow) scan_narrow<R, M>(a, a.items[idx]);
+    }
+}
+
+// ivf_scan_wide: the large lists. Workgroup b takes wide item b: 4 consecutive
+// segments (one per wave) x up to 16 of the list's queries, staged once in LDS.
+template <int M>
+__global__ __launch_bounds__(256) void ivf_scan_wide(ScanArgs a) {
+    // Dynamic LDS: [kWideGroup/2][d4][2] float4 of staged query pairs, then per wave
+    // kWideGroup x k top-k ids (u64), then the same for distances (f32).
     extern __shared__ __attribute__((aligned(16))) float4 qlds[];
     const uint32_t d4 = a.d4;
     uint64_t* tk_i = (uint64_t*)(qlds + (size_t)(kWideGroup / 2) * d4 * 2) + (size_t)wave_index() * kWideGroup * a.k;
     float* tk_d = (float*)((uint64_t*)(qlds + (size_t)(kWideGroup / 2) * d4 * 2) + (size_t)4 * kWideGroup * a.k) +
                   (size_t)wave_index() * kWideGroup * a.k;
-    const uint32_t n_wide = a.counters[3], n_narrow = a.counters[0];
-    const uint32_t nblocks = n_wide + (n_narrow + 3) / 4;
-    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-        if (b >= n_wide) {
-            const uint32_t idx = (b - n_wide) * 4 + wave_index();
-            if (idx < n_narrow) scan_narrow<R, M>(a, a.items[idx]);
-            continue;
+    const uint32_t n_wide = a.counters[3];
+    for (uint32_t b = blockIdx.x; b < n_wide; b += gridDim.x) {
+        const ScanItem it = a.items_w[b];
+        const int np = (int)it.npairs;
+        const int gp = (np + 1) / 2;
+        const int gpv = gp <= 1 ? 1 : gp <= 2 ? 2 : gp <= 3 ? 3 : gp <= 4 ? 4 : gp <= 6 ? 6 : 8;
+        for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
+            const uint32_t p = e / d4, t = e - p * d4;
+            const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
+            const float4 qa = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + ga] >> 16) * d4 * 4))[t];
+            const float4 qb = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + gb] >> 16) * d4 * 4))[t];
+            qlds[(p * d4 + t) * 2 + 0] = make_float4(qa.x, qb.x, qa.y, qb.y);
+            qlds[(p * d4 + t) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
         }
-        if constexpr (R == 1) {
-            const ScanItem it = a.items_w[b];
-            const int np = (int)it.npairs;
-            const int gp = (np + 1) / 2;
-            const int gpv = gp <= 1 ? 1 : gp <= 2 ? 2 : gp <= 3 ? 3 : gp <= 4 ? 4 : gp <= 6 ? 6 : 8;
-            for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
-                const uint32_t p = e / d4, t = e - p * d4;
-                const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
-                const float4 qa = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + ga] >> 16) * d4 * 4))[t];
-                const float4 qb = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + gb] >> 16) * d4 * 4))[t];
-                qlds[(p * d4 + t) * 2 + 0] = make_float4(qa.x, qb.x, qa.y, qb.y);
-                qlds[(p * d4 + t) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
-            }
-            __syncthreads();
-            switch (gpv) {
-                case 1: scan_wide_wave<1, M>(a, it, qlds, tk_d, tk_i); break;
-                case 2: scan_wide_wave<2, M>(a, it, qlds, tk_d, tk_i); break;
-                case 3: scan_wide_wave<3, M>(a, it, qlds, tk_d, tk_i); break;
-                case 4: scan_wide_wave<4, M>(a, it, qlds, tk_d, tk_i); break;
-                case 6: scan_wide_wave<6, M>(a, it, qlds, tk_d, tk_i); break;
-                default: scan_wide_wave<8, M>(a, it, qlds, tk_d, tk_i); break;
-            }
-            __syncthreads();  // qlds is restaged by the next wide item
+        __syncthreads();
+        switch (gpv) {
+            case 1: scan_wide_wave<1, M>(a, it, qlds, tk_d, tk_i); break;
+            case 2: scan_wide_wave<2, M>(a, it, qlds, tk_d, tk_i); break;
+            case 3: scan_wide_wave<3, M>(a, it, qlds, tk_d, tk_i); break;
+            case 4: scan_wide_wave<4, M>(a, it, qlds, tk_d, tk_i); break;
+            case 6: scan_wide_wave<6, M>(a, it, qlds, tk_d, tk_i); break;
+            default: scan_wide_wave<8, M>(a, it, qlds, tk_d, tk_i); break;
         }
+        __syncthreads();  // qlds is restaged by the next wide item
     }
 }
 
@@ -1248,47 +1276,46 @@ void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes
 #undef VDB_MP
 }
 
-template <int R>
-static void scan_dispatch_metric(int metric, uint32_t grid, size_t lds, const ScanArgs& a, hipStream_t s) {
-    if (metric == kL2) ivf_scan<R, kL2><<<grid, 256, lds, s>>>(a);
-    else if (metric == kIP) ivf_scan<R, kIP><<<grid, 256, lds, s>>>(a);
-    else ivf_scan<R, kCos><<<grid, 256, lds, s>>>(a);
-}
-
 size_t scan_wide_lds(uint32_t d4, uint32_t k) {
     return (size_t)(kWideGroup / 2) * d4 * 2 * sizeof(float4) + (size_t)4 * kWideGroup * k * (sizeof(float) + sizeof(uint64_t));
 }
 
-bool scan_wide_fits(uint32_t d4, uint32_t k) { return scan_wide_lds(d4, k) <= kLdsBytes; }
+bool scan_wide_fits(uint32_t d4, uint32_t k) { return k <= 64 && scan_wide_lds(d4, k) <= kLdsBytes; }
 
-void launch_scan(int metric, int regs, int wide, uint32_t grid_blocks, const float4* arena, const uint64_t* ids,
-                 const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
-                 const ScanItem* items, const ScanItem* items_w, const uint32_t* counters,
-                 const uint32_t* sorted_pair, const uint32_t* part_base_sorted, uint32_t k, float* part_d,
-                 uint64_t* part_i, hipStream_t s) {
+void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
     if (!grid_blocks) return;
-    ScanArgs a{arena, ids, block_off, count_local, qpad, items, items_w, counters, sorted_pair, part_base_sorted,
-               part_d, part_i, d4, k};
-    size_t lds = 0;
-    if (wide && regs == 1) {
-        static const bool raised = [] {
-            // wide items stage up to 16 queries in LDS: allow the whole 160 KB of a CU
-            hipFuncSetAttribute((const void*)ivf_scan<1, kL2>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-            hipFuncSetAttribute((const void*)ivf_scan<1, kIP>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-            hipFuncSetAttribute((const void*)ivf_scan<1, kCos>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-            return true;
-        }();
-        (void)raised;
-        lds = scan_wide_lds(d4, k);
-    }
-    const uint32_t grid = launch_grid(grid_blocks, 1);
+    const uint32_t g = launch_grid(grid_blocks, 1);
+#define VDB_SN(R)                                                             \
+    do {                                                                      \
+        if (metric == kL2) ivf_scan_narrow<R, kL2><<<g, 256, 0, s>>>(a);      \
+        else if (metric == kIP) ivf_scan_narrow<R, kIP><<<g, 256, 0, s>>>(a); \
+        else ivf_scan_narrow<R, kCos><<<g, 256, 0, s>>>(a);                   \
+    } while (0)
     switch (regs) {
-        case 1: scan_dispatch_metric<1>(metric, grid, lds, a, s); break;
-        case 2: scan_dispatch_metric<2>(metric, grid, 0, a, s); break;
-        case 4: scan_dispatch_metric<4>(metric, grid, 0, a, s); break;
-        case 8: scan_dispatch_metric<8>(metric, grid, 0, a, s); break;
-        default: scan_dispatch_metric<16>(metric, grid, 0, a, s); break;
+        case 1: VDB_SN(1); break;
+        case 2: VDB_SN(2); break;
+        case 4: VDB_SN(4); break;
+        case 8: VDB_SN(8); break;
+        default: VDB_SN(16); break;
     }
+#undef VDB_SN
+}
+
+void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
+    if (!grid_blocks) return;
+    static const bool raised = [] {
+        // wide items stage up to 16 queries in LDS: allow the whole 160 KB of a CU
+        hipFuncSetAttribute((const void*)ivf_scan_wide<kL2>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        hipFuncSetAttribute((const void*)ivf_scan_wide<kIP>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        hipFuncSetAttribute((const void*)ivf_scan_wide<kCos>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        return true;
+    }();
+    (void)raised;
+    const size_t lds = scan_wide_lds(a.d4, a.k);
+    const uint32_t g = launch_grid(grid_blocks, 1);
+    if (metric == kL2) ivf_scan_wide<kL2><<<g, 256, lds, s>>>(a);
+    else if (metric == kIP) ivf_scan_wide<kIP><<<g, 256, lds, s>>>(a);
+    else ivf_scan_wide<kCos><<<g, 256, lds, s>>>(a);
 }
 
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const uint32_t* nseg_qp,

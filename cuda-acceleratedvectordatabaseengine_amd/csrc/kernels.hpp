@@ -16,7 +16,8 @@ namespace vdbk {
 
 constexpr int kSegBlocks = 8;              // 64-vector blocks per scan work item
 constexpr int kSegVectors = kSegBlocks * 64;
-constexpr int kChunkTiles = 8;             // float4 of a list vector held in registers (32 dims)
+constexpr int kChunkTiles = 8;             // float4 of a list vector per wide-scan chunk (32 dims)
+constexpr int kTileAlign = 2 * kChunkTiles; // D4 is padded to whole double-buffered chunk pairs
 constexpr int kMergeFan = 32;              // segment partials folded per level-1 merge wave
 constexpr int kWideGroup = 16;             // max pairs per wide scan item (large lists)
 constexpr int kWideMinSeg = 4;             // lists with >= 4 segments are scanned by wide items
@@ -57,14 +58,28 @@ void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes
                            const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                            const uint2* l1_items, const uint32_t* counters, const float* part_d,
                            const uint64_t* part_i, uint32_t k, float* l1_d, uint64_t* l1_i, hipStream_t s);
-// One launch for the whole scan of a batch: grid_blocks bounds (wide items + narrow items / 4).
+// Fine scan of one batch (kernels.hip): small lists as narrow items (one wave each),
+// large lists as wide items (one workgroup: 4 segments x <= 16 queries in LDS).
+struct ScanArgs {
+    const float4* __restrict__ arena;
+    const uint64_t* __restrict__ ids;
+    const uint64_t* __restrict__ block_off;
+    const uint32_t* __restrict__ count;
+    const float* __restrict__ qpad;
+    const ScanItem* __restrict__ items;
+    const ScanItem* __restrict__ items_w;
+    const uint32_t* __restrict__ counters;
+    const uint32_t* __restrict__ sorted_pair;
+    const uint32_t* __restrict__ part_base_sorted;
+    float* __restrict__ part_d;
+    uint64_t* __restrict__ part_i;
+    uint32_t d4;
+    uint32_t k;
+};
 size_t scan_wide_lds(uint32_t d4, uint32_t k);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k);
-void launch_scan(int metric, int regs, int wide, uint32_t grid_blocks, const float4* arena, const uint64_t* ids,
-                 const uint64_t* block_off, const uint32_t* count_local, const float* qpad, uint32_t d4,
-                 const ScanItem* items, const ScanItem* items_w, const uint32_t* counters,
-                 const uint32_t* sorted_pair, const uint32_t* part_base_sorted, uint32_t k, float* part_d,
-                 uint64_t* part_i, hipStream_t s);
+void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
+void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                        const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,
