@@ -13,12 +13,11 @@
 
 #include <cfloat>
 
+#include <type_traits>
+
 #include "kernels.hpp"
 #include "wave_topk.hpp"
 
-#ifndef VDB_NARROW_CHUNK
-#define VDB_NARROW_CHUNK 4
-#endif
 
 namespace vdbk {
 
@@ -386,39 +385,42 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
 // partial result of that (query, probe) pair.
 // ============================================================================
 
-constexpr int kNarrowChunk = VDB_NARROW_CHUNK;
 
-// Stream nb 64-vector blocks of one list segment through a wave, C float4 per lane
-// at a time, double-buffered: the next chunk is in flight while the current one is
-// consumed (and the next block's ids while a block is consumed), so a wave keeps HBM
-// reads outstanding while it computes. Tiles of consecutive blocks are contiguous
-// ([block][D4][64] float4) and 2C divides D4 (the layout pads D4), so the loads are
-// unconditional: the last prefetch reads one chunk and one id block past the
-// segment, which the arena's slack block keeps in bounds.
-//   compute(x, t0): consume tiles t0 .. t0+C-1 of the current block
-//   finish(j, id):  block j done; id = this lane's id slot in block j
-template <int C>
-__device__ __forceinline__ void load_chunk(float4 (&x)[C], const float4* vb) {
-#pragma unroll
-    for (int t = 0; t < C; ++t) x[t] = vb[(size_t)t * 64];
+// Stream nb 64-vector blocks of one list segment through a wave as a tile pipeline:
+// T float4 registers per lane hold the next T tiles, and each tile's register is
+// refilled with the tile T ahead right after it is consumed, so T-1 wave-loads
+// (1 KiB each) stay in flight while the wave computes. Tiles of consecutive blocks
+// are contiguous ([block][D4][64] float4) and T divides D4 (the layout pads D4), so
+// every load is unconditional: the pipeline runs T tiles (and one id block) past
+// the segment, which the arena's slack block keeps in bounds.
+//   compute(x, t): consume tile t (0 <= t < d4) of the current block
+//   finish(j, id): block j done; id = this lane's id slot in block j
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
 }
 
-template <int C, class Compute, class Finish>
+template <int T, class Compute, class Finish>
 __device__ __forceinline__ void stream_blocks(const float4* __restrict__ base, const uint64_t* __restrict__ ids,
                                               uint32_t d4, uint32_t nb, Compute&& compute, Finish&& finish) {
-    float4 xa[C], xb[C];
+    float4 x[T];
     const float4* p = base;
-    load_chunk<C>(xa, p);
+#pragma unroll
+    for (int t = 0; t < T; ++t) x[t] = p[(size_t)t * 64];
     uint64_t id_next = ids[0];
     for (uint32_t j = 0; j < nb; ++j) {
         const uint64_t id = id_next;
         id_next = ids[(size_t)(j + 1) * 64];
-        for (uint32_t t0 = 0; t0 < d4; t0 += 2 * C) {
-            load_chunk<C>(xb, p + (size_t)C * 64);
-            compute(xa, t0);
-            load_chunk<C>(xa, p + (size_t)2 * C * 64);
-            compute(xb, t0 + C);
-            p += (size_t)2 * C * 64;
+        for (uint32_t t0 = 0; t0 < d4; t0 += T) {
+            static_for<0, T>([&](auto u) {
+                constexpr int t = decltype(u)::value;
+                compute(x[t], t0 + t, u);
+                x[t] = p[(size_t)(T + t) * 64];
+            });
+            p += (size_t)T * 64;
         }
         finish(j, id);
     }
@@ -459,13 +461,9 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
         acc[g] = 0.0f;
     }
     // one HBM read of a list vector feeds G distance chains, each summed in d order
-    auto compute = [&](const float4(&x)[kNarrowChunk], uint32_t t0) {
+    auto compute = [&](const float4 x, uint32_t t, auto) {
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float4* qg = q[g] + t0;
-#pragma unroll
-            for (int t = 0; t < kNarrowChunk; ++t) acc[g] = acc4<M>(acc[g], qg[t], x[t]);
-        }
+        for (int g = 0; g < G; ++g) acc[g] = acc4<M>(acc[g], q[g][t], x);
     };
     auto finish = [&](uint32_t j, uint64_t id) {
         const bool valid = j * 64 + lane < nv;
@@ -486,7 +484,7 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
 #pragma unroll
         for (int g = 0; g < G; ++g) acc[g] = 0.0f;
     };
-    stream_blocks<kNarrowChunk>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
+    stream_blocks<kTilePipeNarrow>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         if (g >= np) break;
@@ -574,19 +572,28 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
 #pragma unroll
     for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
 
-    auto compute = [&](const float4(&x)[kChunkTiles], uint32_t t0) {
+    // Query pairs of tile t sit at qlds[(t * GP + p) * 2 + {0, 1}]: one address per
+    // tile, the pairs at immediate offsets. Each pair's registers are refilled with
+    // the next tile's pair as soon as they are consumed, so every LDS read has a whole
+    // tile of arithmetic to land in.
+    float4 qb[GP][2];
+    {
+        const float4* src = qlds;
+#pragma unroll
+        for (int p = 0; p < GP; ++p) qb[p][0] = src[2 * p], qb[p][1] = src[2 * p + 1];
+    }
+    auto compute = [&](const float4 x, uint32_t t, auto) {
+        const float4* nxt = qlds + (size_t)(t + 1 == d4 ? 0 : t + 1) * GP * 2;
+        const f2 xlo = {x.x, x.y}, xhi = {x.z, x.w};
 #pragma unroll
         for (int p = 0; p < GP; ++p) {
-            const float4* qp = qlds + ((size_t)p * d4 + t0) * 2;
-#pragma unroll
-            for (int t = 0; t < kChunkTiles; ++t) {
-                const float4 lo = qp[2 * t], hi = qp[2 * t + 1];
-                const f2 xlo = {x[t].x, x[t].y}, xhi = {x[t].z, x[t].w};
-                acc[p] = dist_term2<M, 0>(acc[p], f2{lo.x, lo.y}, xlo);
-                acc[p] = dist_term2<M, 1>(acc[p], f2{lo.z, lo.w}, xlo);
-                acc[p] = dist_term2<M, 0>(acc[p], f2{hi.x, hi.y}, xhi);
-                acc[p] = dist_term2<M, 1>(acc[p], f2{hi.z, hi.w}, xhi);
-            }
+            const float4 lo = qb[p][0], hi = qb[p][1];
+            acc[p] = dist_term2<M, 0>(acc[p], f2{lo.x, lo.y}, xlo);
+            acc[p] = dist_term2<M, 1>(acc[p], f2{lo.z, lo.w}, xlo);
+            acc[p] = dist_term2<M, 0>(acc[p], f2{hi.x, hi.y}, xhi);
+            acc[p] = dist_term2<M, 1>(acc[p], f2{hi.z, hi.w}, xhi);
+            qb[p][0] = nxt[2 * p];
+            qb[p][1] = nxt[2 * p + 1];
         }
     };
     auto finish = [&](uint32_t j, uint64_t id) {
@@ -630,7 +637,7 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
 #pragma unroll
         for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
     };
-    stream_blocks<kChunkTiles>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
+    stream_blocks<kTilePipe>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
     for (int g = 0; g < np; ++g) {
         const uint32_t part = a.part_base_sorted[it.pair_start + g] + seg;
         if (lane < k) {
@@ -670,7 +677,7 @@ __global__ __launch_bounds__(256) void ivf_scan_narrow(ScanArgs a) {
 // segments (one per wave) x up to 16 of the list's queries, staged once in LDS.
 template <int M>
 __global__ __launch_bounds__(256) void ivf_scan_wide(ScanArgs a) {
-    // Dynamic LDS: [kWideGroup/2][d4][2] float4 of staged query pairs, then per wave
+    // Dynamic LDS: [d4][gpv][2] float4 of staged query pairs (tile-major), then per wave
     // kWideGroup x k top-k ids (u64), then the same for distances (f32).
     extern __shared__ __attribute__((aligned(16))) float4 qlds[];
     const uint32_t d4 = a.d4;
@@ -684,12 +691,12 @@ __global__ __launch_bounds__(256) void ivf_scan_wide(ScanArgs a) {
         const int gp = (np + 1) / 2;
         const int gpv = gp <= 1 ? 1 : gp <= 2 ? 2 : gp <= 3 ? 3 : gp <= 4 ? 4 : gp <= 6 ? 6 : 8;
         for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
-            const uint32_t p = e / d4, t = e - p * d4;
+            const uint32_t t = e / gpv, p = e - t * gpv;
             const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
             const float4 qa = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + ga] >> 16) * d4 * 4))[t];
             const float4 qb = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + gb] >> 16) * d4 * 4))[t];
-            qlds[(p * d4 + t) * 2 + 0] = make_float4(qa.x, qb.x, qa.y, qb.y);
-            qlds[(p * d4 + t) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
+            qlds[(t * gpv + p) * 2 + 0] = make_float4(qa.x, qb.x, qa.y, qb.y);
+            qlds[(t * gpv + p) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
         }
         __syncthreads();
         switch (gpv) {

@@ -16,8 +16,9 @@ namespace vdbk {
 
 constexpr int kSegBlocks = 8;              // 64-vector blocks per scan work item
 constexpr int kSegVectors = kSegBlocks * 64;
-constexpr int kChunkTiles = 8;             // float4 of a list vector per wide-scan chunk (32 dims)
-constexpr int kTileAlign = 2 * kChunkTiles; // D4 is padded to whole double-buffered chunk pairs
+constexpr int kTilePipe = 16;              // float4 tiles of a list vector in flight per lane (scan)
+constexpr int kTilePipeNarrow = 4;         // the same for narrow items (queries held in SGPRs)
+constexpr int kTileAlign = kTilePipe;      // D4 is padded to whole pipeline rounds
 constexpr int kMergeFan = 32;              // segment partials folded per level-1 merge wave
 constexpr int kWideGroup = 16;             // max pairs per wide scan item (large lists)
 constexpr int kWideMinSeg = 4;             // lists with >= 4 segments are scanned by wide items
