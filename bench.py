@@ -74,8 +74,6 @@ def build_index(vdb, args, device, rank, world):
     t2 = time.perf_counter()
     del data, ids
     torch.cuda.empty_cache()
-    if world > 1:
-        idx.set_shard(rank, world)
     log(rank, f"[bench] train {t1 - t0:.2f}s add {t2 - t1:.2f}s; index {idx.get_gpu_memory_usage() / 2**30:.1f} GiB on rank 0")
     return idx, {"train_s": round(t1 - t0, 3), "add_s": round(t2 - t1, 3)}
 
@@ -140,6 +138,13 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--cpu-call", type=int, default=4, help="queries per oracle search() call")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--check-batches", type=int, default=4,
+                    help="N>1: timed batches checked bit-for-bit against the unsharded index")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the multi-rank path with host-staged exchange")
+    ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (one-GPU rehearsal)")
+    ap.add_argument("--inflight", type=int, default=2, help="batches in flight (streams) in the timed region")
+    ap.add_argument("--prof-steps", type=int, default=10, help="single-stream steps timed per launch for the roofline")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per ivf_scan launch for this workload (or null)")
     args = ap.parse_args()
@@ -147,10 +152,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", local_rank)
+    device = torch.device("cuda", 0 if args.same_device else local_rank)
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
     vdb = load_vdb()
     # Every kernel of this run (torch's and the engine's) goes to one explicit stream.
     with torch.cuda.stream(torch.cuda.Stream(device)):
@@ -162,34 +170,62 @@ def main():
 def run(vdb, args, device, rank, world):
     idx, build_info = build_index(vdb, args, device, rank, world)
     B, k = args.batch, args.k
-    nq = (args.warmup + args.steps) * B
-    stream = torch.cuda.current_stream()
+    nq = (args.warmup + args.steps + args.prof_steps) * B
+    main_stream = torch.cuda.current_stream()
     queries = torch.empty((nq, args.dim), dtype=torch.float32, device=device)
-    vdb.gen_normal_device(queries.data_ptr(), nq * args.dim, seed=12346, stream=stream.cuda_stream)
+    vdb.gen_normal_device(queries.data_ptr(), nq * args.dim, seed=12346, stream=main_stream.cuda_stream)
     out_d = torch.empty((nq, k), dtype=torch.float32, device=device)
     out_i = torch.empty((nq, k), dtype=torch.int64, device=device)
-    part_d = torch.empty((B, k), dtype=torch.float32, device=device)
-    part_i = torch.empty((B, k), dtype=torch.int64, device=device)
-    gat_d = torch.empty((world, B, k), dtype=torch.float32, device=device)
-    gat_i = torch.empty((world, B, k), dtype=torch.int64, device=device)
+    check = None
+    if world > 1:
+        # Reference for the end-to-end check: the whole (unsharded) index answers the
+        # first timed batches on this rank before it keeps only its LPT shard.
+        nchk = min(args.check_batches, args.steps) * B
+        q0 = args.warmup * B
+        chk_d = torch.empty((nchk, k), dtype=torch.float32, device=device)
+        chk_i = torch.empty((nchk, k), dtype=torch.int64, device=device)
+        for b0 in range(0, nchk, B):
+            idx.search_device(queries[q0 + b0:].data_ptr(), B, args.nprobe, k, chk_d[b0:].data_ptr(),
+                              chk_i[b0:].data_ptr(), main_stream.cuda_stream)
+        torch.cuda.synchronize()
+        check = (q0, nchk, chk_d, chk_i)
+        idx.set_shard(rank, world)
+    # Batches in flight: step s runs on streams[s % inflight]; the engine gives each
+    # concurrent search its own workspace slot, so one batch's small kernels and scan
+    # tail overlap the next batch's scan. Rank partials and gathers are per stream.
+    streams = [main_stream] + [torch.cuda.Stream(device) for _ in range(args.inflight - 1)]
+    part_d = [torch.empty((B, k), dtype=torch.float32, device=device) for _ in streams]
+    part_i = [torch.empty((B, k), dtype=torch.int64, device=device) for _ in streams]
+    gat_d = [torch.empty((world, B, k), dtype=torch.float32, device=device) for _ in streams]
+    gat_i = [torch.empty((world, B, k), dtype=torch.int64, device=device) for _ in streams]
+    torch.cuda.synchronize()
 
-    def step(s):
+    def step(s, slot):
+        st = streams[slot]
         q = queries[s * B:(s + 1) * B]
-        if world == 1:
-            idx.search_device(q.data_ptr(), B, args.nprobe, k, out_d[s * B:].data_ptr(), out_i[s * B:].data_ptr(),
-                              stream.cuda_stream)
-        else:
-            idx.search_device(q.data_ptr(), B, args.nprobe, k, part_d.data_ptr(), part_i.data_ptr(), stream.cuda_stream)
-            dist.all_gather_into_tensor(gat_d, part_d)
-            dist.all_gather_into_tensor(gat_i, part_i)
-            vdb.merge_ranks_device(gat_d.data_ptr(), gat_i.data_ptr(), world, B, k, out_d[s * B:].data_ptr(),
-                                   out_i[s * B:].data_ptr(), stream.cuda_stream)
+        with torch.cuda.stream(st):
+            if world == 1:
+                idx.search_device(q.data_ptr(), B, args.nprobe, k, out_d[s * B:].data_ptr(), out_i[s * B:].data_ptr(),
+                                  st.cuda_stream)
+            else:
+                idx.search_device(q.data_ptr(), B, args.nprobe, k, part_d[slot].data_ptr(), part_i[slot].data_ptr(),
+                                  st.cuda_stream)
+                if args.dist_backend == "nccl":
+                    dist.all_gather_into_tensor(gat_d[slot], part_d[slot])
+                    dist.all_gather_into_tensor(gat_i[slot], part_i[slot])
+                else:  # gloo (one-GPU rehearsal): the same exchange staged through host memory
+                    hd = torch.empty((world * B, k), dtype=torch.float32)
+                    hi = torch.empty((world * B, k), dtype=torch.int64)
+                    dist.all_gather_into_tensor(hd, part_d[slot].cpu())
+                    dist.all_gather_into_tensor(hi, part_i[slot].cpu())
+                    gat_d[slot].copy_(hd.view(world, B, k))
+                    gat_i[slot].copy_(hi.view(world, B, k))
+                vdb.merge_ranks_device(gat_d[slot].data_ptr(), gat_i[slot].data_ptr(), world, B, k,
+                                       out_d[s * B:].data_ptr(), out_i[s * B:].data_ptr(), st.cuda_stream)
 
     for s in range(args.warmup):
-        step(s)
+        step(s, s % len(streams))
     torch.cuda.synchronize()
-    idx.profile_enable(True)
-    idx.profile_reset()
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
@@ -197,21 +233,44 @@ def run(vdb, args, device, rank, world):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j in range(args.steps):
-        starts[j].record(stream)
-        step(args.warmup + j)
-        ends[j].record(stream)
+        slot = j % len(streams)
+        starts[j].record(streams[slot])
+        step(args.warmup + j, slot)
+        ends[j].record(streams[slot])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    prof = idx.profile_read()
-    idx.profile_enable(False)
+    parity_multi = None
+    if check is not None:
+        q0, nchk, chk_d, chk_i = check
+        same = bool(torch.equal(out_i[q0:q0 + nchk], chk_i) and
+                    torch.equal(out_d[q0:q0 + nchk].view(torch.int32), chk_d.view(torch.int32)))
+        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=device)
+        if args.dist_backend == "nccl":
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        else:
+            hf = flag.cpu()
+            dist.all_reduce(hf, op=dist.ReduceOp.MIN)
+            flag = hf
+        parity_multi = bool(int(flag.item()) == 1)
     lat = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     p99 = percentile(lat, 0.99)
     if world > 1:
-        t = torch.tensor([elapsed, p99], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, p99], dtype=torch.float64, device=device if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, p99 = float(t[0]), float(t[1])
+
+    # Roofline pass (untimed for `value`): the same steps one at a time on one stream,
+    # so the engine's per-batch events time each scan launch on its own.
+    torch.cuda.synchronize()
+    idx.profile_enable(True)
+    idx.profile_reset()
+    for j in range(args.prof_steps):
+        step(args.warmup + args.steps + j, 0)
+    torch.cuda.synchronize()
+    prof = idx.profile_read()
+    idx.profile_enable(False)
 
     launches = max(prof["scan_launches"], 1)
     scan_ms = prof["scan_ms"] / launches
@@ -245,8 +304,8 @@ def run(vdb, args, device, rank, world):
                         f"batch {B}, k {k}",
             "nvec": args.nvec, "dim": args.dim, "nlist": args.nlist, "nprobe": args.nprobe, "batch": B, "k": k,
             "train_vectors": min(args.train, args.nvec),
-            "parallelism": f"lists sharded over {world} rank(s) (LPT), RCCL all-gather of per-rank top-k"
-                           if world > 1 else "single GPU",
+            "parallelism": (f"lists sharded over {world} rank(s) (LPT), RCCL all-gather of per-rank top-k"
+                            if world > 1 else "single GPU") + f"; {args.inflight} batches in flight",
         },
         "roofline": {
             "bound": "hbm",
@@ -265,6 +324,8 @@ def run(vdb, args, device, rank, world):
         },
         "build": build_info,
     }
+    if parity_multi is not None:
+        result["parity_vs_single_gpu"] = {"batches": min(args.check_batches, args.steps), "bit_identical": parity_multi}
     if world == 1 and rank == 0 and not args.no_cpu:
         qh = queries[: args.cpu_queries].cpu().numpy()
         result["cpu_baseline"] = cpu_baseline(vdb, idx, args, qh, args.cpu_budget)

@@ -107,8 +107,6 @@ struct vdb_ivf {
     int device = 0;
     uint64_t max_gpu_memory = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;          // narrow-item scan, concurrent with the wide items
-    hipEvent_t fork = nullptr, join = nullptr;
     std::mutex mu;
 
     DevBuf<float> cent_rm;   // [nlist][dp], zero pads
@@ -129,14 +127,27 @@ struct vdb_ivf {
     int stale = 1;
     bool wide_scan = true;
 
-    // search workspace
-    DevBuf<float> qpad, cd, part_d, slot_d, carry_d, out_d, qin;
-    DevBuf<uint64_t> part_i, slot_i, carry_i, out_i;
-    DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters, l1base;
-    DevBuf<uint2> l1_items;
-    DevBuf<float> l1_d;
-    DevBuf<uint64_t> l1_i;
-    DevBuf<vdbk::ScanItem> items, items_w;
+    // Search workspaces: a ring of slots so that searches issued on different streams
+    // run concurrently (one batch's small kernels and scan tail overlap the next
+    // batch's scan). A call takes the next slot; its stream first waits for the
+    // slot's previous batch (slot.done), wherever that ran.
+    struct SearchSlot {
+        DevBuf<float> qpad, cd, part_d, slot_d, carry_d;
+        DevBuf<uint64_t> part_i, slot_i, carry_i;
+        DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters, l1base;
+        DevBuf<uint2> l1_items;
+        DevBuf<float> l1_d;
+        DevBuf<uint64_t> l1_i;
+        DevBuf<vdbk::ScanItem> items, items_w;
+        hipStream_t side = nullptr;  // narrow-item scan, concurrent with the wide items
+        hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
+        bool used = false;
+    };
+    static constexpr int kSlots = 2;
+    SearchSlot slots[kSlots];
+    uint32_t next_slot = 0;
+    DevBuf<float> out_d, qin;  // host-API staging (synchronous calls)
+    DevBuf<uint64_t> out_i;
     DevBuf<unsigned long long> stats;
 
     bool prof = false;
@@ -151,16 +162,27 @@ struct vdb_ivf {
             (void)hipEventDestroy(e.scan_end);
             (void)hipEventDestroy(e.end);
         }
-        if (fork) (void)hipEventDestroy(fork);
-        if (join) (void)hipEventDestroy(join);
-        if (side) (void)hipStreamDestroy(side);
+        for (auto& sl : slots) {
+            if (sl.fork) (void)hipEventDestroy(sl.fork);
+            if (sl.join) (void)hipEventDestroy(sl.join);
+            if (sl.done) (void)hipEventDestroy(sl.done);
+            if (sl.side) (void)hipStreamDestroy(sl.side);
+        }
         if (stream) (void)hipStreamDestroy(stream);
     }
 
     void set_device() { HIPCHECK(hipSetDevice(device)); }
 
+    // Wait for every search still in flight on any stream before the index changes
+    // under it (buffers freed, lists moved, centroids rewritten).
+    void quiesce() {
+        for (auto& sl : slots)
+            if (sl.used) HIPCHECK(hipEventSynchronize(sl.done));
+    }
+
     // Upload the list directory and recompute the segment-count prefix.
     void upload_directory() {
+        quiesce();
         std::vector<uint32_t> cl(nlist), cg(nlist), ns(nlist);
         for (uint32_t l = 0; l < nlist; ++l) {
             require(count[l] < (1ull << 32), "list longer than 2^32 vectors", VDB_ERR_UNSUPPORTED);
@@ -182,6 +204,7 @@ struct vdb_ivf {
     // Rebuild the arena so list l holds `keep[l]` of its current blocks at new
     // offsets sized for `new_count[l]` vectors (0 for lists this handle drops).
     void relayout(const std::vector<uint64_t>& new_count, const std::vector<uint8_t>& new_owned) {
+        quiesce();
         std::vector<uint64_t> new_off(nlist, 0), old_off(nlist, 0);
         std::vector<uint32_t> nblocks(nlist, 0);
         uint64_t blocks = 0;
@@ -231,6 +254,7 @@ struct vdb_ivf {
     }
 
     void refresh_centroid_layout() {
+        quiesce();
         vdbk::launch_interleave(cent_rm.p, nlist, dp, cent_il.p, stream);
         HIPCHECK(hipGetLastError());
     }
@@ -381,44 +405,44 @@ struct vdb_ivf {
         return events[events_used++];
     }
 
-    // Size every per-batch buffer for B queries up front; growing a buffer frees
-    // the old one, so wait for earlier searches that may still read it.
-    void ensure_workspace(uint32_t B, uint32_t P, uint32_t k, hipStream_t s) {
+    // Size every per-batch buffer of a slot for B queries up front; growing a buffer
+    // frees the old one, so first wait for the slot's previous batch.
+    void ensure_workspace(SearchSlot& w, uint32_t B, uint32_t P, uint32_t k) {
         const size_t BP = (size_t)B * P;
         const size_t max_items = (size_t)B * nseg_prefix[P];
         const size_t max_l1 = max_items / vdbk::kMergeFan + BP;
         const size_t max_wide = max_items / 4 + BP + 1;
-        const bool grow = items_w.cap < max_wide || qpad.cap < (size_t)B * dp || cd.cap < (size_t)B * nlist || probes.cap < BP ||
-                          items.cap < max_items || part_d.cap < max_items * k || slot_d.cap < BP * k ||
-                          carry_d.cap < (size_t)P * k || l1_items.cap < max_l1 || l1_d.cap < max_l1 * k;
+        const bool grow = w.items_w.cap < max_wide || w.qpad.cap < (size_t)B * dp || w.cd.cap < (size_t)B * nlist ||
+                          w.probes.cap < BP || w.items.cap < max_items || w.part_d.cap < max_items * k ||
+                          w.slot_d.cap < BP * k || w.carry_d.cap < (size_t)P * k || w.l1_items.cap < max_l1 ||
+                          w.l1_d.cap < max_l1 * k;
         if (!grow) return;
-        HIPCHECK(hipStreamSynchronize(s));
-        HIPCHECK(hipStreamSynchronize(stream));
-        qpad.ensure((size_t)B * dp);
-        cd.ensure((size_t)B * nlist);
-        probes.ensure(BP);
-        nseg_qp.ensure(BP);
-        pbqp.ensure(BP);
-        sorted_pair.ensure(BP);
-        pbs.ensure(BP);
-        counters.ensure(4);
-        l1base.ensure(BP);
-        l1_items.ensure(max_l1);
-        l1_d.ensure(max_l1 * k);
-        l1_i.ensure(max_l1 * k);
-        items.ensure(max_items);
-        items_w.ensure(max_wide);
-        part_d.ensure(max_items * k);
-        part_i.ensure(max_items * k);
-        slot_d.ensure(BP * k);
-        slot_i.ensure(BP * k);
-        carry_d.ensure((size_t)P * k);
-        carry_i.ensure((size_t)P * k);
+        if (w.used) HIPCHECK(hipEventSynchronize(w.done));
+        w.qpad.ensure((size_t)B * dp);
+        w.cd.ensure((size_t)B * nlist);
+        w.probes.ensure(BP);
+        w.nseg_qp.ensure(BP);
+        w.pbqp.ensure(BP);
+        w.sorted_pair.ensure(BP);
+        w.pbs.ensure(BP);
+        w.counters.ensure(4);
+        w.l1base.ensure(BP);
+        w.l1_items.ensure(max_l1);
+        w.l1_d.ensure(max_l1 * k);
+        w.l1_i.ensure(max_l1 * k);
+        w.items.ensure(max_items);
+        w.items_w.ensure(max_wide);
+        w.part_d.ensure(max_items * k);
+        w.part_i.ensure(max_items * k);
+        w.slot_d.ensure(BP * k);
+        w.slot_i.ensure(BP * k);
+        w.carry_d.ensure((size_t)P * k);
+        w.carry_i.ensure((size_t)P * k);
     }
 
     // ---- search: ivf_flat_index.cpp:205-256, one batch of B queries ----
-    void run_batch(const float* d_q, uint32_t B, uint32_t P, uint32_t k, float* out_d_, uint64_t* out_i_,
-                   hipStream_t s) {
+    void run_batch(SearchSlot& w, const float* d_q, uint32_t B, uint32_t P, uint32_t k, float* out_d_,
+                   uint64_t* out_i_, hipStream_t s) {
         const int regs_k = vdbk::topk_regs(k);
         const int regs_p = vdbk::topk_regs(P);
         const uint32_t group = (uint32_t)vdbk::scan_group(regs_k);
@@ -428,37 +452,37 @@ struct vdb_ivf {
         EventSet* ev = prof ? &next_events() : nullptr;
         if (ev) HIPCHECK(hipEventRecord(ev->begin, s));
 
-        vdbk::launch_pad_rows(d_q, B, dim, dp, qpad.p, s);
-        vdbk::launch_coarse(metric, cent_il.p, nlist, d4, qpad.p, B, cd.p, s);
-        vdbk::launch_select(regs_p, cd.p, nlist, B, P, probes.p, s);
+        vdbk::launch_pad_rows(d_q, B, dim, dp, w.qpad.p, s);
+        vdbk::launch_coarse(metric, cent_il.p, nlist, d4, w.qpad.p, B, w.cd.p, s);
+        vdbk::launch_select(regs_p, w.cd.p, nlist, B, P, w.probes.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
         const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
         const uint64_t max_wide = max_items / 4 + BP + 1;
         const bool wide = regs_k == 1 && wide_scan && vdbk::scan_wide_fits(d4, k);
-        vdbk::launch_plan(probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? 1 : 0, items.p, items_w.p,
-                          counters.p, sorted_pair.p, pbs.p, pbqp.p, nseg_qp.p, l1base.p, l1_items.p, stats.p, s);
+        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? 1 : 0, w.items.p, w.items_w.p,
+                          w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
-        const vdbk::ScanArgs sa{arena.p, arena_ids.p, d_block_off.p, d_count_local.p, qpad.p, items.p, items_w.p,
-                                counters.p, sorted_pair.p, pbs.p, part_d.p, part_i.p, d4, k};
+        const vdbk::ScanArgs sa{arena.p, arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
+                                w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k};
         if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
-            HIPCHECK(hipEventRecord(fork, s));
-            HIPCHECK(hipStreamWaitEvent(side, fork, 0));
-            vdbk::launch_scan_narrow(metric, regs_k, (uint32_t)((max_items + 3) / 4), sa, side);
-            HIPCHECK(hipEventRecord(join, side));
+            HIPCHECK(hipEventRecord(w.fork, s));
+            HIPCHECK(hipStreamWaitEvent(w.side, w.fork, 0));
+            vdbk::launch_scan_narrow(metric, regs_k, (uint32_t)((max_items + 3) / 4), sa, w.side);
+            HIPCHECK(hipEventRecord(w.join, w.side));
             vdbk::launch_scan_wide(metric, (uint32_t)max_wide, sa, s);
-            HIPCHECK(hipStreamWaitEvent(s, join, 0));
+            HIPCHECK(hipStreamWaitEvent(s, w.join, 0));
         } else {
             vdbk::launch_scan_narrow(metric, regs_k, (uint32_t)((max_items + 3) / 4), sa, s);
         }
         if (ev) HIPCHECK(hipEventRecord(ev->scan_end, s));
-        vdbk::launch_merge_partials(regs_k, (uint32_t)max_l1, probes.p, d_count_global.p, nseg_qp.p, pbqp.p, l1base.p,
-                                    l1_items.p, counters.p, part_d.p, part_i.p, k, l1_d.p, l1_i.p, s);
-        vdbk::launch_slot_merge(regs_k, probes.p, d_count_global.p, nseg_qp.p, pbqp.p, l1base.p, part_d.p, part_i.p,
-                                l1_d.p, l1_i.p, BP, k, slot_d.p, slot_i.p, s);
-        vdbk::launch_query_merge(regs_k, probes.p, d_count_global.p, slot_d.p, slot_i.p, carry_d.p, carry_i.p, B, P, k,
+        vdbk::launch_merge_partials(regs_k, (uint32_t)max_l1, w.probes.p, d_count_global.p, w.nseg_qp.p, w.pbqp.p, w.l1base.p,
+                                    w.l1_items.p, w.counters.p, w.part_d.p, w.part_i.p, k, w.l1_d.p, w.l1_i.p, s);
+        vdbk::launch_slot_merge(regs_k, w.probes.p, d_count_global.p, w.nseg_qp.p, w.pbqp.p, w.l1base.p, w.part_d.p, w.part_i.p,
+                                w.l1_d.p, w.l1_i.p, BP, k, w.slot_d.p, w.slot_i.p, s);
+        vdbk::launch_query_merge(regs_k, w.probes.p, d_count_global.p, w.slot_d.p, w.slot_i.p, w.carry_d.p, w.carry_i.p, B, P, k,
                                  stale, out_d_, out_i_, s);
-        if (stale) vdbk::launch_carry(probes.p, d_count_global.p, B, P, k, slot_d.p, slot_i.p, carry_d.p, carry_i.p, s);
+        if (stale) vdbk::launch_carry(w.probes.p, d_count_global.p, B, P, k, w.slot_d.p, w.slot_i.p, w.carry_d.p, w.carry_i.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->end, s));
         HIPCHECK(hipGetLastError());
     }
@@ -479,13 +503,18 @@ struct vdb_ivf {
             HIPCHECK(hipMemsetAsync(stats.p, 0, 64, s));
         }
         const uint32_t bmax = std::max<uint32_t>(1, std::min<uint32_t>(batch, vdbk::kPlanMaxPairs / P));
-        ensure_workspace(std::min(bmax, n), P, k, s);
-        // Slot contents live for one search call (cpp:210-211).
-        HIPCHECK(hipMemsetAsync(carry_i.p, 0xFF, (size_t)P * k * 8, s));
+        SearchSlot& w = slots[next_slot];
+        next_slot = (next_slot + 1) % kSlots;
+        ensure_workspace(w, std::min(bmax, n), P, k);
+        if (w.used) HIPCHECK(hipStreamWaitEvent(s, w.done, 0));
+        // Probe-slot contents live for one search call (cpp:210-211).
+        HIPCHECK(hipMemsetAsync(w.carry_i.p, 0xFF, (size_t)P * k * 8, s));
         for (uint32_t b0 = 0; b0 < n; b0 += bmax) {
             const uint32_t B = std::min(bmax, n - b0);
-            run_batch(d_q + (size_t)b0 * dim, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s);
+            run_batch(w, d_q + (size_t)b0 * dim, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s);
         }
+        HIPCHECK(hipEventRecord(w.done, s));
+        w.used = true;
     }
 };
 
@@ -521,9 +550,12 @@ int vdb_ivf_create(const vdb_ivf_config* cfg, vdb_ivf** out) {
             h->max_gpu_memory = cfg->max_gpu_memory;
             h->set_device();
             HIPCHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-            HIPCHECK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-            HIPCHECK(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
-            HIPCHECK(hipEventCreateWithFlags(&h->join, hipEventDisableTiming));
+            for (auto& sl : h->slots) {
+                HIPCHECK(hipStreamCreateWithFlags(&sl.side, hipStreamNonBlocking));
+                HIPCHECK(hipEventCreateWithFlags(&sl.fork, hipEventDisableTiming));
+                HIPCHECK(hipEventCreateWithFlags(&sl.join, hipEventDisableTiming));
+                HIPCHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+            }
             h->cent_rm.ensure((size_t)h->nlist * h->dp);
             h->cent_il.ensure(cdiv(h->nlist, 64) * h->d4 * 64);
             HIPCHECK(hipMemsetAsync(h->cent_rm.p, 0, (size_t)h->nlist * h->dp * 4, h->stream));  // cpp:22

@@ -329,3 +329,34 @@ def test_save_load_round_trip(tmp_path):
     assert lib.vdb_ivf_load(h._h, path) == 0
     assert np.array_equal(h.list_sizes(), g.list_sizes())
     assert_same(*h.search(Q, nprobe=4, k=10), D, I)
+
+
+def test_concurrent_streams_match_sequential():
+    """Batches issued alternately on two streams (two in flight, each in its own
+    engine workspace slot, hub lists included) equal the oracle bit for bit."""
+    import torch
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((30000, 64)).astype(np.float32)
+    Q = rng.standard_normal((8 * 64, 64)).astype(np.float32)
+    ids = np.arange(30000, dtype=np.uint64)
+    C = np.zeros((12, 64), np.float32)
+    C[1:] = 2.5 * rng.standard_normal((11, 64)).astype(np.float32)
+    o = oracle.OracleIndex(64, 12, 0)
+    o.centroids = C
+    o.add(X, ids)
+    g = mirror_from_oracle(o, 64, 12)
+    g.add(X, ids)
+    dev = torch.device("cuda:0")
+    qd = torch.from_numpy(Q).to(dev)
+    od = torch.empty((len(Q), 10), dtype=torch.float32, device=dev)
+    oi = torch.empty((len(Q), 10), dtype=torch.int64, device=dev)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    torch.cuda.synchronize()
+    for b in range(8):
+        s = streams[b % 2]
+        g.search_device(qd[b * 64:].data_ptr(), 64, 4, 10, od[b * 64:].data_ptr(), oi[b * 64:].data_ptr(),
+                        s.cuda_stream)
+    torch.cuda.synchronize()
+    Dr = np.concatenate([o.search(Q[b * 64:(b + 1) * 64], 4, 10)[0] for b in range(8)])
+    Ir = np.concatenate([o.search(Q[b * 64:(b + 1) * 64], 4, 10)[1] for b in range(8)])
+    assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), Dr, Ir)
