@@ -1,0 +1,58 @@
+#!/bin/bash
+# One GPU-box session (run via gpurun from the repo root): parity tests, the default
+# bench line, the kernel-trace summary of the bench command, PMC passes, index dump.
+#   usage: bash tools/gpu_session.sh <tag> [steps, comma-separated:
+#          tests,smoke,bench,dump,prof,pmc]  [extra bench args...]
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -o pipefail
+TAG=${1:-run}
+STEPS=${2:-tests,bench,prof}
+shift 2 2>/dev/null
+BARGS="$*"
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$R" || exit 1
+export TMPDIR=/tmp
+has() { [[ ",$STEPS," == *",$1,"* ]]; }
+run() {  # run <name> <seconds> <cmd...>: stop the session on any failure
+    local name=$1 secs=$2
+    shift 2
+    echo "[$(date +%T)] $name: $*"
+    timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1
+    local rc=$?
+    echo "[$(date +%T)] $name rc=$rc"
+    if [ $rc -ne 0 ]; then
+        tail -40 "$O/$name.log"
+        exit $rc
+    fi
+}
+nproc > "$O/nproc.txt"
+lscpu > "$O/lscpu.txt" 2>/dev/null
+if has tests; then
+    run pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread
+    tail -3 "$O/pytest.log"
+fi
+if has smoke; then
+    run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+    tail -2 "$O/smoke.log"
+fi
+if has bench; then
+    run bench 600 python -u bench.py $BARGS
+    grep '^{' "$O/bench.log" > "$O/bench.json"
+    cat "$O/bench.json"
+fi
+if has dump; then
+    run dump 600 python -u tests/debug_dump_index.py 10000000 4096
+fi
+if has prof; then
+    run prof 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu $BARGS
+    find "$O/prof" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats.csv" \;
+    head -14 "$O/kernel_stats.csv"
+fi
+if has pmc; then
+    # HBM bytes of the scan kernels (FETCH_SIZE; x2 on gfx950, MI355X_MICROARCH.md §HBM)
+    run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ivf_scan_ -d "$O/pmc_f" -o f -f csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --prof-steps 2 $BARGS
+    run pmc_sq 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES --kernel-include-regex ivf_scan_ -d "$O/pmc_s" -o s -f csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --prof-steps 2 $BARGS
+fi
+echo "session $TAG done"
