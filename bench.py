@@ -144,9 +144,12 @@ def main():
                     help="gloo: rehearse the multi-rank path with host-staged exchange")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (one-GPU rehearsal)")
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight (streams) in the timed region")
-    ap.add_argument("--prof-steps", type=int, default=10, help="single-stream steps timed per launch for the roofline")
+    ap.add_argument("--prof-steps", type=int, default=30,
+                    help="single-stream steps timed per launch (roofline, one-in-flight latency)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per ivf_scan launch for this workload (or null)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="engine tuning knob (vdb_ivf_set_option), e.g. wide_stride=1; results never change")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,6 +172,9 @@ def main():
 
 def run(vdb, args, device, rank, world):
     idx, build_info = build_index(vdb, args, device, rank, world)
+    for o in args.opt:
+        name, val = o.split("=", 1)
+        idx.set_option(name, int(val))
     B, k = args.batch, args.k
     nq = (args.warmup + args.steps + args.prof_steps) * B
     main_stream = torch.cuda.current_stream()
@@ -263,14 +269,24 @@ def run(vdb, args, device, rank, world):
 
     # Roofline pass (untimed for `value`): the same steps one at a time on one stream,
     # so the engine's per-batch events time each scan launch on its own.
+    # Its per-step events also give the latency of a batch with nothing else in flight.
     torch.cuda.synchronize()
     idx.profile_enable(True)
     idx.profile_reset()
+    s_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.prof_steps)]
+    e_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.prof_steps)]
     for j in range(args.prof_steps):
+        s_ev[j].record(streams[0])
         step(args.warmup + args.steps + j, 0)
+        e_ev[j].record(streams[0])
     torch.cuda.synchronize()
     prof = idx.profile_read()
     idx.profile_enable(False)
+    p99_single = percentile([a.elapsed_time(b) for a, b in zip(s_ev, e_ev)], 0.99)
+    if world > 1:
+        t = torch.tensor([p99_single], dtype=torch.float64, device=device if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        p99_single = float(t[0])
 
     launches = max(prof["scan_launches"], 1)
     scan_ms = prof["scan_ms"] / launches
@@ -294,6 +310,7 @@ def run(vdb, args, device, rank, world):
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "p99_ms": round(p99, 4),
+        "p99_ms_one_in_flight": round(p99_single, 4),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -323,6 +340,7 @@ def run(vdb, args, device, rank, world):
             "distances_per_batch": int(prof["pair_vectors"] / max(prof["batches"], 1)),
         },
         "build": build_info,
+        "engine_options": dict(o.split("=", 1) for o in args.opt),
     }
     if parity_multi is not None:
         result["parity_vs_single_gpu"] = {"batches": min(args.check_batches, args.steps), "bit_identical": parity_multi}

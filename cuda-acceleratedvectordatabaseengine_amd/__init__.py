@@ -103,6 +103,8 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_get_list": (ctypes.c_int, [vp, u32, vp, vp]),
         "vdb_ivf_set_batch": (ctypes.c_int, [vp, u32]),
         "vdb_ivf_set_stale_slots": (ctypes.c_int, [vp, i32]),
+        "vdb_ivf_set_coarse_mode": (ctypes.c_int, [vp, i32]),
+        "vdb_ivf_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int64]),
         "vdb_ivf_profile_enable": (ctypes.c_int, [vp, i32]),
         "vdb_ivf_profile_reset": (ctypes.c_int, [vp]),
         "vdb_ivf_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(Profile)]),
@@ -291,6 +293,14 @@ class IVFFlatIndex:
 
     def set_stale_slots(self, enable: bool):
         _check(lib().vdb_ivf_set_stale_slots(self._h, int(enable)))
+
+    def set_coarse_mode(self, mode: int):
+        """1: MFMA bounds + exact re-rank (default); 0: exact VALU coarse distances."""
+        _check(lib().vdb_ivf_set_coarse_mode(self._h, mode))
+
+    def set_option(self, name: str, value: int):
+        """Engine tuning knob (vdb_ivf_set_option); never changes results."""
+        _check(lib().vdb_ivf_set_option(self._h, name.encode(), int(value)))
 
     def profile_enable(self, on: bool = True):
         _check(lib().vdb_ivf_profile_enable(self._h, int(on)))

@@ -93,6 +93,18 @@ struct DevBuf {
     }
 };
 
+// Page-locked host buffer (fast device-to-host copies of build-time scratch).
+template <class T>
+struct PinnedBuf {
+    T* p = nullptr;
+    explicit PinnedBuf(size_t n) { HIPCHECK(hipHostMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T))); }
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
 inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 struct EventSet {
@@ -126,15 +138,17 @@ struct vdb_ivf {
     uint32_t batch = 256;
     int stale = 1;
     bool wide_scan = true;
+    int coarse_mode = 1;
+    uint32_t wide_stride = 1;  // wide-item dispatch permutation (1 = plan order; measured best)  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
 
     // Search workspaces: a ring of slots so that searches issued on different streams
     // run concurrently (one batch's small kernels and scan tail overlap the next
     // batch's scan). A call takes the next slot; its stream first waits for the
     // slot's previous batch (slot.done), wherever that ran.
     struct SearchSlot {
-        DevBuf<float> qpad, cd, part_d, slot_d, carry_d;
+        DevBuf<float> qpad, cd, cdelta, part_d, slot_d, carry_d;
         DevBuf<uint64_t> part_i, slot_i, carry_i;
-        DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters, l1base;
+        DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters, l1base, cand;
         DevBuf<uint2> l1_items;
         DevBuf<float> l1_d;
         DevBuf<uint64_t> l1_i;
@@ -292,7 +306,7 @@ struct vdb_ivf {
     // ---- train: ivf_flat_index.cpp:49-145 ----
     void train(const float* d_v, uint64_t n) {
         require(n > 0, "train needs at least one vector");
-        DevBuf<float> tmp, mind, prefix, total;
+        DevBuf<float> tmp, mind;
         const float* vpad = padded_rows(d_v, n, tmp);
         DevBuf<float4> v_il;
         vdbk::launch_interleave(vpad, n, dp, v_il.ensure(cdiv(n, 64) * d4 * 64), stream);
@@ -304,23 +318,29 @@ struct vdb_ivf {
         HIPCHECK(hipMemcpyAsync(cent_rm.p, vpad + first * dp, dp * 4, hipMemcpyDeviceToDevice, stream));
 
         vdbk::launch_mindist_init(mind.ensure(n), n, stream);
-        prefix.ensure(n);
-        total.ensure(1);
-        DevBuf<unsigned long long> pick_idx;
-        pick_idx.ensure(1);
+        // The min-distance update (n x dim work) runs on the device; the two serial
+        // float sums of cpp:87 and cpp:95-96 (n dependent adds each, inherently
+        // sequential) run on the host over a pinned copy, in the reference's order.
+        PinnedBuf<float> hmind(n);
         for (uint32_t c = 1; c < nlist; ++c) {
             vdbk::launch_mindist_update(v_il.p, n, d4, cent_rm.p + (size_t)(c - 1) * dp, mind.p, stream);
-            vdbk::launch_serial_prefix(mind.p, n, prefix.p, total.p, stream);
             HIPCHECK(hipGetLastError());
-            float tot = 0.0f;
-            HIPCHECK(hipMemcpyAsync(&tot, total.p, 4, hipMemcpyDeviceToHost, stream));
+            HIPCHECK(hipMemcpyAsync(hmind.p, mind.p, n * sizeof(float), hipMemcpyDeviceToHost, stream));
             HIPCHECK(hipStreamSynchronize(stream));
+            const float* md = hmind.p;
+            float tot = 0.0f;
+            for (uint64_t v = 0; v < n; ++v) tot += md[v];
             std::uniform_real_distribution<float> prob(0.0f, tot);
             const float target = prob(gen);
-            HIPCHECK(hipMemsetAsync(pick_idx.p, 0xFF, 8, stream));
-            vdbk::launch_first_geq(prefix.p, n, target, pick_idx.p, stream);
-            vdbk::launch_copy_row_if(vpad, n, dp, pick_idx.p, cent_rm.p + (size_t)c * dp, stream);
-            HIPCHECK(hipGetLastError());
+            float cumsum = 0.0f;
+            for (uint64_t v = 0; v < n; ++v) {
+                cumsum += md[v];
+                if (cumsum >= target) {
+                    HIPCHECK(hipMemcpyAsync(cent_rm.p + (size_t)c * dp, vpad + v * dp, dp * sizeof(float),
+                                            hipMemcpyDeviceToDevice, stream));
+                    break;
+                }
+            }
         }
 
         DevBuf<uint32_t> asg, skeys, order, counts, offsets;
@@ -413,6 +433,7 @@ struct vdb_ivf {
         const size_t max_l1 = max_items / vdbk::kMergeFan + BP;
         const size_t max_wide = max_items / 4 + BP + 1;
         const bool grow = w.items_w.cap < max_wide || w.qpad.cap < (size_t)B * dp || w.cd.cap < (size_t)B * nlist ||
+                          w.cdelta.cap < (size_t)B * nlist || w.cand.cap < (size_t)B * nlist ||
                           w.probes.cap < BP || w.items.cap < max_items || w.part_d.cap < max_items * k ||
                           w.slot_d.cap < BP * k || w.carry_d.cap < (size_t)P * k || w.l1_items.cap < max_l1 ||
                           w.l1_d.cap < max_l1 * k;
@@ -420,6 +441,8 @@ struct vdb_ivf {
         if (w.used) HIPCHECK(hipEventSynchronize(w.done));
         w.qpad.ensure((size_t)B * dp);
         w.cd.ensure((size_t)B * nlist);
+        w.cdelta.ensure((size_t)B * nlist);
+        w.cand.ensure((size_t)B * nlist);
         w.probes.ensure(BP);
         w.nseg_qp.ensure(BP);
         w.pbqp.ensure(BP);
@@ -453,8 +476,14 @@ struct vdb_ivf {
         if (ev) HIPCHECK(hipEventRecord(ev->begin, s));
 
         vdbk::launch_pad_rows(d_q, B, dim, dp, w.qpad.p, s);
-        vdbk::launch_coarse(metric, cent_il.p, nlist, d4, w.qpad.p, B, w.cd.p, s);
-        vdbk::launch_select(regs_p, w.cd.p, nlist, B, P, w.probes.p, s);
+        if (coarse_mode == 1 && metric != 2 && vdbk::rerank_rows(dp, regs_p) > 0) {
+            vdbk::launch_coarse_mfma(metric, cent_rm.p, nlist, dp, w.qpad.p, B, w.cd.p, w.cdelta.p, s);
+            vdbk::launch_select_rerank(metric, regs_p, w.cd.p, w.cdelta.p, cent_rm.p, nlist, dp, w.qpad.p, B, P,
+                                       w.cand.p, w.probes.p, s);
+        } else {
+            vdbk::launch_coarse(metric, cent_il.p, nlist, d4, w.qpad.p, B, w.cd.p, s);
+            vdbk::launch_select(regs_p, w.cd.p, nlist, B, P, w.probes.p, s);
+        }
         if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
         const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
         const uint64_t max_wide = max_items / 4 + BP + 1;
@@ -463,7 +492,8 @@ struct vdb_ivf {
                           w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
         const vdbk::ScanArgs sa{arena.p, arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
-                                w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k};
+                                w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
+                                wide_stride};
         if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));
@@ -881,6 +911,38 @@ int vdb_ivf_set_stale_slots(vdb_ivf* h, int enable) {
         require(h, "null handle");
         std::lock_guard<std::mutex> g(h->mu);
         h->stale = enable ? 1 : 0;
+    });
+}
+
+int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
+    return guarded([&] {
+        require(h && name, "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        const std::string n(name);
+        if (n == "coarse_mode") {
+            require(value == 0 || value == 1, "coarse_mode is 0 or 1");
+            h->coarse_mode = (int)value;
+        } else if (n == "wide_scan") {
+            h->wide_scan = value != 0;
+        } else if (n == "wide_stride") {
+            require(value >= 0 && value < (1ll << 31), "wide_stride out of range");
+            h->wide_stride = (uint32_t)value;
+        } else if (n == "batch") {
+            require(value > 0 && value < (1ll << 31), "batch out of range");
+            h->batch = (uint32_t)value;
+        } else if (n == "stale_slots") {
+            h->stale = value ? 1 : 0;
+        } else {
+            throw VdbError(VDB_ERR_INVALID_ARGUMENT, "unknown option " + n);
+        }
+    });
+}
+
+int vdb_ivf_set_coarse_mode(vdb_ivf* h, int mode) {
+    return guarded([&] {
+        require(h && (mode == 0 || mode == 1), "coarse mode is 0 (exact VALU) or 1 (MFMA + exact re-rank)");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->coarse_mode = mode;
     });
 }
 

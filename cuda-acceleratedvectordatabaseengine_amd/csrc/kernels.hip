@@ -13,6 +13,7 @@
 
 #include <cfloat>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "kernels.hpp"
@@ -106,6 +107,10 @@ __global__ __launch_bounds__(256) void ivf_coarse_distances(const float4* __rest
     }
 }
 
+// NaN distances order after every number (the reference's comparisons leave them
+// unordered); keeps every selected list id valid.
+__device__ __forceinline__ float nan_last(float d) { return d == d ? d : __builtin_inff(); }
+
 // ============================================================================
 // Coarse quantiser, selection part: the first min(nprobe, nlist) lists by
 // (dist, list_id) — partial_sort on std::pair (cpp:324-333). One wave per query.
@@ -124,13 +129,256 @@ __global__ __launch_bounds__(256) void ivf_select_probes(const float* __restrict
     for (uint32_t c0 = 0; c0 < nlist; c0 += 64) {
         const uint32_t c = c0 + lane;
         const bool valid = c < nlist;
-        const float d = valid ? row[c] : __builtin_inff();
+        const float d = valid ? nan_last(row[c]) : __builtin_inff();
         offer_lanes<R>(tk, valid && d <= kd, d, (uint64_t)c, (int)P, kd, ki);
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const uint32_t e = r * 64 + lane;
         if (e < P) probes[(size_t)q * P + e] = (uint32_t)tk.id[r];
+    }
+}
+
+// ============================================================================
+// Coarse quantiser on the matrix cores (L2 / IP): the batch x centroid-table
+// product is the path's one real contraction, so it runs on v_mfma_f32_16x16x4_f32
+// (f32 in, f32 accumulate). Its sums run in a different order from the reference's
+// sequential loop, so they only bound the exact distance: with u = 2^-24 and
+// n = padded dimension, |mfma - exact| <= 4 (n + 4) u (|q| + |c|)^2 for L2
+// (|q| |c| for IP), counting the exact sum's own error against the real value.
+// ivf_select_rerank then keeps every centroid whose interval can reach the P-th
+// smallest upper bound, recomputes those exactly and selects by (dist, list).
+// One wave = one 16-query x 16-centroid tile over all dimensions. Lane (r, h):
+// row r = lane & 15 of each operand, dims d0 + 4h .. d0 + 4h + 3 of every
+// 16-dim step, fed to four MFMAs (k index h <-> dim d0 + 4h + s in step s).
+// The operand norms are summed from the same registers on the way.
+// ============================================================================
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+template <int M, int G>
+__global__ __launch_bounds__(256) void ivf_coarse_mfma(const float* __restrict__ cent_rm, uint32_t nlist,
+                                                       uint32_t dp, const float* __restrict__ qpad, uint32_t B,
+                                                       float* __restrict__ approx, float* __restrict__ delta) {
+    const int lane = lane_id();
+    const uint32_t ct = blockIdx.x * 4 + wave_index();  // centroid tile
+    const uint32_t qt = blockIdx.y;                      // query tile
+    if (ct * 16 >= nlist) return;
+    const int r = lane & 15, h = lane >> 4;
+    const uint32_t qrow = qt * 16 + r, crow = ct * 16 + r;
+    const bool qok = qrow < B, cok = crow < nlist;
+    const float4* qa = (const float4*)(qpad + (size_t)(qok ? qrow : 0) * dp) + h;
+    const float4* cb = (const float4*)(cent_rm + (size_t)(cok ? crow : 0) * dp) + h;
+    f4v acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // two chains hide the MFMA latency
+    float qn = 0.f, cn = 0.f;
+    const uint32_t steps = dp / 16;  // a multiple of G (the launcher picks G = 8 or 4)
+    float4 a[G], b[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) a[g] = qa[(size_t)g * 4], b[g] = cb[(size_t)g * 4];
+    for (uint32_t s0 = 0; s0 < steps; s0 += G) {
+        float4 an[G], bn[G];
+        const uint32_t nx = s0 + G < steps ? s0 + G : s0;  // the last group re-loads itself
+#pragma unroll
+        for (int g = 0; g < G; ++g) an[g] = qa[(size_t)(nx + g) * 4], bn[g] = cb[(size_t)(nx + g) * 4];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float4 x = qok ? a[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 y = cok ? b[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+            f4v& ac = acc[g & 1];
+            ac = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, y.x, ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, y.y, ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, y.z, ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, y.w, ac, 0, 0, 0);
+            qn = qn + (x.x * x.x + x.y * x.y) + (x.z * x.z + x.w * x.w);
+            cn = cn + (y.x * y.x + y.y * y.y) + (y.z * y.z + y.w * y.w);
+            a[g] = an[g];
+            b[g] = bn[g];
+        }
+    }
+    acc[0] = acc[0] + acc[1];
+    // row norms: lanes r, r+16, r+32, r+48 hold the four dim quarters of row r
+    qn += __shfl_xor(qn, 16);
+    qn += __shfl_xor(qn, 32);
+    cn += __shfl_xor(cn, 16);
+    cn += __shfl_xor(cn, 32);
+    // C/D layout (16x16): col = lane & 15 (centroid), row = (lane >> 4) * 4 + reg (query)
+    const uint32_t c = ct * 16 + (lane & 15);
+    const float ca = sqrtf(cn);
+    const float K = 4.0f * (float)(dp + 4) * 5.9604645e-8f;  // 4 (n + 4) u
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+        const int row = (lane >> 4) * 4 + reg;
+        const float qrn = __shfl(qn, row);  // lane `row` (< 16) holds query row `row`'s norm
+        const uint32_t q = qt * 16 + row;
+        if (q < B && c < nlist) {
+            const float qa_ = sqrtf(qrn);
+            float ap, dl;
+            if constexpr (M == kL2) {
+                ap = (qrn + cn) - 2.0f * acc[0][reg];
+                dl = K * ((qa_ + ca) * (qa_ + ca)) + 1e-30f;
+            } else {
+                ap = -acc[0][reg];
+                dl = K * (qa_ * ca) + 1e-30f;
+            }
+            approx[(size_t)q * nlist + c] = ap;
+            delta[(size_t)q * nlist + c] = dl;
+        }
+    }
+}
+
+// Sequential exact distance of wave-uniform query row q against this lane's centroid
+// row (the reference's loop order, cpp:308-318). Rows are zero padded to dp.
+template <int M>
+__device__ __forceinline__ float exact_row(const float* __restrict__ qrow, const float* __restrict__ crow,
+                                           uint32_t dp) {
+    const float4* q4 = (const float4*)qrow;
+    const float4* c4 = (const float4*)crow;
+    float acc = 0.0f;
+#pragma unroll 8
+    for (uint32_t t = 0; t < dp / 4; ++t) acc = acc4<M>(acc, q4[t], c4[t]);
+    return dist_finish<M>(acc);
+}
+
+// Per query (one workgroup of 4 waves): tau = P-th smallest upper bound;
+// candidates = lists whose lower bound is <= tau (this always contains the exact
+// top-P: P lists have exact distance <= tau); exact distances of the candidates;
+// top-P by (dist, list) as the reference's partial_sort on std::pair
+// (cpp:324-333). Non-finite bounds make a list a candidate; NaN distances order
+// last. Candidate centroid rows are staged in LDS (coalesced loads, rows padded by
+// 4 floats so the lane-per-row reads are conflict-free) in chunks of `ch` rows;
+// one lane per candidate then runs the reference's sequential sum.
+template <int R, int M>
+__global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict__ approx,
+                                                         const float* __restrict__ delta,
+                                                         const float* __restrict__ cent_rm, uint32_t nlist,
+                                                         uint32_t dp, const float* __restrict__ qpad, uint32_t B,
+                                                         uint32_t P, uint32_t ch, uint32_t* __restrict__ cand,
+                                                         uint32_t* __restrict__ probes) {
+    extern __shared__ __attribute__((aligned(16))) float4 smem[];
+    __shared__ float s_top_d[4 * R * 64];
+    __shared__ uint32_t s_top_i[4 * R * 64];
+    __shared__ float s_tau;
+    __shared__ uint32_t s_n;
+    const uint32_t q = blockIdx.x;
+    if (q >= B) return;
+    const int lane = lane_id();
+    const uint32_t w = wave_index();
+    const float* ar = approx + (size_t)q * nlist;
+    const float* dr = delta + (size_t)q * nlist;
+    if (threadIdx.x == 0) s_n = 0;
+    // pass 1: each wave's top-P upper bounds over its quarter (c = w*64 + 256 j + lane).
+    // The wave's lists are read in rounds of kPre per lane, all loads issued up front
+    // (a dependent offer between loads would expose the memory latency per load).
+    constexpr int kPre = 16;
+    {
+        WaveTopK<R> tk;
+        tk.init();
+        float kd = __builtin_inff();
+        uint64_t ki = kNoId;
+        for (uint32_t r0 = w * 64; r0 < nlist; r0 += 256 * kPre) {
+            float hv[kPre];
+#pragma unroll
+            for (int j = 0; j < kPre; ++j) {
+                const uint32_t c = r0 + j * 256 + lane;
+                hv[j] = c < nlist ? nan_last(ar[c] + dr[c]) : __builtin_inff();
+            }
+#pragma unroll
+            for (int j = 0; j < kPre; ++j) {
+                const uint32_t c = r0 + j * 256 + lane;
+                offer_lanes<R>(tk, c < nlist && hv[j] <= kd, hv[j], (uint64_t)c, (int)P, kd, ki);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            s_top_d[(w * R + r) * 64 + lane] = tk.d[r];
+            s_top_i[(w * R + r) * 64 + lane] = (uint32_t)tk.id[r];
+        }
+    }
+    __syncthreads();
+    if (w == 0) {  // tau = P-th smallest of the four partial lists
+        WaveTopK<R> tk;
+        tk.init();
+        float kd = __builtin_inff();
+        uint64_t ki = kNoId;
+        for (uint32_t e0 = 0; e0 < 4 * R * 64; e0 += 64) {
+            const float d = s_top_d[e0 + lane];
+            const uint32_t id = s_top_i[e0 + lane];
+            const bool valid = id != 0xFFFFFFFFu;
+            offer_lanes<R>(tk, valid && d <= kd, d, (uint64_t)id, (int)P, kd, ki);
+        }
+        if (lane == 0) s_tau = kd;
+    }
+    __syncthreads();
+    const float tau = s_tau;
+    // pass 2: candidates, appended through one LDS counter per wave-iteration
+    uint32_t* cl = cand + (size_t)q * nlist;
+    const uint64_t below = (1ull << lane) - 1;
+    for (uint32_t r0 = w * 64; r0 < nlist; r0 += 256 * kPre) {
+        bool want[kPre];
+#pragma unroll
+        for (int j = 0; j < kPre; ++j) {
+            const uint32_t c = r0 + j * 256 + lane;
+            want[j] = c < nlist && !(ar[c] - dr[c] > tau);
+        }
+#pragma unroll
+        for (int j = 0; j < kPre; ++j) {
+            const uint64_t m = __ballot(want[j]);
+            if (!m) continue;
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&s_n, (uint32_t)__popcll(m));
+            base = __shfl(base, 0);
+            if (want[j]) cl[base + __popcll(m & below)] = r0 + j * 256 + lane;
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t n = s_n;
+    // pass 3: exact sequential distances of the candidates, ch rows at a time
+    const uint32_t rs = dp / 4 + 1;  // LDS row stride in float4 (one float4 of padding)
+    float4* q_l = smem;
+    float4* rows = smem + dp / 4;
+    for (uint32_t e = threadIdx.x; e < dp / 4; e += 256) q_l[e] = ((const float4*)(qpad + (size_t)q * dp))[e];
+    WaveTopK<R> tk;
+    tk.init();
+    float kd = __builtin_inff();
+    uint64_t ki = kNoId;
+    __shared__ uint32_t s_ci[64];
+    for (uint32_t i0 = 0; i0 < n; i0 += ch) {
+        const uint32_t cnt = min(ch, n - i0);
+        __syncthreads();  // previous chunk consumed (and q_l written)
+        if (threadIdx.x < cnt) s_ci[threadIdx.x] = cl[i0 + threadIdx.x];
+        __syncthreads();
+        // each wave copies whole rows: 64 lanes x float4 per load, independent loads
+        for (uint32_t r = w; r < cnt; r += 4) {
+            const float4* src = (const float4*)(cent_rm + (size_t)s_ci[r] * dp);
+            float4* dst = rows + r * rs;
+#pragma unroll 4
+            for (uint32_t t = lane; t < dp / 4; t += 64) dst[t] = src[t];
+        }
+        __syncthreads();
+        if (w == 0) {
+            for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
+                const uint32_t j = j0 + lane;
+                const bool valid = j < cnt;
+                float d = __builtin_inff();
+                uint32_t c = 0;
+                if (valid) {
+                    const float4* x = rows + j * rs;
+                    float acc = 0.0f;
+#pragma unroll 8
+                    for (uint32_t t = 0; t < dp / 4; ++t) acc = acc4<M>(acc, q_l[t], x[t]);
+                    d = nan_last(dist_finish<M>(acc));
+                    c = s_ci[j];
+                }
+                offer_lanes<R>(tk, valid && d <= kd, d, (uint64_t)c, (int)P, kd, ki);
+            }
+        }
+    }
+    if (w == 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t e = r * 64 + lane;
+            if (e < P) probes[(size_t)q * P + e] = (uint32_t)tk.id[r];
+        }
     }
 }
 
@@ -395,13 +643,6 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
 // the segment, which the arena's slack block keeps in bounds.
 //   compute(x, t): consume tile t (0 <= t < d4) of the current block
 //   finish(j, id): block j done; id = this lane's id slot in block j
-template <int I, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
 
 template <int T, class Compute, class Finish>
 __device__ __forceinline__ void stream_blocks(const float4* __restrict__ base, const uint64_t* __restrict__ ids,
@@ -685,11 +926,18 @@ __global__ __launch_bounds__(256) void ivf_scan_wide(ScanArgs a) {
     float* tk_d = (float*)((uint64_t*)(qlds + (size_t)(kWideGroup / 2) * d4 * 2) + (size_t)4 * kWideGroup * a.k) +
                   (size_t)wave_index() * kWideGroup * a.k;
     const uint32_t n_wide = a.counters[3];
+    // Items of one list are adjacent in the plan; dispatching them in a strided order
+    // mixes lists of many queries (VALU-heavy) with lists of few (HBM-heavy) on the
+    // CUs at every moment. The stride is a prime that does not divide n_wide, so the
+    // map is a permutation.
+    uint32_t stride = a.wide_stride;
+    if (stride > 1 && n_wide % stride == 0) stride = stride == 40009u ? 40013u : 40009u;
     for (uint32_t b = blockIdx.x; b < n_wide; b += gridDim.x) {
-        const ScanItem it = a.items_w[b];
+        const uint32_t item = stride > 1 ? (uint32_t)(((uint64_t)b * stride) % n_wide) : b;
+        const ScanItem it = a.items_w[item];
         const int np = (int)it.npairs;
         const int gp = (np + 1) / 2;
-        const int gpv = gp <= 1 ? 1 : gp <= 2 ? 2 : gp <= 3 ? 3 : gp <= 4 ? 4 : gp <= 6 ? 6 : 8;
+        const int gpv = gp;  // every pair count 1..8 has its own instantiation
         for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
             const uint32_t t = e / gpv, p = e - t * gpv;
             const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
@@ -704,10 +952,50 @@ __global__ __launch_bounds__(256) void ivf_scan_wide(ScanArgs a) {
             case 2: scan_wide_wave<2, M>(a, it, qlds, tk_d, tk_i); break;
             case 3: scan_wide_wave<3, M>(a, it, qlds, tk_d, tk_i); break;
             case 4: scan_wide_wave<4, M>(a, it, qlds, tk_d, tk_i); break;
+            case 5: scan_wide_wave<5, M>(a, it, qlds, tk_d, tk_i); break;
             case 6: scan_wide_wave<6, M>(a, it, qlds, tk_d, tk_i); break;
+            case 7: scan_wide_wave<7, M>(a, it, qlds, tk_d, tk_i); break;
             default: scan_wide_wave<8, M>(a, it, qlds, tk_d, tk_i); break;
         }
         __syncthreads();  // qlds is restaged by the next wide item
+    }
+}
+
+// Offer n contiguous (dist, id) entries to a wave top-k: 64 x kPre entries per round,
+// every load of a round issued before the first offer (the offers are dependent
+// wave-wide steps; a load between them would expose its latency each time).
+// UNIQUE: merge_results semantics (cpp:481-504) — UINT64_MAX ids are not results and
+// each id is kept once at its smallest (dist, id).
+template <int R, bool UNIQUE>
+__device__ __forceinline__ void offer_array(WaveTopK<R>& tk, const float* __restrict__ d,
+                                            const uint64_t* __restrict__ id, uint32_t n, int k, float& kd,
+                                            uint64_t& ki) {
+    constexpr int kPre = 8;
+    const int lane = lane_id();
+    for (uint32_t r0 = 0; r0 < n; r0 += 64 * kPre) {
+        float dv[kPre];
+        uint64_t iv[kPre];
+#pragma unroll
+        for (int j = 0; j < kPre; ++j) {
+            const uint32_t e = r0 + j * 64 + lane;
+            const bool v = e < n;
+            dv[j] = v ? d[e] : __builtin_inff();
+            iv[j] = v ? id[e] : kNoId;
+        }
+#pragma unroll
+        for (int j = 0; j < kPre; ++j) {
+            const bool v = r0 + j * 64 + lane < n;
+            if constexpr (UNIQUE) {
+                uint64_t mask = __ballot(v && iv[j] != kNoId && dv[j] <= kd);
+                while (mask) {
+                    const int l = __ffsll((long long)mask) - 1;
+                    mask &= mask - 1;
+                    tk.offer_unique(rd_lane(dv[j], l), rd_lane(iv[j], l), k, kd, ki);
+                }
+            } else {
+                offer_lanes<R>(tk, v && dv[j] <= kd, dv[j], iv[j], k, kd, ki);
+            }
+        }
     }
 }
 
@@ -762,14 +1050,7 @@ __device__ __forceinline__ void merge_partial_item(const uint32_t* __restrict__ 
     tk.init();
     float kd = __builtin_inff();
     uint64_t ki = kNoId;
-    const uint32_t n = cnt * k;
-    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
-        const uint32_t c = c0 + lane;
-        const bool valid = c < n;
-        const float d = valid ? part_d[base + c] : __builtin_inff();
-        const uint64_t id = valid ? part_i[base + c] : kNoId;
-        offer_lanes<R>(tk, valid && d <= kd, d, id, kk, kd, ki);
-    }
+    offer_array<R, false>(tk, part_d + base, part_i + base, cnt * k, kk, kd, ki);
     float* od = l1_d + ((size_t)l1base_qp[i] + j) * k;
     uint64_t* oi = l1_i + ((size_t)l1base_qp[i] + j) * k;
 #pragma unroll
@@ -834,14 +1115,7 @@ __global__ __launch_bounds__(256) void ivf_merge_slots(const uint32_t* __restric
     tk.init();
     float kd = __builtin_inff();
     uint64_t ki = kNoId;
-    const uint32_t n = nin * k;
-    for (uint32_t c0 = 0; c0 < n; c0 += 64) {
-        const uint32_t c = c0 + lane;
-        const bool valid = c < n;
-        const float d = valid ? sd[c] : __builtin_inff();
-        const uint64_t id = valid ? si[c] : kNoId;
-        offer_lanes<R>(tk, valid && d <= kd, d, id, kk, kd, ki);
-    }
+    offer_array<R, false>(tk, sd, si, nin * k, kk, kd, ki);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int e = r * 64 + lane;
@@ -905,6 +1179,16 @@ __global__ __launch_bounds__(256) void ivf_merge_query(const uint32_t* __restric
     tk.init();
     float kd = __builtin_inff();
     uint64_t ki = kNoId;
+    bool any_empty = false;
+    for (uint32_t p0 = 0; p0 < P; p0 += 64) {
+        const uint32_t p = p0 + lane_id();
+        any_empty |= __ballot(p < P && count_global[probes[(size_t)q * P + p]] == 0) != 0;
+    }
+    if (!any_empty) {  // every probed list non-empty: the query's P slots are contiguous
+        offer_array<R, true>(tk, slot_d + (size_t)q * P * k, slot_i + (size_t)q * P * k, P * k, (int)k, kd, ki);
+        write_final<R>(tk, k, out_d + (size_t)q * k, out_i + (size_t)q * k);
+        return;
+    }
     for (uint32_t p = 0; p < P; ++p) {
         const float* sd = nullptr;
         const uint64_t* si = nullptr;
@@ -1140,40 +1424,6 @@ __global__ __launch_bounds__(256) void kmeanspp_mindist(const float4* __restrict
     }
 }
 
-// The serial float sum of cpp:87 and the cumsum of cpp:95-96 produce the same
-// running values; one wave walks them in order, lane j latching element j.
-__global__ void kmeanspp_serial_prefix(const float* __restrict__ mind, uint64_t n, float* __restrict__ prefix,
-                                float* __restrict__ total) {
-    const int lane = lane_id();
-    float s = 0.0f;
-    for (uint64_t c0 = 0; c0 < n; c0 += 64) {
-        const uint64_t e = c0 + lane;
-        const float v = e < n ? mind[e] : 0.0f;
-        float mine = 0.0f;
-        const int cnt = (int)min<uint64_t>(64, n - c0);
-        for (int j = 0; j < cnt; ++j) {
-            s = s + rd_lane(v, j);
-            if (lane == j) mine = s;
-        }
-        if (e < n) prefix[e] = mine;
-    }
-    if (lane == 0) *total = s;
-}
-
-// First v with cumsum >= target (cpp:95-103); n if none.
-__global__ void kmeanspp_pick(const float* __restrict__ prefix, uint64_t n, float target,
-                            unsigned long long* __restrict__ out) {
-    for (uint64_t e = gtid(); e < n; e += gstride())
-        if (prefix[e] >= target) atomicMin(out, (unsigned long long)e);
-}
-
-__global__ void kmeanspp_copy_row(const float* __restrict__ vpad, uint64_t n, uint32_t dp,
-                              const unsigned long long* __restrict__ idx, float* __restrict__ dst) {
-    const uint64_t i = *idx;
-    if (i >= n) return;
-    for (uint32_t d = threadIdx.x; d < dp; d += blockDim.x) dst[d] = vpad[i * dp + d];
-}
-
 // Lloyd update (cpp:122-141): per (cluster, dim), sum members in input order,
 // then divide by the count; empty clusters keep their centroid.
 __global__ void lloyd_update(const float* __restrict__ vpad, uint32_t dp, const uint32_t* __restrict__ order,
@@ -1255,6 +1505,65 @@ void launch_select(int regs, const float* cd, uint32_t nlist, uint32_t B, uint32
     }
 }
 
+void launch_coarse_mfma(int metric, const float* cent_rm, uint32_t nlist, uint32_t dp, const float* qpad,
+                        uint32_t B, float* approx, float* delta, hipStream_t s) {
+    dim3 grid(cdiv(cdiv(nlist, 16), 4), cdiv(B, 16));
+    const bool g8 = (dp / 16) % 8 == 0;  // dp is a multiple of 64, so steps are a multiple of 4
+    if (metric == kL2) {
+        if (g8) ivf_coarse_mfma<kL2, 8><<<grid, 256, 0, s>>>(cent_rm, nlist, dp, qpad, B, approx, delta);
+        else ivf_coarse_mfma<kL2, 4><<<grid, 256, 0, s>>>(cent_rm, nlist, dp, qpad, B, approx, delta);
+    } else {
+        if (g8) ivf_coarse_mfma<kIP, 8><<<grid, 256, 0, s>>>(cent_rm, nlist, dp, qpad, B, approx, delta);
+        else ivf_coarse_mfma<kIP, 4><<<grid, 256, 0, s>>>(cent_rm, nlist, dp, qpad, B, approx, delta);
+    }
+}
+
+// Static LDS of ivf_select_rerank<R>: the four partial top-P lists, tau, n, the
+// chunk's candidate ids (plus slack).
+static constexpr size_t rerank_static_lds(int regs) { return (size_t)4 * regs * 64 * 8 + 512; }
+
+uint32_t rerank_rows(uint32_t dp, int regs) {
+    const size_t fixed = (size_t)dp * 4 + rerank_static_lds(regs);
+    const size_t row = ((size_t)dp + 4) * 4;
+    if (fixed + row > kLdsBytes) return 0;
+    return (uint32_t)std::min<size_t>(64, (kLdsBytes - fixed) / row);
+}
+
+void launch_select_rerank(int metric, int regs, const float* approx, const float* delta, const float* cent_rm,
+                          uint32_t nlist, uint32_t dp, const float* qpad, uint32_t B, uint32_t P, uint32_t* cand,
+                          uint32_t* probes, hipStream_t s) {
+    const uint32_t ch = rerank_rows(dp, regs);
+    const size_t lds = ((size_t)dp / 4 + (size_t)ch * (dp / 4 + 1)) * sizeof(float4);
+#define VDB_SR(R)                                                                                             \
+    do {                                                                                                      \
+        static const bool raised_ = [] {                                                                      \
+            /* dynamic share = the CU's LDS minus this instantiation's static arrays */                       \
+            const int dyn = (int)(kLdsBytes - rerank_static_lds(R));                                          \
+            (void)hipFuncSetAttribute((const void*)ivf_select_rerank<R, kL2>,                                 \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, dyn);                       \
+            (void)hipFuncSetAttribute((const void*)ivf_select_rerank<R, kIP>,                                 \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, dyn);                       \
+            (void)hipGetLastError();                                                                          \
+            return true;                                                                                      \
+        }();                                                                                                  \
+        (void)raised_;                                                                                        \
+        if (metric == kL2)                                                                                    \
+            ivf_select_rerank<R, kL2><<<B, 256, lds, s>>>(approx, delta, cent_rm, nlist, dp, qpad, B, P, ch,  \
+                                                          cand, probes);                                      \
+        else                                                                                                  \
+            ivf_select_rerank<R, kIP><<<B, 256, lds, s>>>(approx, delta, cent_rm, nlist, dp, qpad, B, P, ch,  \
+                                                          cand, probes);                                      \
+    } while (0)
+    switch (regs) {
+        case 1: VDB_SR(1); break;
+        case 2: VDB_SR(2); break;
+        case 4: VDB_SR(4); break;
+        case 8: VDB_SR(8); break;
+        default: VDB_SR(16); break;
+    }
+#undef VDB_SR
+}
+
 void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint32_t* count_local, uint32_t B,
                  uint32_t P, uint32_t group, int wide, ScanItem* items, ScanItem* items_w, uint32_t* counters,
                  uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp, uint32_t* nseg_qp,
@@ -1312,9 +1621,9 @@ void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipSt
     if (!grid_blocks) return;
     static const bool raised = [] {
         // wide items stage up to 16 queries in LDS: allow the whole 160 KB of a CU
-        hipFuncSetAttribute((const void*)ivf_scan_wide<kL2>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        hipFuncSetAttribute((const void*)ivf_scan_wide<kIP>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        hipFuncSetAttribute((const void*)ivf_scan_wide<kCos>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kL2>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kIP>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kCos>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
         return true;
     }();
     (void)raised;
@@ -1437,20 +1746,6 @@ void launch_mindist_update(const float4* v_il, uint64_t n, uint32_t d4, const fl
                            hipStream_t s) {
     if (!n) return;
     kmeanspp_mindist<<<launch_grid((n + 63) / 64, 4), 256, 0, s>>>(v_il, n, d4, crow, mind);
-}
-
-void launch_serial_prefix(const float* mind, uint64_t n, float* prefix, float* total, hipStream_t s) {
-    kmeanspp_serial_prefix<<<1, 64, 0, s>>>(mind, n, prefix, total);
-}
-
-void launch_first_geq(const float* prefix, uint64_t n, float target, unsigned long long* out, hipStream_t s) {
-    if (!n) return;
-    kmeanspp_pick<<<launch_grid(n), 256, 0, s>>>(prefix, n, target, out);
-}
-
-void launch_copy_row_if(const float* vpad, uint64_t n, uint32_t dp, const unsigned long long* idx, float* dst_row,
-                        hipStream_t s) {
-    kmeanspp_copy_row<<<1, 256, 0, s>>>(vpad, n, dp, idx, dst_row);
 }
 
 void launch_centroid_update(const float* vpad, uint32_t dp, const uint32_t* order, const uint32_t* offsets,

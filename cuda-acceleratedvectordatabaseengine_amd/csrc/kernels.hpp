@@ -48,6 +48,16 @@ inline int scan_group(int regs) { return scan_group_max(regs); }
 void launch_pad_rows(const float* src, uint64_t n, uint32_t dim, uint32_t dp, float* dst, hipStream_t s);
 void launch_coarse(int metric, const float4* cent_il, uint32_t nlist, uint32_t d4, const float* qpad,
                    uint32_t B, float* cd, hipStream_t s);
+// Coarse step on the matrix cores (L2 / IP): bounds-carrying approximate distances
+// [B][nlist] + their error bounds, then exact re-rank of the lists that can reach the
+// top P (bit-identical probe sets to the exact path).
+void launch_coarse_mfma(int metric, const float* cent_rm, uint32_t nlist, uint32_t dp, const float* qpad,
+                        uint32_t B, float* approx, float* delta, hipStream_t s);
+// LDS rows per re-rank chunk for padded dimension dp (0: dp too large for the MFMA path).
+uint32_t rerank_rows(uint32_t dp, int regs);
+void launch_select_rerank(int metric, int regs, const float* approx, const float* delta, const float* cent_rm,
+                          uint32_t nlist, uint32_t dp, const float* qpad, uint32_t B, uint32_t P, uint32_t* cand,
+                          uint32_t* probes, hipStream_t s);
 void launch_select(int regs, const float* cd, uint32_t nlist, uint32_t B, uint32_t P, uint32_t* probes,
                    hipStream_t s);
 void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint32_t* count_local,
@@ -76,6 +86,7 @@ struct ScanArgs {
     uint64_t* __restrict__ part_i;
     uint32_t d4;
     uint32_t k;
+    uint32_t wide_stride;  // wide-item dispatch stride (prime; 0/1 = plan order)
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k);
@@ -112,10 +123,6 @@ void launch_histogram(const uint32_t* keys, uint64_t n, uint32_t* counts, hipStr
 void launch_mindist_init(float* mind, uint64_t n, hipStream_t s);
 void launch_mindist_update(const float4* v_il, uint64_t n, uint32_t d4, const float* centroid_row,
                            float* mind, hipStream_t s);
-void launch_serial_prefix(const float* mind, uint64_t n, float* prefix, float* total, hipStream_t s);
-void launch_first_geq(const float* prefix, uint64_t n, float target, unsigned long long* out, hipStream_t s);
-void launch_copy_row_if(const float* vpad, uint64_t n, uint32_t dp, const unsigned long long* idx,
-                        float* dst_row, hipStream_t s);
 void launch_centroid_update(const float* vpad, uint32_t dp, const uint32_t* order, const uint32_t* offsets,
                             const uint32_t* counts, uint32_t nlist, uint32_t dim, float* cent_rm,
                             hipStream_t s);

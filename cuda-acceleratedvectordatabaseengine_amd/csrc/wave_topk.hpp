@@ -16,12 +16,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace vdbk {
 
 constexpr uint64_t kNoId = ~0ull;
 
 __device__ __forceinline__ bool key_less(float d1, uint64_t i1, float d2, uint64_t i2) {
-    return d1 < d2 || (d1 == d2 && i1 < i2);
+    return (d1 < d2) | ((d1 == d2) & (i1 < i2));  // bitwise: no branch around the id compare
 }
 
 __device__ __forceinline__ float rd_lane(float v, int l) {
@@ -43,6 +45,47 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
 __device__ __forceinline__ float shfl_f(float v, int src) { return __shfl(v, src); }
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// ---- lane exchanges without the LDS crossbar where gfx950 allows it ----------
+// x ^ MASK for MASK in {1, 2, 4, 8}: DPP moves inside a 16-lane row; 16: ds_swizzle
+// (bit mode, xor inside 32 lanes); 32: ds_bpermute. Callers run with every lane of
+// the wave active (the top-k code is wave-uniform).
+template <int MASK>
+__device__ __forceinline__ uint32_t xor_u32(uint32_t v) {
+    const int x = (int)v;
+    if constexpr (MASK == 1) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    else if constexpr (MASK == 2) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+    else if constexpr (MASK == 4)  // half-row mirror (i ^ 7), then quad_perm [3,2,1,0] (i ^ 3)
+        return (uint32_t)__builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false), 0x1B, 0xF, 0xF,
+                                                  false);
+    else if constexpr (MASK == 8) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    else if constexpr (MASK == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle(x, 0x401F);  // and 0x1F, xor 0x10
+    else return (uint32_t)__shfl_xor(x, MASK);
+}
+template <int MASK>
+__device__ __forceinline__ float xor_f(float v) {
+    return __uint_as_float(xor_u32<MASK>(__float_as_uint(v)));
+}
+template <int MASK>
+__device__ __forceinline__ uint64_t xor_u64(uint64_t v) {
+    return ((uint64_t)xor_u32<MASK>((uint32_t)(v >> 32)) << 32) | xor_u32<MASK>((uint32_t)v);
+}
+// lane i <- lane i - 1 (lane 0 <- fill) and lane i <- lane i + 1 (lane 63 <- fill):
+// DPP wave_shr:1 / wave_shl:1.
+__device__ __forceinline__ uint32_t up1_u32(uint32_t v, uint32_t fill) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t down1_u32(uint32_t v, uint32_t fill) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x130, 0xF, 0xF, false);
+}
 
 template <int R>
 struct WaveTopK {
@@ -82,23 +125,15 @@ struct WaveTopK {
         uint64_t carry_i = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int src = lane == 0 ? 0 : lane - 1;
-            float up_d = shfl_f(d[r], src);
-            uint64_t up_i = shfl_u64(id[r], src);
+            // lane i takes lane i-1's element; lane 0 takes the previous register's last
+            const float up_d = __uint_as_float(up1_u32(__float_as_uint(d[r]), __float_as_uint(carry_d)));
+            const uint64_t up_i = ((uint64_t)up1_u32((uint32_t)(id[r] >> 32), (uint32_t)(carry_i >> 32)) << 32) |
+                                  up1_u32((uint32_t)id[r], (uint32_t)carry_i);
             const float last_d = rd_lane(d[r], 63);
             const uint64_t last_i = rd_lane(id[r], 63);
-            if (lane == 0) {
-                up_d = carry_d;
-                up_i = carry_i;
-            }
             const int e = r * 64 + lane;
-            if (e > pos) {
-                d[r] = up_d;
-                id[r] = up_i;
-            } else if (e == pos) {
-                d[r] = cd;
-                id[r] = cid;
-            }
+            d[r] = e > pos ? up_d : (e == pos ? cd : d[r]);
+            id[r] = e > pos ? up_i : (e == pos ? cid : id[r]);
             carry_d = last_d;
             carry_i = last_i;
         }
@@ -109,22 +144,19 @@ struct WaveTopK {
         const int lane = lane_id();
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int src = lane == 63 ? 63 : lane + 1;
-            float dn_d = shfl_f(d[r], src);
-            uint64_t dn_i = shfl_u64(id[r], src);
-            if (lane == 63) {
-                if (r + 1 < R) {
-                    dn_d = rd_lane(d[r + 1 < R ? r + 1 : r], 0);
-                    dn_i = rd_lane(id[r + 1 < R ? r + 1 : r], 0);
-                } else {
-                    dn_d = __builtin_inff();
-                    dn_i = kNoId;
-                }
+            // lane 63 takes the next register's first element (or the empty key)
+            float nd = __builtin_inff();
+            uint64_t ni = kNoId;
+            if (r + 1 < R) {
+                nd = rd_lane(d[r + 1 < R ? r + 1 : r], 0);
+                ni = rd_lane(id[r + 1 < R ? r + 1 : r], 0);
             }
-            if (r * 64 + lane >= e) {
-                d[r] = dn_d;
-                id[r] = dn_i;
-            }
+            const float dn_d = __uint_as_float(down1_u32(__float_as_uint(d[r]), __float_as_uint(nd)));
+            const uint64_t dn_i = ((uint64_t)down1_u32((uint32_t)(id[r] >> 32), (uint32_t)(ni >> 32)) << 32) |
+                                  down1_u32((uint32_t)id[r], (uint32_t)ni);
+            const bool mv = r * 64 + lane >= e;
+            d[r] = mv ? dn_d : d[r];
+            id[r] = mv ? dn_i : id[r];
         }
     }
 
@@ -159,25 +191,29 @@ struct WaveTopK {
     }
 };
 
+// One compare-exchange step of a bitonic network at lane distance J: keep the
+// smaller key if keep_min, else the larger. Branch-free (selects, no exec masking).
+template <int J>
+__device__ __forceinline__ void cmpx(float& d, uint64_t& id, bool keep_min) {
+    const float od = xor_f<J>(d);
+    const uint64_t oi = xor_u64<J>(id);
+    const bool take = keep_min ? key_less(od, oi, d, id) : key_less(d, id, od, oi);
+    d = take ? od : d;
+    id = take ? oi : id;
+}
+
 // Bitonic sort of one (dist, id) per lane, ascending over lanes 0..63.
 __device__ __forceinline__ void bitonic_sort64(float& d, uint64_t& id) {
     const int lane = lane_id();
-#pragma unroll
-    for (int kk = 2; kk <= 64; kk <<= 1) {
-#pragma unroll
-        for (int j = kk >> 1; j > 0; j >>= 1) {
-            const float od = __shfl_xor(d, j);
-            const uint64_t oi = shfl_u64(id, lane ^ j);
-            const bool asc = (lane & kk) == 0;
-            const bool lower = (lane & j) == 0;
-            const bool keep_min = (lower == asc);
-            const bool take = keep_min ? key_less(od, oi, d, id) : key_less(d, id, od, oi);
-            if (take) {
-                d = od;
-                id = oi;
-            }
-        }
-    }
+    static_for<1, 7>([&](auto ks) {  // kk = 2^ks = 2 .. 64
+        constexpr int KK = 1 << decltype(ks)::value;
+        const bool asc = (lane & KK) == 0;
+        static_for<0, decltype(ks)::value>([&](auto js) {  // j = KK/2 .. 1
+            constexpr int J = (KK >> 1) >> decltype(js)::value;
+            const bool lower = (lane & J) == 0;
+            cmpx<J>(d, id, lower == asc);
+        });
+    });
 }
 
 // Sorted-ascending list (one element per lane) merged with a sorted batch: keeps
@@ -186,21 +222,13 @@ __device__ __forceinline__ void bitonic_merge64(float& ad, uint64_t& ai, float b
     const int lane = lane_id();
     const float rd = shfl_f(bd, 63 - lane);
     const uint64_t ri = shfl_u64(bi, 63 - lane);
-    if (key_less(rd, ri, ad, ai)) {
-        ad = rd;
-        ai = ri;
-    }
-#pragma unroll
-    for (int j = 32; j > 0; j >>= 1) {
-        const float od = __shfl_xor(ad, j);
-        const uint64_t oi = shfl_u64(ai, lane ^ j);
-        const bool lower = (lane & j) == 0;
-        const bool take = lower ? key_less(od, oi, ad, ai) : key_less(ad, ai, od, oi);
-        if (take) {
-            ad = od;
-            ai = oi;
-        }
-    }
+    const bool t = key_less(rd, ri, ad, ai);
+    ad = t ? rd : ad;
+    ai = t ? ri : ai;
+    static_for<0, 6>([&](auto js) {  // j = 32 .. 1
+        constexpr int J = 32 >> decltype(js)::value;
+        cmpx<J>(ad, ai, (lane & J) == 0);
+    });
 }
 
 // Fold this lane's candidate (cd, cid) — if `want` — into the list. Candidates

@@ -141,6 +141,16 @@ int vdb_ivf_set_batch(vdb_ivf* index, uint32_t batch);
  * slot content in the merge. 1 (default) reproduces it; 0 drops empty slots. */
 int vdb_ivf_set_stale_slots(vdb_ivf* index, int enable);
 
+/* Coarse-quantiser mode: 1 (default) = MFMA distance bounds + exact re-rank of the
+ * lists that can reach the top nprobe (same probe sets as mode 0); 0 = exact VALU
+ * distances of every centroid. Cosine always uses mode 0. */
+int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
+/* Engine tuning knobs by name (results never change, only speed): "coarse_mode"
+ * (0/1, as above), "wide_scan" (0/1: large lists as multi-query workgroup items),
+ * "wide_stride" (prime dispatch stride of wide items; 1 = plan order), "batch",
+ * "stale_slots" (as vdb_ivf_set_batch / vdb_ivf_set_stale_slots). */
+int vdb_ivf_set_option(vdb_ivf* index, const char* name, int64_t value);
+
 int vdb_ivf_profile_enable(vdb_ivf* index, int enable);
 int vdb_ivf_profile_reset(vdb_ivf* index);
 int vdb_ivf_profile_read(vdb_ivf* index, vdb_ivf_profile* out);  /* synchronises the stream */

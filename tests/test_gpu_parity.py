@@ -272,7 +272,9 @@ def test_hub_lists_wide_items(k):
     g.add(X, ids)
     for batch in (64, 130):
         g.set_batch(batch)
-        assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))
+        for stride in (40009, 1, 7):   # wide-item dispatch order never changes results
+            g.set_option("wide_stride", stride)
+            assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))
 
 
 def test_launches_beyond_2_32_workitems():
@@ -360,3 +362,68 @@ def test_concurrent_streams_match_sequential():
     Dr = np.concatenate([o.search(Q[b * 64:(b + 1) * 64], 4, 10)[0] for b in range(8)])
     Ir = np.concatenate([o.search(Q[b * 64:(b + 1) * 64], 4, 10)[1] for b in range(8)])
     assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), Dr, Ir)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("nprobe", [1, 7, 64, 100, 300])
+def test_mfma_coarse_selects_exact_probe_sets(metric, nprobe):
+    """The MFMA coarse step (distance bounds + exact re-rank) must pick the same
+    probe lists as the reference's sequential distances (select_nprobe_lists,
+    ivf_flat_index.cpp:298-336), including P > 64 and P = nlist."""
+    rng = np.random.default_rng(100 + nprobe)
+    dim, nlist = 96, 300
+    X = rng.standard_normal((20000, dim)).astype(np.float32)
+    Q = rng.standard_normal((70, dim)).astype(np.float32)
+    ids = np.arange(len(X), dtype=np.uint64)
+    o = oracle.OracleIndex(dim, nlist, metric)
+    o.centroids = X[:nlist] * 0.3
+    o.add(X, ids)
+    for mode in (1, 0):
+        g = mirror_from_oracle(o, dim, nlist, metric)
+        g.set_coarse_mode(mode)
+        g.add(X, ids)
+        assert_same(*g.search(Q, nprobe=nprobe, k=10), *o.search(Q, nprobe, 10))
+
+
+def test_mfma_coarse_near_ties():
+    """Centroids one ulp apart and exact duplicates: the approximate order differs
+    from the exact one; the re-rank must restore (dist, list_id) order exactly."""
+    rng = np.random.default_rng(5)
+    dim, nlist = 64, 256
+    base = rng.standard_normal((32, dim)).astype(np.float32)
+    C = np.repeat(base, 8, axis=0)
+    bump = rng.integers(-2, 3, size=C.shape).astype(np.int32)
+    C = (C.view(np.int32) + bump * (np.arange(len(C)) % 8 != 0)[:, None]).view(np.float32)  # ulp jitter, 1 exact copy
+    C[1::8] = C[0::8]                                                                       # exact duplicates
+    X = rng.standard_normal((8000, dim)).astype(np.float32)
+    Q = np.concatenate([base + 1e-3 * rng.standard_normal(base.shape).astype(np.float32),
+                        rng.standard_normal((32, dim)).astype(np.float32)])
+    ids = np.arange(len(X), dtype=np.uint64)
+    o = oracle.OracleIndex(dim, nlist, 0)
+    o.centroids = C
+    o.add(X, ids)
+    for nprobe in (3, 8, 20):
+        probes_ref = np.stack([o.select_nprobe(q, nprobe) for q in Q])
+        g = mirror_from_oracle(o, dim, nlist)
+        g.add(X, ids)
+        assert_same(*g.search(Q, nprobe=nprobe, k=10), *o.search(Q, nprobe, 10))
+        assert probes_ref.shape == (len(Q), nprobe)
+
+
+def test_nan_query_is_contained():
+    """A NaN query must not make the engine read outside its lists (no crash), and
+    the other queries of the batch keep their exact results."""
+    X, Q, ids = oracle.reference_test_data(3000, 12, 16, seed=8)
+    o = oracle.OracleIndex(16, 10, 0)
+    o.centroids = X[:10]
+    o.add(X, ids)
+    g = mirror_from_oracle(o, 16, 10)
+    g.add(X, ids)
+    Qn = Q.copy()
+    Qn[3, 5] = np.nan
+    for mode in (1, 0):
+        g.set_coarse_mode(mode)
+        D, I = g.search(Qn, nprobe=4, k=5)
+        keep = np.arange(len(Q)) > 3          # rows after the NaN row (rows before it are unaffected too)
+        Dr, Ir = o.search(Q[keep], 4, 5)
+        assert_same(D[keep], I[keep], Dr, Ir)

@@ -53,6 +53,7 @@ fi
 if has pmc; then
     # HBM bytes of the scan kernels (FETCH_SIZE; x2 on gfx950, MI355X_MICROARCH.md §HBM)
     run pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ivf_scan_ -d "$O/pmc_f" -o f -f csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --prof-steps 2 $BARGS
+    python3 tools/pmc_traffic.py "$O/pmc_f" 8 "10000000x768/4096/32/64/10/N1" "$O/traffic.json" | head -8
     run pmc_sq 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES --kernel-include-regex ivf_scan_ -d "$O/pmc_s" -o s -f csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --prof-steps 2 $BARGS
 fi
 echo "session $TAG done"
