@@ -644,22 +644,31 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
 //   compute(x, t): consume tile t (0 <= t < d4) of the current block
 //   finish(j, id): block j done; id = this lane's id slot in block j
 
+// List data is read once per batch: non-temporal loads (nt) keep it from displacing
+// reusable lines and stream measurably faster on gfx950 (tools/stream_probe.hip:
+// 6.8 vs 6.25 TB/s for this access pattern).
+typedef float v4f_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 load_nt(const float4* p) {
+    const v4f_nt v = __builtin_nontemporal_load((const v4f_nt*)p);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 template <int T, class Compute, class Finish>
 __device__ __forceinline__ void stream_blocks(const float4* __restrict__ base, const uint64_t* __restrict__ ids,
                                               uint32_t d4, uint32_t nb, Compute&& compute, Finish&& finish) {
     float4 x[T];
     const float4* p = base;
 #pragma unroll
-    for (int t = 0; t < T; ++t) x[t] = p[(size_t)t * 64];
-    uint64_t id_next = ids[0];
+    for (int t = 0; t < T; ++t) x[t] = load_nt(p + (size_t)t * 64);
+    uint64_t id_next = __builtin_nontemporal_load(ids);
     for (uint32_t j = 0; j < nb; ++j) {
         const uint64_t id = id_next;
-        id_next = ids[(size_t)(j + 1) * 64];
+        id_next = __builtin_nontemporal_load(ids + (size_t)(j + 1) * 64);
         for (uint32_t t0 = 0; t0 < d4; t0 += T) {
             static_for<0, T>([&](auto u) {
                 constexpr int t = decltype(u)::value;
                 compute(x[t], t0 + t, u);
-                x[t] = p[(size_t)(T + t) * 64];
+                x[t] = load_nt(p + (size_t)(T + t) * 64);
             });
             p += (size_t)T * 64;
         }

@@ -21,8 +21,13 @@
     } while (0)
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldnt(const float4* p) {
+    const v4f v = __builtin_nontemporal_load((const v4f*)p);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 
-template <int T, int WORK>
+template <int T, int WORK, bool NT = false>
 __global__ __launch_bounds__(256) void seg_stream(const float4* __restrict__ buf, uint64_t seg_tiles, uint64_t nseg,
                                                   float* __restrict__ sink) {
     const int lane = threadIdx.x & 63;
@@ -33,7 +38,7 @@ __global__ __launch_bounds__(256) void seg_stream(const float4* __restrict__ buf
         const float4* p = buf + s * seg_tiles * 64 + lane;
         float4 x[T];
 #pragma unroll
-        for (int t = 0; t < T; ++t) x[t] = p[(size_t)t * 64];
+        for (int t = 0; t < T; ++t) x[t] = NT ? ldnt(p + (size_t)t * 64) : p[(size_t)t * 64];
         for (uint64_t t0 = 0; t0 < seg_tiles; t0 += T) {
 #pragma unroll
             for (int t = 0; t < T; ++t) {
@@ -45,7 +50,7 @@ __global__ __launch_bounds__(256) void seg_stream(const float4* __restrict__ buf
                 }
                 acc = acc + a + b;
                 // the last round prefetches up to T tiles into the next segment (or the slack)
-                x[t] = p[(size_t)(T + t) * 64];
+                x[t] = NT ? ldnt(p + (size_t)(T + t) * 64) : p[(size_t)(T + t) * 64];
             }
             p += (size_t)T * 64;
         }
@@ -96,14 +101,15 @@ int main(int argc, char** argv) {
         const double ms = time_ms([&] { flat_stream<<<256 * 32, 256>>>(buf, bytes / 16, sink); });
         printf("flat grid-stride float4       : %.3f ms  %.2f TB/s\n", ms, bytes / ms / 1e9);
     }
-#define RUN(T, W, WGS)                                                                                         \
+#define RUN(T, W, WGS, NT)                                                                                     \
     {                                                                                                          \
         const uint32_t grid = 256 * (WGS);                                                                     \
-        const double ms = time_ms([&] { seg_stream<T, W><<<grid, 256>>>(buf, seg_tiles, nseg, sink); });       \
-        printf("segments T=%2d work=%d wg/cu=%d : %.3f ms  %.2f TB/s\n", T, W, WGS, ms, bytes / ms / 1e9);      \
+        const double ms = time_ms([&] { seg_stream<T, W, NT><<<grid, 256>>>(buf, seg_tiles, nseg, sink); });   \
+        printf("segments T=%2d work=%d wg/cu=%d nt=%d : %.3f ms  %.2f TB/s\n", T, W, WGS, (int)NT, ms,          \
+               bytes / ms / 1e9);                                                                              \
     }
-    RUN(8, 0, 2) RUN(16, 0, 2) RUN(16, 0, 3) RUN(16, 0, 4) RUN(8, 0, 4) RUN(4, 0, 4) RUN(16, 0, 8)
-    RUN(16, 8, 2) RUN(16, 16, 2) RUN(16, 24, 2) RUN(16, 16, 3) RUN(16, 24, 3) RUN(8, 16, 2)
+    RUN(16, 0, 2, false) RUN(16, 0, 2, true) RUN(8, 0, 2, true) RUN(16, 0, 4, true) RUN(16, 16, 2, false)
+    RUN(16, 16, 2, true) RUN(16, 24, 2, true) RUN(8, 16, 3, true)
     CHECK(hipFree(buf));
     return 0;
 }
