@@ -448,7 +448,7 @@ struct vdb_ivf {
         w.pbqp.ensure(BP);
         w.sorted_pair.ensure(BP);
         w.pbs.ensure(BP);
-        w.counters.ensure(4);
+        w.counters.ensure(8);
         w.l1base.ensure(BP);
         w.l1_items.ensure(max_l1);
         w.l1_d.ensure(max_l1 * k);
@@ -493,7 +493,7 @@ struct vdb_ivf {
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
         const vdbk::ScanArgs sa{arena.p, arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
-                                wide_stride};
+                                wide_stride, w.counters.p + 4};
         if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));

@@ -619,6 +619,8 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         counters[1] = nparts;
         counters[2] = nl1;
         counters[3] = n_wide;
+        counters[4] = 0;  // work queues of the persistent scan kernels (narrow waves, wide workgroups)
+        counters[5] = 0;
         atomicAdd(&stats[0], (unsigned long long)nd);
         atomicAdd(&stats[2], (unsigned long long)(n_narrow + n_wide));
         atomicAdd(&stats[3], 1ull);
@@ -914,12 +916,16 @@ __device__ __forceinline__ void scan_narrow(const ScanArgs& a, const ScanItem it
 // lists: each wave takes one narrow item (one segment x <= 4 queries, queries via
 // scalar loads, top-k in registers).
 template <int R, int M>
+// Persistent: a grid sized to the machine, each wave pulling items from a queue
+// (one device-scope atomic per item) until the batch's items run out.
 __global__ __launch_bounds__(256) void ivf_scan_narrow(ScanArgs a) {
     const uint32_t n_narrow = a.counters[0];
-    const uint32_t nblocks = (n_narrow + 3) / 4;
-    for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-        const uint32_t idx = b * 4 + wave_index();
-        if (idx < n_narrow) scan_narrow<R, M>(a, a.items[idx]);
+    for (;;) {
+        uint32_t idx = 0;
+        if (lane_id() == 0) idx = atomicAdd(&a.work[0], 1u);
+        idx = __builtin_amdgcn_readfirstlane(idx);
+        if (idx >= n_narrow) break;
+        scan_narrow<R, M>(a, a.items[idx]);
     }
 }
 
@@ -941,7 +947,13 @@ __global__ __launch_bounds__(256) void ivf_scan_wide(ScanArgs a) {
     // map is a permutation.
     uint32_t stride = a.wide_stride;
     if (stride > 1 && n_wide % stride == 0) stride = stride == 40009u ? 40013u : 40009u;
-    for (uint32_t b = blockIdx.x; b < n_wide; b += gridDim.x) {
+    __shared__ uint32_t s_next;
+    for (;;) {
+        // persistent workgroups pull items from a queue (one atomic per item)
+        if (threadIdx.x == 0) s_next = atomicAdd(&a.work[1], 1u);
+        __syncthreads();
+        const uint32_t b = s_next;
+        if (b >= n_wide) break;
         const uint32_t item = stride > 1 ? (uint32_t)(((uint64_t)b * stride) % n_wide) : b;
         const ScanItem it = a.items_w[item];
         const int np = (int)it.npairs;
@@ -1601,15 +1613,17 @@ void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes
 #undef VDB_MP
 }
 
+static constexpr size_t kWideStaticLds = 64;  // ivf_scan_wide's static LDS (the queue slot), rounded up
+
 size_t scan_wide_lds(uint32_t d4, uint32_t k) {
     return (size_t)(kWideGroup / 2) * d4 * 2 * sizeof(float4) + (size_t)4 * kWideGroup * k * (sizeof(float) + sizeof(uint64_t));
 }
 
-bool scan_wide_fits(uint32_t d4, uint32_t k) { return k <= 64 && scan_wide_lds(d4, k) <= kLdsBytes; }
+bool scan_wide_fits(uint32_t d4, uint32_t k) { return k <= 64 && scan_wide_lds(d4, k) <= kLdsBytes - kWideStaticLds; }
 
 void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
     if (!grid_blocks) return;
-    const uint32_t g = launch_grid(grid_blocks, 1);
+    const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
 #define VDB_SN(R)                                                             \
     do {                                                                      \
         if (metric == kL2) ivf_scan_narrow<R, kL2><<<g, 256, 0, s>>>(a);      \
@@ -1630,14 +1644,16 @@ void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipSt
     if (!grid_blocks) return;
     static const bool raised = [] {
         // wide items stage up to 16 queries in LDS: allow the whole 160 KB of a CU
-        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kL2>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kIP>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kCos>, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        const int dyn = (int)(kLdsBytes - kWideStaticLds);
+        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kL2>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kIP>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kCos>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+        (void)hipGetLastError();
         return true;
     }();
     (void)raised;
     const size_t lds = scan_wide_lds(a.d4, a.k);
-    const uint32_t g = launch_grid(grid_blocks, 1);
+    const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
     if (metric == kL2) ivf_scan_wide<kL2><<<g, 256, lds, s>>>(a);
     else if (metric == kIP) ivf_scan_wide<kIP><<<g, 256, lds, s>>>(a);
     else ivf_scan_wide<kCos><<<g, 256, lds, s>>>(a);

@@ -26,6 +26,7 @@ constexpr int kNarrowMax = 4;              // pairs per narrow scan item
 constexpr int kPlanMaxPairs = 8192;        // batch * nprobe per plan launch
 constexpr int kMaxK = 1024;                // top-k capacity (16 registers x 64 lanes)
 constexpr size_t kLdsBytes = 160 * 1024;   // LDS per CU (gfx950)
+constexpr uint32_t kPersistentBlocks = 512; // scan grid: 2 workgroups per CU on 256 CUs
 
 struct ScanItem {
     uint32_t list;
@@ -87,6 +88,7 @@ struct ScanArgs {
     uint32_t d4;
     uint32_t k;
     uint32_t wide_stride;  // wide-item dispatch stride (prime; 0/1 = plan order)
+    uint32_t* work;        // [2] item queues (narrow, wide), reset by the plan kernel
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k);
