@@ -265,11 +265,38 @@ __global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict
     const float* ar = approx + (size_t)q * nlist;
     const float* dr = delta + (size_t)q * nlist;
     if (threadIdx.x == 0) s_n = 0;
-    // pass 1: each wave's top-P upper bounds over its quarter (c = w*64 + 256 j + lane).
-    // The wave's lists are read in rounds of kPre per lane, all loads issued up front
-    // (a dependent offer between loads would expose the memory latency per load).
+    // pass 1: tau, an upper bound on the P-th smallest upper bound. Lists are read in
+    // rounds of kPre per lane (c = w*64 + 256 j + lane), every load issued up front.
     constexpr int kPre = 16;
-    {
+    if constexpr (R == 1) {
+        // P <= 64: the P-th smallest of the block's 256 lane minima. P lanes hold a
+        // value <= it, so at least P upper bounds are <= it; no top-P list is needed.
+        float lm = __builtin_inff();
+        for (uint32_t r0 = w * 64; r0 < nlist; r0 += 256 * kPre) {
+            float hv[kPre];
+#pragma unroll
+            for (int j = 0; j < kPre; ++j) {
+                const uint32_t c = r0 + j * 256 + lane;
+                hv[j] = c < nlist ? nan_last(ar[c] + dr[c]) : __builtin_inff();
+            }
+#pragma unroll
+            for (int j = 0; j < kPre; ++j) lm = hv[j] < lm ? hv[j] : lm;
+        }
+        uint64_t li = (uint64_t)(w * 64 + lane);
+        bitonic_sort64(lm, li);
+        s_top_d[w * 64 + lane] = lm;
+        s_top_i[w * 64 + lane] = (uint32_t)li;
+        __syncthreads();
+        if (w == 0) {
+            float a = s_top_d[lane];
+            uint64_t ai = s_top_i[lane];
+            for (int v = 1; v < 4; ++v) bitonic_merge64(a, ai, s_top_d[v * 64 + lane], s_top_i[v * 64 + lane]);
+            const float t = rd_lane(a, (int)P - 1);
+            if (lane == 0) s_tau = t;
+        }
+        __syncthreads();
+    } else {
+        // P > 64: each wave's top-P upper bounds, then the P-th smallest of their union
         WaveTopK<R> tk;
         tk.init();
         float kd = __builtin_inff();
@@ -292,22 +319,22 @@ __global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict
             s_top_d[(w * R + r) * 64 + lane] = tk.d[r];
             s_top_i[(w * R + r) * 64 + lane] = (uint32_t)tk.id[r];
         }
-    }
-    __syncthreads();
-    if (w == 0) {  // tau = P-th smallest of the four partial lists
-        WaveTopK<R> tk;
-        tk.init();
-        float kd = __builtin_inff();
-        uint64_t ki = kNoId;
-        for (uint32_t e0 = 0; e0 < 4 * R * 64; e0 += 64) {
-            const float d = s_top_d[e0 + lane];
-            const uint32_t id = s_top_i[e0 + lane];
-            const bool valid = id != 0xFFFFFFFFu;
-            offer_lanes<R>(tk, valid && d <= kd, d, (uint64_t)id, (int)P, kd, ki);
+        __syncthreads();
+        if (w == 0) {
+            WaveTopK<R> tk2;
+            tk2.init();
+            float kd2 = __builtin_inff();
+            uint64_t ki2 = kNoId;
+            for (uint32_t e0 = 0; e0 < 4 * R * 64; e0 += 64) {
+                const float d = s_top_d[e0 + lane];
+                const uint32_t id = s_top_i[e0 + lane];
+                const bool valid = id != 0xFFFFFFFFu;
+                offer_lanes<R>(tk2, valid && d <= kd2, d, (uint64_t)id, (int)P, kd2, ki2);
+            }
+            if (lane == 0) s_tau = kd2;
         }
-        if (lane == 0) s_tau = kd;
+        __syncthreads();
     }
-    __syncthreads();
     const float tau = s_tau;
     // pass 2: candidates, appended through one LDS counter per wave-iteration
     uint32_t* cl = cand + (size_t)q * nlist;
@@ -334,7 +361,7 @@ __global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict
     const uint32_t n = s_n;
     // pass 3: exact sequential distances of the candidates, ch rows at a time
     const uint32_t rs = dp / 4 + 1;  // LDS row stride in float4 (one float4 of padding)
-    float4* q_l = smem;
+    float4* q_l = smem;  // the query row (broadcast reads)
     float4* rows = smem + dp / 4;
     for (uint32_t e = threadIdx.x; e < dp / 4; e += 256) q_l[e] = ((const float4*)(qpad + (size_t)q * dp))[e];
     WaveTopK<R> tk;
@@ -344,31 +371,53 @@ __global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict
     __shared__ uint32_t s_ci[64];
     for (uint32_t i0 = 0; i0 < n; i0 += ch) {
         const uint32_t cnt = min(ch, n - i0);
-        __syncthreads();  // previous chunk consumed (and q_l written)
+        __syncthreads();  // previous chunk consumed
         if (threadIdx.x < cnt) s_ci[threadIdx.x] = cl[i0 + threadIdx.x];
         __syncthreads();
-        // each wave copies whole rows: 64 lanes x float4 per load, independent loads
-        for (uint32_t r = w; r < cnt; r += 4) {
-            const float4* src = (const float4*)(cent_rm + (size_t)s_ci[r] * dp);
-            float4* dst = rows + r * rs;
-#pragma unroll 4
-            for (uint32_t t = lane; t < dp / 4; t += 64) dst[t] = src[t];
+        // rows to LDS: independent loads, up to 32 per thread in flight (one round for
+        // the usual ~40 candidate rows at 768 dims)
+        const uint32_t n4 = dp / 4;
+        const uint32_t tot = cnt * n4;
+        for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += 256 * 24) {
+            float4 v[24];
+#pragma unroll
+            for (int u = 0; u < 24; ++u) {  // unconditional (clamped) loads keep v in registers
+                const uint32_t e = min(e0 + u * 256, tot - 1);
+                const uint32_t r = e / n4, t = e - r * n4;
+                v[u] = ((const float4*)(cent_rm + (size_t)s_ci[r] * dp))[t];
+            }
+#pragma unroll
+            for (int u = 0; u < 24; ++u) {
+                const uint32_t e = e0 + u * 256;
+                const uint32_t r = e / n4, t = e - r * n4;
+                if (e < tot) rows[r * rs + t] = v[u];
+            }
         }
         __syncthreads();
         if (w == 0) {
+            // lane j: sequential sum over candidate row j; LDS reads double-buffered 8
+            // float4 ahead of the dependent add chain (n4 is a multiple of 16)
             for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
                 const uint32_t j = j0 + lane;
                 const bool valid = j < cnt;
-                float d = __builtin_inff();
-                uint32_t c = 0;
-                if (valid) {
-                    const float4* x = rows + j * rs;
-                    float acc = 0.0f;
-#pragma unroll 8
-                    for (uint32_t t = 0; t < dp / 4; ++t) acc = acc4<M>(acc, q_l[t], x[t]);
-                    d = nan_last(dist_finish<M>(acc));
-                    c = s_ci[j];
+                const float4* x = rows + (valid ? j : 0) * rs;
+                float acc = 0.0f;
+                float4 xa[8], qa[8], xb[8], qb[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xa[u] = x[u], qa[u] = q_l[u];
+                for (uint32_t t0 = 0; t0 < n4; t0 += 16) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) xb[u] = x[t0 + 8 + u], qb[u] = q_l[t0 + 8 + u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc = acc4<M>(acc, qa[u], xa[u]);
+                    const uint32_t tn = t0 + 16 < n4 ? t0 + 16 : 0;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) xa[u] = x[tn + u], qa[u] = q_l[tn + u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) acc = acc4<M>(acc, qb[u], xb[u]);
                 }
+                const float d = valid ? nan_last(dist_finish<M>(acc)) : __builtin_inff();
+                const uint32_t c = valid ? s_ci[j] : 0u;
                 offer_lanes<R>(tk, valid && d <= kd, d, (uint64_t)c, (int)P, kd, ki);
             }
         }

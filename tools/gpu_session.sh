@@ -42,6 +42,12 @@ if has bench; then
     grep '^{' "$O/bench.log" > "$O/bench.json"
     cat "$O/bench.json"
 fi
+if has multi; then
+    # one-GPU rehearsal of the N-rank path: 2 ranks on cuda:0, gloo exchange staged through host
+    run multi 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --same-device --dist-backend gloo --steps 20 --warmup 3 --no-cpu --prof-steps 4
+    grep '^{' "$O/multi.log" > "$O/multi.json"
+    cat "$O/multi.json"
+fi
 if has dump; then
     run dump 600 python -u tests/debug_dump_index.py 10000000 4096
 fi
