@@ -148,6 +148,9 @@ def main():
                     help="single-stream steps timed per launch (roofline, one-in-flight latency)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per ivf_scan launch for this workload (or null)")
+    ap.add_argument("--emulate-shard", type=int, default=0, metavar="W",
+                    help="diagnostic: one process keeps rank 0's LPT shard of W and runs its partial search "
+                         "(the per-GPU work of a W-GPU node, without the all-gather); not a bench line")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning knob (vdb_ivf_set_option), e.g. wide_stride=1; results never change")
     args = ap.parse_args()
@@ -175,6 +178,8 @@ def run(vdb, args, device, rank, world):
     for o in args.opt:
         name, val = o.split("=", 1)
         idx.set_option(name, int(val))
+    if args.emulate_shard > 1 and world == 1:
+        idx.set_shard(0, args.emulate_shard)
     B, k = args.batch, args.k
     nq = (args.warmup + args.steps + args.prof_steps) * B
     main_stream = torch.cuda.current_stream()
@@ -200,10 +205,12 @@ def run(vdb, args, device, rank, world):
     # concurrent search its own workspace slot, so one batch's small kernels and scan
     # tail overlap the next batch's scan. Rank partials and gathers are per stream.
     streams = [main_stream] + [torch.cuda.Stream(device) for _ in range(args.inflight - 1)]
-    part_d = [torch.empty((B, k), dtype=torch.float32, device=device) for _ in streams]
-    part_i = [torch.empty((B, k), dtype=torch.int64, device=device) for _ in streams]
-    gat_d = [torch.empty((world, B, k), dtype=torch.float32, device=device) for _ in streams]
-    gat_i = [torch.empty((world, B, k), dtype=torch.int64, device=device) for _ in streams]
+    # One packed record per rank and batch (f32 dist[B][k] | pad | u64 ids[B][k]): ONE
+    # all-gather per batch over RCCL, then the on-device merge of the world records.
+    rec = vdb.rank_record_bytes(B, k)
+    ids_off = vdb.rank_record_ids_offset(B, k)
+    part = [torch.empty(rec, dtype=torch.uint8, device=device) for _ in streams]
+    gat = [torch.empty(world * rec, dtype=torch.uint8, device=device) for _ in streams]
     torch.cuda.synchronize()
 
     def step(s, slot):
@@ -214,20 +221,16 @@ def run(vdb, args, device, rank, world):
                 idx.search_device(q.data_ptr(), B, args.nprobe, k, out_d[s * B:].data_ptr(), out_i[s * B:].data_ptr(),
                                   st.cuda_stream)
             else:
-                idx.search_device(q.data_ptr(), B, args.nprobe, k, part_d[slot].data_ptr(), part_i[slot].data_ptr(),
-                                  st.cuda_stream)
+                p0 = part[slot].data_ptr()
+                idx.search_device(q.data_ptr(), B, args.nprobe, k, p0, p0 + ids_off, st.cuda_stream)
                 if args.dist_backend == "nccl":
-                    dist.all_gather_into_tensor(gat_d[slot], part_d[slot])
-                    dist.all_gather_into_tensor(gat_i[slot], part_i[slot])
+                    dist.all_gather_into_tensor(gat[slot], part[slot])
                 else:  # gloo (one-GPU rehearsal): the same exchange staged through host memory
-                    hd = torch.empty((world * B, k), dtype=torch.float32)
-                    hi = torch.empty((world * B, k), dtype=torch.int64)
-                    dist.all_gather_into_tensor(hd, part_d[slot].cpu())
-                    dist.all_gather_into_tensor(hi, part_i[slot].cpu())
-                    gat_d[slot].copy_(hd.view(world, B, k))
-                    gat_i[slot].copy_(hi.view(world, B, k))
-                vdb.merge_ranks_device(gat_d[slot].data_ptr(), gat_i[slot].data_ptr(), world, B, k,
-                                       out_d[s * B:].data_ptr(), out_i[s * B:].data_ptr(), st.cuda_stream)
+                    h = torch.empty(world * rec, dtype=torch.uint8)
+                    dist.all_gather_into_tensor(h, part[slot].cpu())
+                    gat[slot].copy_(h)
+                vdb.merge_ranks_packed_device(gat[slot].data_ptr(), world, B, k, out_d[s * B:].data_ptr(),
+                                              out_i[s * B:].data_ptr(), st.cuda_stream)
 
     for s in range(args.warmup):
         step(s, s % len(streams))
@@ -321,7 +324,8 @@ def run(vdb, args, device, rank, world):
                         f"batch {B}, k {k}",
             "nvec": args.nvec, "dim": args.dim, "nlist": args.nlist, "nprobe": args.nprobe, "batch": B, "k": k,
             "train_vectors": min(args.train, args.nvec),
-            "parallelism": (f"lists sharded over {world} rank(s) (LPT), RCCL all-gather of per-rank top-k"
+            "parallelism": (f"lists sharded over {world} rank(s) (LPT), one all-gather per batch of per-rank top-k "
+                            f"({'RCCL' if args.dist_backend == 'nccl' else 'gloo, host-staged rehearsal'})"
                             if world > 1 else "single GPU") + f"; {args.inflight} batches in flight",
         },
         "roofline": {
@@ -341,10 +345,12 @@ def run(vdb, args, device, rank, world):
         },
         "build": build_info,
         "engine_options": dict(o.split("=", 1) for o in args.opt),
+        **({"emulated_shard": f"rank 0 of {args.emulate_shard} (partial results; diagnostic, not a bench line)"}
+           if args.emulate_shard > 1 else {}),
     }
     if parity_multi is not None:
         result["parity_vs_single_gpu"] = {"batches": min(args.check_batches, args.steps), "bit_identical": parity_multi}
-    if world == 1 and rank == 0 and not args.no_cpu:
+    if world == 1 and rank == 0 and not args.no_cpu and args.emulate_shard <= 1:
         qh = queries[: args.cpu_queries].cpu().numpy()
         result["cpu_baseline"] = cpu_baseline(vdb, idx, args, qh, args.cpu_budget)
     if rank == 0:

@@ -95,6 +95,8 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_set_shard": (ctypes.c_int, [vp, u32, u32]),
         "vdb_merge_ranks_device": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp, vp]),
         "vdb_shard_plan": (ctypes.c_int, [vp, u32, u32, vp]),
+        "vdb_rank_record_bytes": (u64, [u32, u32]),
+        "vdb_merge_ranks_packed_device": (ctypes.c_int, [vp, u32, u32, u32, vp, vp, vp]),
         "vdb_ivf_warmup": (ctypes.c_int, [vp, vp, u32]),
         "vdb_ivf_evict": (ctypes.c_int, [vp, u32]),
         "vdb_ivf_gpu_bytes": (u64, [vp]),
@@ -153,6 +155,22 @@ def merge_ranks_device(dist_ptr: int, ids_ptr: int, nranks: int, n: int, k: int,
     _check(lib().vdb_merge_ranks_device(ctypes.c_void_p(dist_ptr), ctypes.c_void_p(ids_ptr), nranks, n, k,
                                         ctypes.c_void_p(out_dist_ptr), ctypes.c_void_p(out_ids_ptr),
                                         ctypes.c_void_p(stream or 0)))
+
+
+def rank_record_bytes(n: int, k: int) -> int:
+    """Bytes of one rank's packed partial record (f32 dist [n][k], pad to 8, u64 ids [n][k])."""
+    return int(lib().vdb_rank_record_bytes(n, k))
+
+
+def rank_record_ids_offset(n: int, k: int) -> int:
+    return (n * k * 4 + 7) // 8 * 8
+
+
+def merge_ranks_packed_device(records_ptr: int, nranks: int, n: int, k: int, out_dist_ptr: int, out_ids_ptr: int,
+                              stream: int | None = None):
+    _check(lib().vdb_merge_ranks_packed_device(ctypes.c_void_p(records_ptr), nranks, n, k,
+                                               ctypes.c_void_p(out_dist_ptr), ctypes.c_void_p(out_ids_ptr),
+                                               ctypes.c_void_p(stream or 0)))
 
 
 class IVFFlatIndex:

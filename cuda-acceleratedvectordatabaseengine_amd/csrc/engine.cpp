@@ -139,7 +139,9 @@ struct vdb_ivf {
     int stale = 1;
     bool wide_scan = true;
     int coarse_mode = 1;
-    uint32_t wide_stride = 1;  // wide-item dispatch permutation (1 = plan order; measured best)  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
+    uint32_t wide_stride = 1;  // wide-item dispatch permutation (1 = plan order; measured best)
+    uint32_t seg_blocks = vdbk::kMaxSegBlocks;  // current segment size (blocks of 64 vectors)
+    uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
 
     // Search workspaces: a ring of slots so that searches issued on different streams
     // run concurrently (one batch's small kernels and scan tail overlap the next
@@ -197,12 +199,24 @@ struct vdb_ivf {
     // Upload the list directory and recompute the segment-count prefix.
     void upload_directory() {
         quiesce();
+        // Segment size: the largest of 512/256/128/64 vectors that still cuts this
+        // handle's lists into >= 4096 segments, so a shard of an 8-GPU node keeps
+        // enough scan work items for load balance (measured on a 1/8 shard of the
+        // 10M x 768 index: 256 beats 512 by 5 % and 64 by 9 %).
+        uint64_t local = 0;
+        for (uint32_t l = 0; l < nlist; ++l) local += owned[l] ? count[l] : 0;
+        if (seg_blocks_opt) {
+            seg_blocks = seg_blocks_opt;
+        } else {
+            seg_blocks = vdbk::kMaxSegBlocks;
+            while (seg_blocks > 1 && local / ((uint64_t)seg_blocks * 64) < 4096) seg_blocks >>= 1;
+        }
         std::vector<uint32_t> cl(nlist), cg(nlist), ns(nlist);
         for (uint32_t l = 0; l < nlist; ++l) {
             require(count[l] < (1ull << 32), "list longer than 2^32 vectors", VDB_ERR_UNSUPPORTED);
             cg[l] = (uint32_t)count[l];
             cl[l] = owned[l] ? (uint32_t)count[l] : 0u;
-            ns[l] = (uint32_t)cdiv(cl[l], vdbk::kSegVectors);
+            ns[l] = (uint32_t)cdiv(cl[l], (uint64_t)seg_blocks * 64);
         }
         HIPCHECK(hipMemcpyAsync(d_block_off.ensure(nlist), block_off.data(), nlist * 8, hipMemcpyHostToDevice, stream));
         HIPCHECK(hipMemcpyAsync(d_count_local.ensure(nlist), cl.data(), nlist * 4, hipMemcpyHostToDevice, stream));
@@ -493,7 +507,7 @@ struct vdb_ivf {
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
         const vdbk::ScanArgs sa{arena.p, arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
-                                wide_stride, w.counters.p + 4};
+                                wide_stride, w.counters.p + 4, seg_blocks};
         if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));
@@ -822,7 +836,26 @@ int vdb_merge_ranks_device(const float* d_dist, const uint64_t* d_ids, uint32_t 
         if (n == 0 || k == 0) return;
         require(d_dist && d_ids && d_out_dist && d_out_ids && nranks > 0, "null argument");
         require(k <= (uint32_t)vdbk::kMaxK, "k above 1024 is not supported", VDB_ERR_UNSUPPORTED);
-        vdbk::launch_rank_merge(vdbk::topk_regs(k), d_dist, d_ids, nranks, n, k, d_out_dist, d_out_ids,
+        vdbk::launch_rank_merge(vdbk::topk_regs(k), d_dist, d_ids, (uint64_t)n * k, (uint64_t)n * k, nranks, n, k,
+                                d_out_dist, d_out_ids, (hipStream_t)stream);
+        HIPCHECK(hipGetLastError());
+    });
+}
+
+uint64_t vdb_rank_record_bytes(uint32_t n, uint32_t k) {
+    return ((uint64_t)n * k * 4 + 7) / 8 * 8 + (uint64_t)n * k * 8;
+}
+
+int vdb_merge_ranks_packed_device(const void* d_records, uint32_t nranks, uint32_t n, uint32_t k, float* d_out_dist,
+                                  uint64_t* d_out_ids, void* stream) {
+    return guarded([&] {
+        if (n == 0 || k == 0) return;
+        require(d_records && d_out_dist && d_out_ids && nranks > 0, "null argument");
+        require(k <= (uint32_t)vdbk::kMaxK, "k above 1024 is not supported", VDB_ERR_UNSUPPORTED);
+        const uint64_t rec = vdb_rank_record_bytes(n, k);
+        const float* d = (const float*)d_records;
+        const uint64_t* ids = (const uint64_t*)((const char*)d_records + ((uint64_t)n * k * 4 + 7) / 8 * 8);
+        vdbk::launch_rank_merge(vdbk::topk_regs(k), d, ids, rec / 4, rec / 8, nranks, n, k, d_out_dist, d_out_ids,
                                 (hipStream_t)stream);
         HIPCHECK(hipGetLastError());
     });
@@ -927,6 +960,12 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "wide_stride") {
             require(value >= 0 && value < (1ll << 31), "wide_stride out of range");
             h->wide_stride = (uint32_t)value;
+        } else if (n == "seg_vectors") {
+            require(value == 0 || value == 64 || value == 128 || value == 256 || value == 512,
+                    "seg_vectors is 0 (auto), 64, 128, 256 or 512");
+            h->seg_blocks_opt = (uint32_t)(value / 64);
+            h->set_device();
+            h->upload_directory();
         } else if (n == "batch") {
             require(value > 0 && value < (1ll << 31), "batch out of range");
             h->batch = (uint32_t)value;

@@ -733,9 +733,10 @@ template <int R, int G, int M>
 __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) {
     const int lane = lane_id();
     const uint32_t count = a.count[it.list];
-    const uint64_t b0 = a.block_off[it.list] + (uint64_t)it.seg * kSegBlocks;
-    const uint32_t v0 = it.seg * kSegVectors;
-    const uint32_t nv = min(count - v0, (uint32_t)kSegVectors);
+    const uint32_t seg_vectors = a.seg_blocks * 64;
+    const uint64_t b0 = a.block_off[it.list] + (uint64_t)it.seg * a.seg_blocks;
+    const uint32_t v0 = it.seg * seg_vectors;
+    const uint32_t nv = min(count - v0, seg_vectors);
     const uint32_t nb = (nv + 63) >> 6;
     const uint32_t d4 = a.d4;
     const int k = (int)a.k;
@@ -853,12 +854,13 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
     const int np = (int)it.npairs;
     const int lane = lane_id();
     const uint32_t count = a.count[it.list];
-    const uint32_t nseg = (count + kSegVectors - 1) / kSegVectors;
+    const uint32_t seg_vectors = a.seg_blocks * 64;
+    const uint32_t nseg = (count + seg_vectors - 1) / seg_vectors;
     const uint32_t seg = it.seg * 4 + wave_index();
     if (seg >= nseg) return;  // this wave idles until the block's next item
-    const uint64_t b0 = a.block_off[it.list] + (uint64_t)seg * kSegBlocks;
-    const uint32_t v0 = seg * kSegVectors;
-    const uint32_t nv = min(count - v0, (uint32_t)kSegVectors);
+    const uint64_t b0 = a.block_off[it.list] + (uint64_t)seg * a.seg_blocks;
+    const uint32_t v0 = seg * seg_vectors;
+    const uint32_t nv = min(count - v0, seg_vectors);
     const uint32_t nb = (nv + 63) >> 6;
     const int k = (int)a.k;
 
@@ -1315,9 +1317,12 @@ __global__ void ivf_carry_slots(const uint32_t* __restrict__ probes, const uint3
 
 // Final combine of per-rank partials [nranks][n][k] (list-sharded multi-GPU).
 template <int R>
+// Rank r's partials sit at d + r * d_stride and ids + r * i_stride (elements), each
+// [n][k]: back to back ([nranks][n][k]) or interleaved per rank in one packed record.
 __global__ __launch_bounds__(256) void ivf_merge_ranks(const float* __restrict__ d, const uint64_t* __restrict__ ids,
-                                                    uint32_t nranks, uint32_t n, uint32_t k,
-                                                    float* __restrict__ out_d, uint64_t* __restrict__ out_i) {
+                                                    uint64_t d_stride, uint64_t i_stride, uint32_t nranks,
+                                                    uint32_t n, uint32_t k, float* __restrict__ out_d,
+                                                    uint64_t* __restrict__ out_i) {
     const uint32_t q = blockIdx.x * 4 + wave_index();
     if (q >= n) return;
     WaveTopK<R> tk;
@@ -1325,7 +1330,7 @@ __global__ __launch_bounds__(256) void ivf_merge_ranks(const float* __restrict__
     float kd = __builtin_inff();
     uint64_t ki = kNoId;
     for (uint32_t r = 0; r < nranks; ++r)
-        offer_slot_unique<R>(tk, d + ((size_t)r * n + q) * k, ids + ((size_t)r * n + q) * k, k, kd, ki);
+        offer_slot_unique<R>(tk, d + r * d_stride + (size_t)q * k, ids + r * i_stride + (size_t)q * k, k, kd, ki);
     write_final<R>(tk, k, out_d + (size_t)q * k, out_i + (size_t)q * k);
 }
 
@@ -1747,11 +1752,11 @@ void launch_carry(const uint32_t* probes, const uint32_t* count_global, uint32_t
     ivf_carry_slots<<<P, 64, 0, s>>>(probes, count_global, B, P, k, slot_d, slot_i, carry_d, carry_i);
 }
 
-void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint32_t nranks, uint32_t n, uint32_t k,
-                       float* out_d, uint64_t* out_i, hipStream_t s) {
+void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint64_t d_stride, uint64_t i_stride,
+                       uint32_t nranks, uint32_t n, uint32_t k, float* out_d, uint64_t* out_i, hipStream_t s) {
     const uint32_t g = cdiv(n, 4);
     if (!g) return;
-#define VDB_RM(R) ivf_merge_ranks<R><<<g, 256, 0, s>>>(d, i, nranks, n, k, out_d, out_i)
+#define VDB_RM(R) ivf_merge_ranks<R><<<g, 256, 0, s>>>(d, i, d_stride, i_stride, nranks, n, k, out_d, out_i)
     switch (regs) {
         case 1: VDB_RM(1); break;
         case 2: VDB_RM(2); break;

@@ -14,8 +14,8 @@
 
 namespace vdbk {
 
-constexpr int kSegBlocks = 8;              // 64-vector blocks per scan work item
-constexpr int kSegVectors = kSegBlocks * 64;
+constexpr int kMaxSegBlocks = 8;           // 64-vector blocks per scan segment (the runtime
+                                           // size is 1..8, chosen per shard size by the engine)
 constexpr int kTilePipe = 16;              // float4 tiles of a list vector in flight per lane (scan)
 constexpr int kTilePipeNarrow = 4;         // the same for narrow items (queries held in SGPRs)
 constexpr int kTileAlign = kTilePipe;      // D4 is padded to whole pipeline rounds
@@ -89,6 +89,7 @@ struct ScanArgs {
     uint32_t k;
     uint32_t wide_stride;  // wide-item dispatch stride (prime; 0/1 = plan order)
     uint32_t* work;        // [2] item queues (narrow, wide), reset by the plan kernel
+    uint32_t seg_blocks;   // 64-vector blocks per list segment (one wave's unit of a scan item)
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k);
@@ -105,8 +106,8 @@ void launch_query_merge(int regs, const uint32_t* probes, const uint32_t* count_
 void launch_carry(const uint32_t* probes, const uint32_t* count_global, uint32_t B, uint32_t P, uint32_t k,
                   const float* slot_d, const uint64_t* slot_i, float* carry_d, uint64_t* carry_i,
                   hipStream_t s);
-void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint32_t nranks, uint32_t n, uint32_t k,
-                       float* out_d, uint64_t* out_i, hipStream_t s);
+void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint64_t d_stride, uint64_t i_stride,
+                       uint32_t nranks, uint32_t n, uint32_t k, float* out_d, uint64_t* out_i, hipStream_t s);
 void launch_fill_empty(uint64_t n, float* d, uint64_t* i, hipStream_t s);
 
 // ---- build (train / add / layout) ----

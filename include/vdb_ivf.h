@@ -120,6 +120,13 @@ int vdb_ivf_set_shard(vdb_ivf* index, uint32_t rank, uint32_t world);
 /* Combine per-rank partials gathered as [nranks][n][k] into final [n][k]. */
 int vdb_merge_ranks_device(const float* d_dist, const uint64_t* d_ids, uint32_t nranks, uint32_t n,
                            uint32_t k, float* d_out_dist, uint64_t* d_out_ids, void* stream);
+/* One rank's partials as a single record for ONE collective per batch: f32 dist[n][k],
+ * padded to 8 bytes, then u64 ids[n][k]. vdb_rank_record_bytes gives its size; a
+ * search writes into it with d_distances = record, d_ids = record + that padding. */
+uint64_t vdb_rank_record_bytes(uint32_t n, uint32_t k);
+/* Combine gathered records [nranks][record] into final [n][k]. */
+int vdb_merge_ranks_packed_device(const void* d_records, uint32_t nranks, uint32_t n, uint32_t k,
+                                  float* d_out_dist, uint64_t* d_out_ids, void* stream);
 /* Host-only: the LPT owner of every list for `world` ranks (no GPU needed). */
 int vdb_shard_plan(const uint64_t* list_sizes, uint32_t nlist, uint32_t world, uint32_t* owner);
 
@@ -148,7 +155,8 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
 /* Engine tuning knobs by name (results never change, only speed): "coarse_mode"
  * (0/1, as above), "wide_scan" (0/1: large lists as multi-query workgroup items),
  * "wide_stride" (prime dispatch stride of wide items; 1 = plan order), "batch",
- * "stale_slots" (as vdb_ivf_set_batch / vdb_ivf_set_stale_slots). */
+ * "stale_slots" (as vdb_ivf_set_batch / vdb_ivf_set_stale_slots), "seg_vectors" (0 = auto, or
+ * 64/128/256/512: list vectors per scan segment). */
 int vdb_ivf_set_option(vdb_ivf* index, const char* name, int64_t value);
 
 int vdb_ivf_profile_enable(vdb_ivf* index, int enable);

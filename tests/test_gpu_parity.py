@@ -252,10 +252,22 @@ def test_two_shards_merge_equals_single():
                            torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), Dr, Ir)
+    # the packed-record form bench.py gathers with one collective per batch
+    rec, off = vdb.rank_record_bytes(40, 10), vdb.rank_record_ids_offset(40, 10)
+    recs = np.zeros((2, rec), np.uint8)
+    for r in range(2):
+        recs[r, :parts_d[r].nbytes] = parts_d[r].view(np.uint8).ravel()
+        recs[r, off:off + parts_i[r].nbytes] = parts_i[r].view(np.uint8).ravel()
+    rd = torch.from_numpy(recs.ravel()).to(dev)
+    vdb.merge_ranks_packed_device(rd.data_ptr(), 2, 40, 10, od.data_ptr(), oi.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), Dr, Ir)
 
 
+@pytest.mark.parametrize("seg", [0, 64, 512])
 @pytest.mark.parametrize("k", [10, 64, 65])
-def test_hub_lists_wide_items(k):
+def test_hub_lists_wide_items(k, seg):
     """Skewed lists probed by every query of the batch: wide scan items (groups of
     8 queries), XCD-alignment padding items and two-level partial merges."""
     rng = np.random.default_rng(7)
@@ -270,6 +282,7 @@ def test_hub_lists_wide_items(k):
     assert max(o.list_count(l) for l in range(6)) > 32 * 512, "need > kMergeFan segments in one list"
     g = mirror_from_oracle(o, 48, 6)
     g.add(X, ids)
+    g.set_option("seg_vectors", seg)   # segment size never changes results
     for batch in (64, 130):
         g.set_batch(batch)
         for stride in (40009, 1, 7):   # wide-item dispatch order never changes results
