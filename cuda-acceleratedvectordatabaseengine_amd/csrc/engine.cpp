@@ -141,7 +141,8 @@ struct vdb_ivf {
     int coarse_mode = 1;
     uint32_t wide_stride = 1;  // wide-item dispatch permutation (1 = plan order; measured best)
     uint32_t seg_blocks = vdbk::kMaxSegBlocks;  // current segment size (blocks of 64 vectors)
-    uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
+    uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)
+    uint32_t diag = 0;                          // scan diagnostics (results invalid when set)  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
 
     // Search workspaces: a ring of slots so that searches issued on different streams
     // run concurrently (one batch's small kernels and scan tail overlap the next
@@ -507,7 +508,7 @@ struct vdb_ivf {
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
         const vdbk::ScanArgs sa{arena.p, arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
-                                wide_stride, w.counters.p + 4, seg_blocks};
+                                wide_stride, w.counters.p + 4, seg_blocks, diag};
         if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));
@@ -966,6 +967,8 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->seg_blocks_opt = (uint32_t)(value / 64);
             h->set_device();
             h->upload_directory();
+        } else if (n == "diag") {
+            h->diag = (uint32_t)value;  // timing experiments only: results are invalid when non-zero
         } else if (n == "batch") {
             require(value > 0 && value < (1ll << 31), "batch out of range");
             h->batch = (uint32_t)value;

@@ -907,6 +907,7 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
             const float dist = dist_finish<M>((g & 1) ? acc[g >> 1].y : acc[g >> 1].x);
             if (g < np && __ballot(valid && dist <= kd[g])) pend |= 1u << g;
         }
+        if (a.diag & 1) pend = 0;  // DIAGNOSTIC: no top-k maintenance (results invalid)
         if (pend) {
             const uint64_t vid = valid ? id : kNoId;
             do {
@@ -983,7 +984,7 @@ __global__ __launch_bounds__(256) void ivf_scan_narrow(ScanArgs a) {
 // ivf_scan_wide: the large lists. Workgroup b takes wide item b: 4 consecutive
 // segments (one per wave) x up to 16 of the list's queries, staged once in LDS.
 template <int M>
-__global__ __launch_bounds__(256) void ivf_scan_wide(ScanArgs a) {
+__global__ __launch_bounds__(256, 2) void ivf_scan_wide(ScanArgs a) {
     // Dynamic LDS: [d4][gpv][2] float4 of staged query pairs (tile-major), then per wave
     // kWideGroup x k top-k ids (u64), then the same for distances (f32).
     extern __shared__ __attribute__((aligned(16))) float4 qlds[];
@@ -1009,7 +1010,8 @@ __global__ __launch_bounds__(256) void ivf_scan_wide(ScanArgs a) {
         const ScanItem it = a.items_w[item];
         const int np = (int)it.npairs;
         const int gp = (np + 1) / 2;
-        const int gpv = gp;  // every pair count 1..8 has its own instantiation
+        const int gpv = (a.diag & 2) ? 1 : gp;  // every pair count 1..8 has its own instantiation
+                                                // (DIAGNOSTIC diag&2: one pair only, results invalid)
         for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
             const uint32_t t = e / gpv, p = e - t * gpv;
             const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);

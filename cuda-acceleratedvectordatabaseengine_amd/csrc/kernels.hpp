@@ -90,6 +90,7 @@ struct ScanArgs {
     uint32_t wide_stride;  // wide-item dispatch stride (prime; 0/1 = plan order)
     uint32_t* work;        // [2] item queues (narrow, wide), reset by the plan kernel
     uint32_t seg_blocks;   // 64-vector blocks per list segment (one wave's unit of a scan item)
+    uint32_t diag;         // diagnostics only (0 in production): 1 skip top-k upkeep, 2 one query pair
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k);

@@ -108,8 +108,8 @@ int main(int argc, char** argv) {
         printf("segments T=%2d work=%d wg/cu=%d nt=%d : %.3f ms  %.2f TB/s\n", T, W, WGS, (int)NT, ms,          \
                bytes / ms / 1e9);                                                                              \
     }
-    RUN(16, 0, 2, false) RUN(16, 0, 2, true) RUN(8, 0, 2, true) RUN(16, 0, 4, true) RUN(16, 16, 2, false)
-    RUN(16, 16, 2, true) RUN(16, 24, 2, true) RUN(8, 16, 3, true)
+    RUN(16, 0, 2, true) RUN(16, 24, 2, true) RUN(16, 32, 2, true) RUN(16, 48, 2, true) RUN(8, 48, 2, true)
+    RUN(8, 48, 3, true) RUN(8, 64, 2, true) RUN(8, 96, 2, true)
     CHECK(hipFree(buf));
     return 0;
 }
