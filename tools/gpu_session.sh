@@ -52,7 +52,7 @@ if has dump; then
     run dump 600 python -u tests/debug_dump_index.py 10000000 4096
 fi
 if has prof; then
-    run prof 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu $BARGS
+    run prof 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight 1 $BARGS
     find "$O/prof" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats.csv" \;
     head -14 "$O/kernel_stats.csv"
 fi
