@@ -107,6 +107,7 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_set_stale_slots": (ctypes.c_int, [vp, i32]),
         "vdb_ivf_set_coarse_mode": (ctypes.c_int, [vp, i32]),
         "vdb_ivf_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int64]),
+        "vdb_ivf_coalesce_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "vdb_ivf_profile_enable": (ctypes.c_int, [vp, i32]),
         "vdb_ivf_profile_reset": (ctypes.c_int, [vp]),
         "vdb_ivf_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(Profile)]),
@@ -319,6 +320,12 @@ class IVFFlatIndex:
     def set_option(self, name: str, value: int):
         """Engine tuning knob (vdb_ivf_set_option); never changes results."""
         _check(lib().vdb_ivf_set_option(self._h, name.encode(), int(value)))
+
+    def coalesce_stats(self):
+        """(device batches, search() calls served) of the host-API coalescing queue."""
+        b, r = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(lib().vdb_ivf_coalesce_stats(self._h, ctypes.byref(b), ctypes.byref(r)))
+        return b.value, r.value
 
     def profile_enable(self, on: bool = True):
         _check(lib().vdb_ivf_profile_enable(self._h, int(on)))

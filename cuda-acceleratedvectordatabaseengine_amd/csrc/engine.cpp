@@ -13,6 +13,11 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -111,6 +116,31 @@ struct EventSet {
     hipEvent_t begin, coarse_end, scan_begin, scan_end, end;
 };
 
+// One host-API search() call waiting in the coalescing queue.
+struct PendingSearch {
+    const float* q;
+    uint32_t n, nprobe, k;
+    float* dist;
+    uint64_t* ids;
+    int rc = 1;  // 1 = pending, then a VDB_* code
+    std::string err;
+};
+
+// Request coalescing (the reference's intent: QueryServiceImpl::Config max_batch_size /
+// coalesce_window_ms, query_service.h:25-31, never implemented there): concurrent
+// vdb_ivf_search callers enqueue; one worker thread takes every compatible waiting call
+// (same nprobe and k), up to max_queries, and runs them as ONE device search whose
+// per-call slot semantics are kept exact (request boundaries, kernels' req_start).
+// While the device works on one batch, the next one accumulates.
+struct Coalescer {
+    std::mutex m;
+    std::condition_variable wake, done;
+    std::deque<PendingSearch*> queue;
+    std::thread worker;
+    bool stop = false;
+    uint64_t batches = 0, requests = 0;
+};
+
 }  // namespace
 
 struct vdb_ivf {
@@ -140,7 +170,7 @@ struct vdb_ivf {
     bool wide_scan = true;
     int coarse_mode = 1;
     uint32_t wide_stride = 1;  // wide-item dispatch permutation (1 = plan order; measured best)
-    uint32_t seg_blocks = vdbk::kMaxSegBlocks;  // current segment size (blocks of 64 vectors)
+    uint32_t seg_blocks = 8;  // current segment size (blocks of 64 vectors; upload_directory sets it)
     uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)
     uint32_t diag = 0;                          // scan diagnostics (results invalid when set)  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
 
@@ -165,6 +195,15 @@ struct vdb_ivf {
     uint32_t next_slot = 0;
     DevBuf<float> out_d, qin;  // host-API staging (synchronous calls)
     DevBuf<uint64_t> out_i;
+    DevBuf<uint32_t> d_req;    // coalesced calls: request start per query
+    std::unique_ptr<Coalescer> co;
+    std::mutex co_init_mu;
+    bool coalesce = true;
+    uint32_t coalesce_max_queries = 1024;
+    uint32_t coalesce_window_us = 0;
+    std::vector<float> hq_stage;
+    std::vector<float> hd_stage;
+    std::vector<uint64_t> hi_stage;
     DevBuf<unsigned long long> stats;
 
     bool prof = false;
@@ -172,6 +211,7 @@ struct vdb_ivf {
     size_t events_used = 0;
 
     ~vdb_ivf() {
+        stop_coalescer();
         for (auto& e : events) {
             (void)hipEventDestroy(e.begin);
             (void)hipEventDestroy(e.coarse_end);
@@ -189,6 +229,128 @@ struct vdb_ivf {
     }
 
     void set_device() { HIPCHECK(hipSetDevice(device)); }
+
+    // ---- host-API search: direct, or through the coalescing queue ----
+    void search_host(const float* q, uint32_t n, uint32_t nprobe, uint32_t k, float* dist, uint64_t* ids,
+                     const uint32_t* h_req_start) {
+        set_device();
+        HIPCHECK(hipMemcpyAsync(qin.ensure((size_t)n * dim), q, (size_t)n * dim * 4, hipMemcpyHostToDevice, stream));
+        const uint32_t* dr = nullptr;
+        if (h_req_start) {
+            HIPCHECK(hipMemcpyAsync(d_req.ensure(n), h_req_start, (size_t)n * 4, hipMemcpyHostToDevice, stream));
+            dr = d_req.p;
+        }
+        search_device(qin.p, n, nprobe, k, out_d.ensure((size_t)n * k), out_i.ensure((size_t)n * k), stream, dr);
+        HIPCHECK(hipMemcpyAsync(dist, out_d.p, (size_t)n * k * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipMemcpyAsync(ids, out_i.p, (size_t)n * k * 8, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+    }
+
+    void start_coalescer() {
+        if (co) return;
+        co.reset(new Coalescer());
+        co->worker = std::thread([this] { coalesce_loop(); });
+    }
+
+    void stop_coalescer() {
+        if (!co) return;
+        {
+            std::lock_guard<std::mutex> g(co->m);
+            co->stop = true;
+        }
+        co->wake.notify_all();
+        if (co->worker.joinable()) co->worker.join();
+        co.reset();
+    }
+
+    void coalesce_loop() {
+        Coalescer& c = *co;
+        for (;;) {
+            std::vector<PendingSearch*> run;
+            uint32_t nq = 0;
+            {
+                std::unique_lock<std::mutex> lk(c.m);
+                c.wake.wait(lk, [&] { return c.stop || !c.queue.empty(); });
+                if (c.queue.empty()) return;  // stop requested and nothing left
+                if (coalesce_window_us)
+                    c.wake.wait_for(lk, std::chrono::microseconds(coalesce_window_us), [&] {
+                        uint64_t t = 0;
+                        for (auto* r : c.queue) t += r->n;
+                        return c.stop || t >= coalesce_max_queries;
+                    });
+                const uint32_t P = c.queue.front()->nprobe, K = c.queue.front()->k;
+                for (auto it = c.queue.begin(); it != c.queue.end();) {
+                    PendingSearch* r = *it;
+                    if (r->nprobe == P && r->k == K && (run.empty() || nq + r->n <= coalesce_max_queries)) {
+                        run.push_back(r);
+                        nq += r->n;
+                        it = c.queue.erase(it);
+                    } else {
+                        ++it;
+                    }
+                }
+                c.batches++;
+                c.requests += run.size();
+            }
+            int rc = VDB_OK;
+            std::string err;
+            try {
+                std::lock_guard<std::mutex> g(mu);
+                if (run.size() == 1) {
+                    PendingSearch* r = run[0];
+                    search_host(r->q, r->n, r->nprobe, r->k, r->dist, r->ids, nullptr);
+                } else {
+                    const uint32_t K = run[0]->k;
+                    hq_stage.resize((size_t)nq * dim);
+                    hd_stage.resize((size_t)nq * K);
+                    hi_stage.resize((size_t)nq * K);
+                    std::vector<uint32_t> rs(nq);
+                    uint32_t o = 0;
+                    for (PendingSearch* r : run) {
+                        std::memcpy(hq_stage.data() + (size_t)o * dim, r->q, (size_t)r->n * dim * 4);
+                        for (uint32_t i = 0; i < r->n; ++i) rs[o + i] = o;
+                        o += r->n;
+                    }
+                    search_host(hq_stage.data(), nq, run[0]->nprobe, K, hd_stage.data(), hi_stage.data(), rs.data());
+                    o = 0;
+                    for (PendingSearch* r : run) {
+                        std::memcpy(r->dist, hd_stage.data() + (size_t)o * K, (size_t)r->n * K * 4);
+                        std::memcpy(r->ids, hi_stage.data() + (size_t)o * K, (size_t)r->n * K * 8);
+                        o += r->n;
+                    }
+                }
+            } catch (const VdbError& e) {
+                rc = e.code;
+                err = e.what();
+            } catch (const std::exception& e) {
+                rc = VDB_ERR_DEVICE;
+                err = e.what();
+            }
+            {
+                std::lock_guard<std::mutex> g(c.m);
+                for (PendingSearch* r : run) {
+                    r->err = err;
+                    r->rc = rc;
+                }
+            }
+            c.done.notify_all();
+        }
+    }
+
+    void search_coalesced(const float* q, uint32_t n, uint32_t nprobe, uint32_t k, float* dist, uint64_t* ids) {
+        PendingSearch r{q, n, nprobe, k, dist, ids};
+        {
+            // not `mu`: the worker holds that while the device runs a batch, and callers
+            // must be able to queue meanwhile
+            std::lock_guard<std::mutex> g(co_init_mu);
+            start_coalescer();
+        }
+        std::unique_lock<std::mutex> lk(co->m);
+        co->queue.push_back(&r);
+        co->wake.notify_one();
+        co->done.wait(lk, [&] { return r.rc != 1; });
+        if (r.rc != VDB_OK) throw VdbError(r.rc, r.err);
+    }
 
     // Wait for every search still in flight on any stream before the index changes
     // under it (buffers freed, lists moved, centroids rewritten).
@@ -209,7 +371,7 @@ struct vdb_ivf {
         if (seg_blocks_opt) {
             seg_blocks = seg_blocks_opt;
         } else {
-            seg_blocks = vdbk::kMaxSegBlocks;
+            seg_blocks = 8;  // 512 vectors at most by default (1024 is an explicit option)
             while (seg_blocks > 1 && local / ((uint64_t)seg_blocks * 64) < 4096) seg_blocks >>= 1;
         }
         std::vector<uint32_t> cl(nlist), cg(nlist), ns(nlist);
@@ -480,7 +642,7 @@ struct vdb_ivf {
 
     // ---- search: ivf_flat_index.cpp:205-256, one batch of B queries ----
     void run_batch(SearchSlot& w, const float* d_q, uint32_t B, uint32_t P, uint32_t k, float* out_d_,
-                   uint64_t* out_i_, hipStream_t s) {
+                   uint64_t* out_i_, hipStream_t s, const uint32_t* req_start, uint32_t b0) {
         const int regs_k = vdbk::topk_regs(k);
         const int regs_p = vdbk::topk_regs(P);
         const uint32_t group = (uint32_t)vdbk::scan_group(regs_k);
@@ -526,14 +688,18 @@ struct vdb_ivf {
         vdbk::launch_slot_merge(regs_k, w.probes.p, d_count_global.p, w.nseg_qp.p, w.pbqp.p, w.l1base.p, w.part_d.p, w.part_i.p,
                                 w.l1_d.p, w.l1_i.p, BP, k, w.slot_d.p, w.slot_i.p, s);
         vdbk::launch_query_merge(regs_k, w.probes.p, d_count_global.p, w.slot_d.p, w.slot_i.p, w.carry_d.p, w.carry_i.p, B, P, k,
-                                 stale, out_d_, out_i_, s);
-        if (stale) vdbk::launch_carry(w.probes.p, d_count_global.p, B, P, k, w.slot_d.p, w.slot_i.p, w.carry_d.p, w.carry_i.p, s);
+                                 stale, req_start, b0, out_d_, out_i_, s);
+        if (stale)
+            vdbk::launch_carry(w.probes.p, d_count_global.p, B, P, k, w.slot_d.p, w.slot_i.p, req_start, b0, w.carry_d.p,
+                               w.carry_i.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->end, s));
         HIPCHECK(hipGetLastError());
     }
 
+    // req_start: null (one reference search() call) or, for a coalesced batch of calls,
+    // per query the call-global index of its request's first query (device memory).
     void search_device(const float* d_q, uint32_t n, uint32_t nprobe, uint32_t k, float* d_dist, uint64_t* d_ids,
-                       hipStream_t s) {
+                       hipStream_t s, const uint32_t* req_start = nullptr) {
         if (n == 0 || k == 0) return;
         require(k <= (uint32_t)vdbk::kMaxK, "k above 1024 is not supported", VDB_ERR_UNSUPPORTED);
         const uint32_t P = std::min(nprobe, nlist);  // cpp:218-222 reads out of bounds beyond nlist
@@ -556,7 +722,8 @@ struct vdb_ivf {
         HIPCHECK(hipMemsetAsync(w.carry_i.p, 0xFF, (size_t)P * k * 8, s));
         for (uint32_t b0 = 0; b0 < n; b0 += bmax) {
             const uint32_t B = std::min(bmax, n - b0);
-            run_batch(w, d_q + (size_t)b0 * dim, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s);
+            run_batch(w, d_q + (size_t)b0 * dim, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s, req_start,
+                      b0);
         }
         HIPCHECK(hipEventRecord(w.done, s));
         w.used = true;
@@ -798,16 +965,14 @@ int vdb_ivf_search(vdb_ivf* h, const float* q, uint32_t n, uint32_t nprobe, uint
                    uint64_t* ids) {
     return guarded([&] {
         require(h && ((q && dist && ids) || n == 0 || k == 0), "null argument");
-        std::lock_guard<std::mutex> g(h->mu);
-        h->set_device();
         if (n == 0 || k == 0) return;
-        HIPCHECK(hipMemcpyAsync(h->qin.ensure((size_t)n * h->dim), q, (size_t)n * h->dim * 4, hipMemcpyHostToDevice,
-                                h->stream));
-        h->search_device(h->qin.p, n, nprobe, k, h->out_d.ensure((size_t)n * k), h->out_i.ensure((size_t)n * k),
-                         h->stream);
-        HIPCHECK(hipMemcpyAsync(dist, h->out_d.p, (size_t)n * k * 4, hipMemcpyDeviceToHost, h->stream));
-        HIPCHECK(hipMemcpyAsync(ids, h->out_i.p, (size_t)n * k * 8, hipMemcpyDeviceToHost, h->stream));
-        HIPCHECK(hipStreamSynchronize(h->stream));
+        require(k <= (uint32_t)vdbk::kMaxK, "k above 1024 is not supported", VDB_ERR_UNSUPPORTED);
+        if (h->coalesce) {
+            h->search_coalesced(q, n, nprobe, k, dist, ids);  // concurrent callers share device batches
+        } else {
+            std::lock_guard<std::mutex> g(h->mu);
+            h->search_host(q, n, nprobe, k, dist, ids, nullptr);
+        }
     });
 }
 
@@ -962,11 +1127,19 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             require(value >= 0 && value < (1ll << 31), "wide_stride out of range");
             h->wide_stride = (uint32_t)value;
         } else if (n == "seg_vectors") {
-            require(value == 0 || value == 64 || value == 128 || value == 256 || value == 512,
-                    "seg_vectors is 0 (auto), 64, 128, 256 or 512");
+            require(value == 0 || value == 64 || value == 128 || value == 256 || value == 512 || value == 1024,
+                    "seg_vectors is 0 (auto), 64, 128, 256, 512 or 1024");
             h->seg_blocks_opt = (uint32_t)(value / 64);
             h->set_device();
             h->upload_directory();
+        } else if (n == "coalesce") {
+            h->coalesce = value != 0;
+        } else if (n == "coalesce_max_queries") {
+            require(value > 0 && value < (1ll << 31), "coalesce_max_queries out of range");
+            h->coalesce_max_queries = (uint32_t)value;
+        } else if (n == "coalesce_window_us") {
+            require(value >= 0 && value < 1000000, "coalesce_window_us out of range");
+            h->coalesce_window_us = (uint32_t)value;
         } else if (n == "diag") {
             h->diag = (uint32_t)value;  // timing experiments only: results are invalid when non-zero
         } else if (n == "batch") {
@@ -976,6 +1149,19 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->stale = value ? 1 : 0;
         } else {
             throw VdbError(VDB_ERR_INVALID_ARGUMENT, "unknown option " + n);
+        }
+    });
+}
+
+int vdb_ivf_coalesce_stats(vdb_ivf* h, uint64_t* batches, uint64_t* requests) {
+    return guarded([&] {
+        require(h && batches && requests, "null argument");
+        *batches = 0;
+        *requests = 0;
+        if (h->co) {
+            std::lock_guard<std::mutex> g(h->co->m);
+            *batches = h->co->batches;
+            *requests = h->co->requests;
         }
     });
 }

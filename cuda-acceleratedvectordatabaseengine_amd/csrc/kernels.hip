@@ -1245,10 +1245,17 @@ __global__ __launch_bounds__(256) void ivf_merge_query(const uint32_t* __restric
                                                      const uint64_t* __restrict__ slot_i,
                                                      const float* __restrict__ carry_d,
                                                      const uint64_t* __restrict__ carry_i, uint32_t B, uint32_t P,
-                                                     uint32_t k, int stale, float* __restrict__ out_d,
+                                                     uint32_t k, int stale, const uint32_t* __restrict__ req_start,
+                                                     uint32_t b0, float* __restrict__ out_d,
                                                      uint64_t* __restrict__ out_i) {
     const uint32_t q = blockIdx.x * 4 + wave_index();
     if (q >= B) return;
+    // Coalesced calls: slots live per reference search() call (cpp:210-211), so a
+    // stale-slot lookup never crosses into another request (req_start: first query of
+    // this query's request, call-global; null = one request).
+    const uint32_t qs = req_start ? req_start[b0 + q] : 0u;
+    const uint32_t q_lo = qs > b0 ? qs - b0 : 0u;  // lowest in-batch query of the request
+    const bool carry_ok = qs < b0 || b0 == 0;       // the carry is this request's (or the call's fresh one)
     WaveTopK<R> tk;
     tk.init();
     float kd = __builtin_inff();
@@ -1272,7 +1279,7 @@ __global__ __launch_bounds__(256) void ivf_merge_query(const uint32_t* __restric
         } else if (stale) {
             uint32_t q2 = q;
             bool found = false;
-            while (q2 > 0) {
+            while (q2 > q_lo) {
                 --q2;
                 if (count_global[probes[(size_t)q2 * P + p]] > 0) {
                     found = true;
@@ -1282,10 +1289,10 @@ __global__ __launch_bounds__(256) void ivf_merge_query(const uint32_t* __restric
             if (found) {
                 sd = slot_d + ((size_t)q2 * P + p) * k;
                 si = slot_i + ((size_t)q2 * P + p) * k;
-            } else {
+            } else if (carry_ok) {
                 sd = carry_d + (size_t)p * k;
                 si = carry_i + (size_t)p * k;
-            }
+            }  // else: the request's slot p is still empty
         }
         if (sd) offer_slot_unique<R>(tk, sd, si, k, kd, ki);
     }
@@ -1293,15 +1300,20 @@ __global__ __launch_bounds__(256) void ivf_merge_query(const uint32_t* __restric
 }
 
 // Slot content that survives into the next batch of the same search call.
+// The carry belongs to the request of the batch's last query: only that request's
+// queries are searched; if that request began in this batch and never filled slot p,
+// the carried slot is empty.
 __global__ void ivf_carry_slots(const uint32_t* __restrict__ probes, const uint32_t* __restrict__ count_global,
                         uint32_t B, uint32_t P, uint32_t k, const float* __restrict__ slot_d,
-                        const uint64_t* __restrict__ slot_i, float* __restrict__ carry_d,
-                        uint64_t* __restrict__ carry_i) {
+                        const uint64_t* __restrict__ slot_i, const uint32_t* __restrict__ req_start, uint32_t b0,
+                        float* __restrict__ carry_d, uint64_t* __restrict__ carry_i) {
     __shared__ int s_q;
     const uint32_t p = blockIdx.x;
+    const uint32_t qs = req_start ? req_start[b0 + B - 1] : 0u;
+    const int q_lo = qs > b0 ? (int)(qs - b0) : 0;
     if (threadIdx.x == 0) {
         int found = -1;
-        for (int q = (int)B - 1; q >= 0; --q)
+        for (int q = (int)B - 1; q >= q_lo; --q)
             if (count_global[probes[(size_t)q * P + p]] > 0) {
                 found = q;
                 break;
@@ -1309,7 +1321,11 @@ __global__ void ivf_carry_slots(const uint32_t* __restrict__ probes, const uint3
         s_q = found;
     }
     __syncthreads();
-    if (s_q < 0) return;
+    if (s_q < 0) {
+        if (qs >= b0)  // a request that began in this batch: its slot p is empty
+            for (uint32_t e = threadIdx.x; e < k; e += blockDim.x) carry_i[(size_t)p * k + e] = kNoId;
+        return;
+    }
     const size_t src = ((size_t)s_q * P + p) * k;
     for (uint32_t e = threadIdx.x; e < k; e += blockDim.x) {
         carry_d[(size_t)p * k + e] = slot_d[src + e];
@@ -1734,10 +1750,11 @@ void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_g
 
 void launch_query_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const float* slot_d,
                         const uint64_t* slot_i, const float* carry_d, const uint64_t* carry_i, uint32_t B,
-                        uint32_t P, uint32_t k, int stale, float* out_d, uint64_t* out_i, hipStream_t s) {
+                        uint32_t P, uint32_t k, int stale, const uint32_t* req_start, uint32_t b0, float* out_d,
+                        uint64_t* out_i, hipStream_t s) {
     const uint32_t g = cdiv(B, 4);
     if (!g) return;
-#define VDB_QM(R) ivf_merge_query<R><<<g, 256, 0, s>>>(probes, count_global, slot_d, slot_i, carry_d, carry_i, B, P, k, stale, out_d, out_i)
+#define VDB_QM(R) ivf_merge_query<R><<<g, 256, 0, s>>>(probes, count_global, slot_d, slot_i, carry_d, carry_i, B, P, k, stale, req_start, b0, out_d, out_i)
     switch (regs) {
         case 1: VDB_QM(1); break;
         case 2: VDB_QM(2); break;
@@ -1749,9 +1766,10 @@ void launch_query_merge(int regs, const uint32_t* probes, const uint32_t* count_
 }
 
 void launch_carry(const uint32_t* probes, const uint32_t* count_global, uint32_t B, uint32_t P, uint32_t k,
-                  const float* slot_d, const uint64_t* slot_i, float* carry_d, uint64_t* carry_i, hipStream_t s) {
+                  const float* slot_d, const uint64_t* slot_i, const uint32_t* req_start, uint32_t b0,
+                  float* carry_d, uint64_t* carry_i, hipStream_t s) {
     if (!P || !B) return;
-    ivf_carry_slots<<<P, 64, 0, s>>>(probes, count_global, B, P, k, slot_d, slot_i, carry_d, carry_i);
+    ivf_carry_slots<<<P, 64, 0, s>>>(probes, count_global, B, P, k, slot_d, slot_i, req_start, b0, carry_d, carry_i);
 }
 
 void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint64_t d_stride, uint64_t i_stride,

@@ -14,7 +14,7 @@
 
 namespace vdbk {
 
-constexpr int kMaxSegBlocks = 8;           // 64-vector blocks per scan segment (the runtime
+constexpr int kMaxSegBlocks = 16;          // 64-vector blocks per scan segment (the runtime
                                            // size is 1..8, chosen per shard size by the engine)
 constexpr int kTilePipe = 16;              // float4 tiles of a list vector in flight per lane (scan)
 constexpr int kTilePipeNarrow = 4;         // the same for narrow items (queries held in SGPRs)
@@ -100,13 +100,15 @@ void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_g
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                        const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,
                        uint32_t BP, uint32_t k, float* slot_d, uint64_t* slot_i, hipStream_t s);
+// req_start (device, per call-global query: its request's first query; null = one
+// request) keeps the stale-slot semantics per coalesced request.
 void launch_query_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const float* slot_d,
                         const uint64_t* slot_i, const float* carry_d, const uint64_t* carry_i,
-                        uint32_t B, uint32_t P, uint32_t k, int stale, float* out_d, uint64_t* out_i,
-                        hipStream_t s);
+                        uint32_t B, uint32_t P, uint32_t k, int stale, const uint32_t* req_start, uint32_t b0,
+                        float* out_d, uint64_t* out_i, hipStream_t s);
 void launch_carry(const uint32_t* probes, const uint32_t* count_global, uint32_t B, uint32_t P, uint32_t k,
-                  const float* slot_d, const uint64_t* slot_i, float* carry_d, uint64_t* carry_i,
-                  hipStream_t s);
+                  const float* slot_d, const uint64_t* slot_i, const uint32_t* req_start, uint32_t b0,
+                  float* carry_d, uint64_t* carry_i, hipStream_t s);
 void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint64_t d_stride, uint64_t i_stride,
                        uint32_t nranks, uint32_t n, uint32_t k, float* out_d, uint64_t* out_i, hipStream_t s);
 void launch_fill_empty(uint64_t n, float* d, uint64_t* i, hipStream_t s);

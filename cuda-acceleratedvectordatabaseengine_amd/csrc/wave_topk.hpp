@@ -243,7 +243,13 @@ __device__ __forceinline__ void offer_lanes(WaveTopK<R>& tk, bool want, float cd
             float bd = want ? cd : __builtin_inff();
             uint64_t bi = want ? cid : kNoId;
             bitonic_sort64(bd, bi);
-            bitonic_merge64(tk.d[0], tk.id[0], bd, bi);
+            if (kd == __builtin_inff() && ki == kNoId && rd_lane(tk.id[0], 0) == kNoId) {
+                // empty list (a segment's first block): the sorted batch is the list
+                tk.d[0] = bd;
+                tk.id[0] = bi;
+            } else {
+                bitonic_merge64(tk.d[0], tk.id[0], bd, bi);
+            }
             tk.at(k - 1, kd, ki);
             return;
         }

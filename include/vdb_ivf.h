@@ -104,7 +104,10 @@ int vdb_ivf_add_to_lists(vdb_ivf* index, const float* vectors, const uint64_t* i
 int vdb_ivf_save(vdb_ivf* index, const char* path);
 int vdb_ivf_load(vdb_ivf* index, const char* path);
 
-/* search: host buffers in and out (PCIe included). nprobe is clamped to nlist. */
+/* search: host buffers in and out (PCIe included). nprobe is clamped to nlist.
+ * Thread-safe: concurrent callers are coalesced into shared device batches (calls with
+ * the same nprobe and k), each call keeping exactly the results it would get alone
+ * (option "coalesce" = 0 serialises calls instead). */
 int vdb_ivf_search(vdb_ivf* index, const float* queries, uint32_t n, uint32_t nprobe, uint32_t k,
                    float* distances, uint64_t* ids);
 /* search on device buffers, enqueued on `stream` (NULL = the handle's stream),
@@ -156,8 +159,11 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * (0/1, as above), "wide_scan" (0/1: large lists as multi-query workgroup items),
  * "wide_stride" (prime dispatch stride of wide items; 1 = plan order), "batch",
  * "stale_slots" (as vdb_ivf_set_batch / vdb_ivf_set_stale_slots), "seg_vectors" (0 = auto, or
- * 64/128/256/512: list vectors per scan segment). */
+ * 64/128/256/512/1024: list vectors per scan segment), "coalesce" (0/1), "coalesce_max_queries",
+ * "coalesce_window_us" (0: no waiting; calls arriving while the device is busy batch up). */
 int vdb_ivf_set_option(vdb_ivf* index, const char* name, int64_t value);
+/* Host-API coalescing counters: device batches run and search() calls they served. */
+int vdb_ivf_coalesce_stats(vdb_ivf* index, uint64_t* batches, uint64_t* requests);
 
 int vdb_ivf_profile_enable(vdb_ivf* index, int enable);
 int vdb_ivf_profile_reset(vdb_ivf* index);

@@ -440,3 +440,51 @@ def test_nan_query_is_contained():
         keep = np.arange(len(Q)) > 3          # rows after the NaN row (rows before it are unaffected too)
         Dr, Ir = o.search(Q[keep], 4, 5)
         assert_same(D[keep], I[keep], Dr, Ir)
+
+
+def test_coalesced_concurrent_calls_keep_per_call_semantics():
+    """Concurrent host-API search() calls are coalesced into shared device batches; every
+    call must still get exactly what the reference gives that call alone — including the
+    per-call stale-slot behaviour of empty lists (cpp:210-233), which must not leak
+    between coalesced calls."""
+    import threading
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((3000, 16)).astype(np.float32)
+    ids = np.arange(3000, dtype=np.uint64)
+    C = np.concatenate([X[:10], 6.0 + rng.standard_normal((6, 16)).astype(np.float32) * 0.1])
+    C[10:] *= np.where(rng.random((6, 1)) < 0.5, -1, 1).astype(np.float32)
+    o = oracle.OracleIndex(16, 16, 0)
+    o.centroids = C
+    o.add(X, ids)
+    assert any(o.list_count(l) == 0 for l in range(16))
+    g = mirror_from_oracle(o, 16, 16)
+    g.add(X, ids)
+    g.set_batch(7)                      # internal batches cut across coalesced calls too
+    calls = []
+    for t in range(12):
+        for c in range(6):
+            n = int(rng.integers(1, 20))
+            nprobe, k = (12, 8) if (t + c) % 3 else (5, 3)
+            calls.append((rng.standard_normal((n, 16)).astype(np.float32), nprobe, k))
+    results = [None] * len(calls)
+    errors = []
+
+    def worker(t):
+        try:
+            for j in range(t, len(calls), 12):
+                Q, nprobe, k = calls[j]
+                results[j] = g.search(Q, nprobe=nprobe, k=k)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
+    for (Q, nprobe, k), (D, I) in zip(calls, results):
+        assert_same(D, I, *o.search(Q, nprobe, k))
+    batches, served = g.coalesce_stats()
+    assert served == len(calls)
+    assert batches <= served
