@@ -93,6 +93,8 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_search": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp]),
         "vdb_ivf_search_device": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp, vp]),
         "vdb_ivf_set_shard": (ctypes.c_int, [vp, u32, u32]),
+        "vdb_ivf_save": (ctypes.c_int, [vp, ctypes.c_char_p]),
+        "vdb_ivf_load": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "vdb_merge_ranks_device": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp, vp]),
         "vdb_shard_plan": (ctypes.c_int, [vp, u32, u32, vp]),
         "vdb_rank_record_bytes": (u64, [u32, u32]),
@@ -270,6 +272,16 @@ class IVFFlatIndex:
             D, I = self.search(q, p)
             d[...] = D.reshape(d.shape)
             i[...] = I.reshape(i.shape)
+
+    # ---- persistence (IVFFlatIndex::save/load, ivf_flat_index.h:66-67) ----
+    def save(self, path: str):
+        _check(lib().vdb_ivf_save(self._h, os.fsencode(path)))
+
+    def load(self, path: str):
+        _check(lib().vdb_ivf_load(self._h, os.fsencode(path)))
+
+    def get_dimension(self) -> int:
+        return self.config.dimension
 
     # ---- sharding ----
     def set_shard(self, rank: int, world: int):

@@ -48,6 +48,11 @@ if has multi; then
     grep '^{' "$O/multi.log" > "$O/multi.json"
     cat "$O/multi.json"
 fi
+if has grpc; then
+    run grpc 600 python -u tools/grpc_load.py
+    grep '^{' "$O/grpc.log" > "$O/grpc.json"
+    cat "$O/grpc.json"
+fi
 if has dump; then
     run dump 600 python -u tests/debug_dump_index.py 10000000 4096
 fi
