@@ -172,7 +172,8 @@ struct vdb_ivf {
     uint32_t wide_stride = 1;  // wide-item dispatch permutation (1 = plan order; measured best)
     uint32_t seg_blocks = 8;  // current segment size (blocks of 64 vectors; upload_directory sets it)
     uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)
-    uint32_t diag = 0;                          // scan diagnostics (results invalid when set)  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
+    uint32_t diag = 0;                          // scan diagnostics (results invalid when set)
+    uint32_t narrow_blocks = 64;  // persistent narrow-scan workgroups beside the wide scan (1/8 shard: +1.5 % vs 512)  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
 
     // Search workspaces: a ring of slots so that searches issued on different streams
     // run concurrently (one batch's small kernels and scan tail overlap the next
@@ -675,7 +676,8 @@ struct vdb_ivf {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));
             HIPCHECK(hipStreamWaitEvent(w.side, w.fork, 0));
-            vdbk::launch_scan_narrow(metric, regs_k, (uint32_t)((max_items + 3) / 4), sa, w.side);
+            vdbk::launch_scan_narrow(metric, regs_k, std::min<uint32_t>((uint32_t)((max_items + 3) / 4), narrow_blocks), sa,
+                                     w.side);
             HIPCHECK(hipEventRecord(w.join, w.side));
             vdbk::launch_scan_wide(metric, (uint32_t)max_wide, sa, s);
             HIPCHECK(hipStreamWaitEvent(s, w.join, 0));
@@ -1140,6 +1142,9 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "coalesce_window_us") {
             require(value >= 0 && value < 1000000, "coalesce_window_us out of range");
             h->coalesce_window_us = (uint32_t)value;
+        } else if (n == "narrow_blocks") {
+            require(value > 0 && value <= 4096, "narrow_blocks out of range");
+            h->narrow_blocks = (uint32_t)value;
         } else if (n == "diag") {
             h->diag = (uint32_t)value;  // timing experiments only: results are invalid when non-zero
         } else if (n == "batch") {
