@@ -168,12 +168,12 @@ struct vdb_ivf {
     uint32_t batch = 256;
     int stale = 1;
     bool wide_scan = true;
-    int coarse_mode = 1;
+    int coarse_mode = 1;  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
     uint32_t wide_stride = 1;  // wide-item dispatch permutation (1 = plan order; measured best)
     uint32_t seg_blocks = 8;  // current segment size (blocks of 64 vectors; upload_directory sets it)
     uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)
     uint32_t diag = 0;                          // scan diagnostics (results invalid when set)
-    uint32_t narrow_blocks = 64;  // persistent narrow-scan workgroups beside the wide scan (1/8 shard: +1.5 % vs 512)  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
+    uint32_t narrow_blocks = 64;  // persistent narrow-scan workgroups beside the wide scan (1/8 shard: +1.5 % vs 512)
 
     // Search workspaces: a ring of slots so that searches issued on different streams
     // run concurrently (one batch's small kernels and scan tail overlap the next
