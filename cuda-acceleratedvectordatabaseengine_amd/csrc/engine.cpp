@@ -173,6 +173,7 @@ struct vdb_ivf {
     uint32_t seg_blocks = 8;  // current segment size (blocks of 64 vectors; upload_directory sets it)
     uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)
     uint32_t diag = 0;                          // scan diagnostics (results invalid when set)
+    uint32_t segs_item_opt = 0;   // segments per wide item (0 = 4: one per wave, taken dynamically)
     uint32_t narrow_blocks = 64;  // persistent narrow-scan workgroups beside the wide scan (1/8 shard: +1.5 % vs 512)
 
     // Search workspaces: a ring of slots so that searches issued on different streams
@@ -666,12 +667,13 @@ struct vdb_ivf {
         const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
         const uint64_t max_wide = max_items / 4 + BP + 1;
         const bool wide = regs_k == 1 && wide_scan && vdbk::scan_wide_fits(d4, k);
-        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? 1 : 0, w.items.p, w.items_w.p,
+        const uint32_t segs_item = segs_item_opt ? segs_item_opt : 4u;  // 8+ adds tail latency, no throughput
+        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? 1 : 0, segs_item, w.items.p, w.items_w.p,
                           w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
         const vdbk::ScanArgs sa{arena.p, arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
-                                wide_stride, w.counters.p + 4, seg_blocks, diag};
+                                wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item};
         if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));
@@ -1142,6 +1144,9 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "coalesce_window_us") {
             require(value >= 0 && value < 1000000, "coalesce_window_us out of range");
             h->coalesce_window_us = (uint32_t)value;
+        } else if (n == "segs_per_item") {
+            require(value == 0 || (value >= 4 && value <= 64), "segs_per_item is 0 (auto) or 4..64");
+            h->segs_item_opt = (uint32_t)value;
         } else if (n == "narrow_blocks") {
             require(value > 0 && value <= 4096, "narrow_blocks out of range");
             h->narrow_blocks = (uint32_t)value;

@@ -471,7 +471,7 @@ __device__ uint32_t plan_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
 
 // Query groups of one list with m (query, probe) pairs and ns segments. A list of at
 // least kWideMinSeg segments (with top-k in one register) is scanned by wide items:
-// ceil(m / kWideGroup) balanced groups x ceil(ns / 4) segment quads, so each list is
+// ceil(m / kWideGroup) balanced groups x ceil(ns / segs_item) segment ranges, so each list is
 // read ceil(m / 16) times per batch. Other lists: narrow items of <= gn pairs x ns.
 struct ListGroups {
     uint32_t wide, narrow;
@@ -503,6 +503,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
                                                         const uint32_t* __restrict__ nseg_local,
                                                         const uint32_t* __restrict__ count_local, uint32_t B,
                                                         uint32_t P, uint32_t NP, uint32_t gn, uint32_t wide_on,
+                                                        uint32_t segs_item,
                                                         ScanItem* __restrict__ items_n, ScanItem* __restrict__ items_w,
                                                         uint32_t* __restrict__ counters,
                                                         uint32_t* __restrict__ sorted_pair,
@@ -608,7 +609,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
             const uint32_t ns = nseg_local[list_of(s)];
             const ListGroups g = list_groups(starts[cur + 1] - starts[cur], ns, gn, wide);
             nsum_n += g.narrow * ns;
-            nsum_w += g.wide * ((ns + 3) / 4);
+            nsum_w += g.wide * ((ns + segs_item - 1) / segs_item);
         }
     }
     uint32_t n_narrow, n_wide;
@@ -626,7 +627,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
             base_n[cur] = bn;
             base_w[cur] = bw;
             bn += g.narrow * ns;
-            bw += g.wide * ((ns + 3) / 4);
+            bw += g.wide * ((ns + segs_item - 1) / segs_item);
             atomicAdd(&stats[1], (unsigned long long)count_local[l]);
         }
     }
@@ -848,16 +849,13 @@ __device__ __forceinline__ f2 dist_term2(f2 acc, f2 q, f2 x) {
 // the insertion code exists once, looping over the queries that have candidates.
 template <int GP, int M>
 __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds, float* tk_d,
-                                               uint64_t* tk_i) {
+                                               uint64_t* tk_i, const uint32_t seg) {
     constexpr int G = 2 * GP;
     const uint32_t d4 = a.d4;
     const int np = (int)it.npairs;
     const int lane = lane_id();
     const uint32_t count = a.count[it.list];
     const uint32_t seg_vectors = a.seg_blocks * 64;
-    const uint32_t nseg = (count + seg_vectors - 1) / seg_vectors;
-    const uint32_t seg = it.seg * 4 + wave_index();
-    if (seg >= nseg) return;  // this wave idles until the block's next item
     const uint64_t b0 = a.block_off[it.list] + (uint64_t)seg * a.seg_blocks;
     const uint32_t v0 = seg * seg_vectors;
     const uint32_t nv = min(count - v0, seg_vectors);
@@ -1000,6 +998,7 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_wide(ScanArgs a) {
     uint32_t stride = a.wide_stride;
     if (stride > 1 && n_wide % stride == 0) stride = stride == 40009u ? 40013u : 40009u;
     __shared__ uint32_t s_next;
+    __shared__ uint32_t s_seg;  // next segment of the current item
     for (;;) {
         // persistent workgroups pull items from a queue (one atomic per item)
         if (threadIdx.x == 0) s_next = atomicAdd(&a.work[1], 1u);
@@ -1010,6 +1009,7 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_wide(ScanArgs a) {
         const ScanItem it = a.items_w[item];
         const int np = (int)it.npairs;
         const int gp = (np + 1) / 2;
+        if (threadIdx.x == 0) s_seg = 0;  // visible after the staging barrier below
         const int gpv = (a.diag & 2) ? 1 : gp;  // every pair count 1..8 has its own instantiation
                                                 // (DIAGNOSTIC diag&2: one pair only, results invalid)
         for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
@@ -1021,15 +1021,26 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_wide(ScanArgs a) {
             qlds[(t * gpv + p) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
         }
         __syncthreads();
-        switch (gpv) {
-            case 1: scan_wide_wave<1, M>(a, it, qlds, tk_d, tk_i); break;
-            case 2: scan_wide_wave<2, M>(a, it, qlds, tk_d, tk_i); break;
-            case 3: scan_wide_wave<3, M>(a, it, qlds, tk_d, tk_i); break;
-            case 4: scan_wide_wave<4, M>(a, it, qlds, tk_d, tk_i); break;
-            case 5: scan_wide_wave<5, M>(a, it, qlds, tk_d, tk_i); break;
-            case 6: scan_wide_wave<6, M>(a, it, qlds, tk_d, tk_i); break;
-            case 7: scan_wide_wave<7, M>(a, it, qlds, tk_d, tk_i); break;
-            default: scan_wide_wave<8, M>(a, it, qlds, tk_d, tk_i); break;
+        // the item's segments [seg0, seg1) go to the waves dynamically: a wave that
+        // finishes early takes the next one, so waves idle only at the item's end
+        const uint32_t seg_vectors = a.seg_blocks * 64;
+        const uint32_t nseg = (a.count[it.list] + seg_vectors - 1) / seg_vectors;
+        const uint32_t seg0 = it.seg * a.segs_item, seg1 = min(nseg, seg0 + a.segs_item);
+        for (;;) {
+            uint32_t sg = 0;
+            if (lane_id() == 0) sg = atomicAdd(&s_seg, 1u);
+            sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
+            if (sg >= seg1) break;
+            switch (gpv) {
+                case 1: scan_wide_wave<1, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                case 2: scan_wide_wave<2, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                case 3: scan_wide_wave<3, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                case 4: scan_wide_wave<4, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                case 5: scan_wide_wave<5, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                case 6: scan_wide_wave<6, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                case 7: scan_wide_wave<7, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                default: scan_wide_wave<8, M>(a, it, qlds, tk_d, tk_i, sg); break;
+            }
         }
         __syncthreads();  // qlds is restaged by the next wide item
     }
@@ -1658,12 +1669,13 @@ void launch_select_rerank(int metric, int regs, const float* approx, const float
 }
 
 void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint32_t* count_local, uint32_t B,
-                 uint32_t P, uint32_t group, int wide, ScanItem* items, ScanItem* items_w, uint32_t* counters,
+                 uint32_t P, uint32_t group, int wide, uint32_t segs_item, ScanItem* items, ScanItem* items_w,
+                 uint32_t* counters,
                  uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp, uint32_t* nseg_qp,
                  uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats, hipStream_t s) {
     uint32_t np = 1;
     while (np < B * P) np <<= 1;
-    ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, wide ? 1u : 0u, items,
+    ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, wide ? 1u : 0u, segs_item, items,
                                        items_w, counters, sorted_pair, part_base_sorted, part_base_qp, nseg_qp,
                                        l1base_qp, l1_items, stats);
 }

@@ -62,7 +62,7 @@ void launch_select_rerank(int metric, int regs, const float* approx, const float
 void launch_select(int regs, const float* cd, uint32_t nlist, uint32_t B, uint32_t P, uint32_t* probes,
                    hipStream_t s);
 void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint32_t* count_local,
-                 uint32_t B, uint32_t P, uint32_t group, int wide, ScanItem* items, ScanItem* items_w,
+                 uint32_t B, uint32_t P, uint32_t group, int wide, uint32_t segs_item, ScanItem* items, ScanItem* items_w,
                  uint32_t* counters, uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp,
                  uint32_t* nseg_qp, uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats,
                  hipStream_t s);
@@ -91,6 +91,7 @@ struct ScanArgs {
     uint32_t* work;        // [2] item queues (narrow, wide), reset by the plan kernel
     uint32_t seg_blocks;   // 64-vector blocks per list segment (one wave's unit of a scan item)
     uint32_t diag;         // diagnostics only (0 in production): 1 skip top-k upkeep, 2 one query pair
+    uint32_t segs_item;    // segments per wide item (>= 4; the 4 waves take them dynamically)
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k);

@@ -285,8 +285,9 @@ def test_hub_lists_wide_items(k, seg):
     g.set_option("seg_vectors", seg)   # segment size never changes results
     for batch in (64, 130):
         g.set_batch(batch)
-        for stride in (40009, 1, 7):   # wide-item dispatch order never changes results
+        for stride, spi in ((40009, 0), (1, 4), (7, 12)):   # dispatch order / item size never change results
             g.set_option("wide_stride", stride)
+            g.set_option("segs_per_item", spi)
             assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))
 
 
