@@ -299,7 +299,10 @@ def run(vdb, args, device, rank, world):
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("workload") == f"{args.nvec}x{args.dim}/{args.nlist}/{args.nprobe}/{B}/{k}/N{world}":
+        key = f"{args.nvec}x{args.dim}/{args.nlist}/{args.nprobe}/{B}/{k}/N{world}"
+        if args.emulate_shard > 1:
+            key += f"/shard0of{args.emulate_shard}"
+        if tj.get("workload") == key:
             traffic = tj.get("hbm_bytes_per_scan_launch")
     except (OSError, ValueError):
         pass
