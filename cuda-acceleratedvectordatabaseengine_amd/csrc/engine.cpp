@@ -452,7 +452,29 @@ struct vdb_ivf {
         HIPCHECK(hipGetLastError());
     }
 
+    // assign_to_lists (cpp:259-295): exact argmin with ties to the lowest centroid. For
+    // L2 / IP it is the coarse step's top-1: MFMA distance bounds, then the exact
+    // sequential distances of every centroid that can still be the minimum
+    // (ivf_assign_rerank: candidates whose lower bound <= the smallest upper bound; NaN
+    // orders last, so an all-NaN row goes to list 0 as with the strict '<').
+    // Rows are processed in chunks whose bound matrices fit a fixed workspace.
     void assign(const float* vpad, uint64_t n, uint32_t* out) {
+        if (coarse_mode == 1 && metric != 2 && vdbk::rerank_rows(dp, 1) > 0) {
+            const uint64_t budget = 1024ull << 20;  // bytes of the two bound matrices per chunk
+            uint64_t chunk = std::max<uint64_t>(256, budget / ((uint64_t)nlist * 8) / 16 * 16);
+            chunk = std::min<uint64_t>(chunk, n);
+            DevBuf<float> ap, de;
+            ap.ensure(chunk * nlist);
+            de.ensure(chunk * nlist);
+            for (uint64_t r0 = 0; r0 < n; r0 += chunk) {
+                const uint32_t b = (uint32_t)std::min<uint64_t>(chunk, n - r0);
+                vdbk::launch_coarse_mfma(metric, cent_rm.p, nlist, dp, vpad + r0 * dp, b, ap.p, de.p, stream);
+                vdbk::launch_assign_rerank(metric, ap.p, de.p, cent_rm.p, nlist, dp, vpad + r0 * dp, b, out + r0, stream);
+                HIPCHECK(hipGetLastError());
+            }
+            HIPCHECK(hipStreamSynchronize(stream));  // the chunk buffers are freed on return
+            return;
+        }
         vdbk::launch_assign(metric, vpad, n, dp, cent_il.p, nlist, out, stream);
         HIPCHECK(hipGetLastError());
     }

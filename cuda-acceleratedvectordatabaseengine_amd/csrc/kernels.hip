@@ -431,6 +431,77 @@ __global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict
     }
 }
 
+// assign_to_lists (cpp:259-295) from the MFMA bounds: one wave per row. tau = the
+// smallest upper bound; every centroid whose lower bound is <= tau may be the exact
+// minimum (usually one or two); each such candidate's exact sequential distance is
+// computed by one lane, and the row goes to the smallest (dist, centroid) — the first
+// strict '<' winner of the reference loop. NaN distances order last (an all-NaN row
+// goes to list 0, as the reference's FLT_MAX start does).
+template <int M>
+__global__ __launch_bounds__(256) void ivf_assign_rerank(const float* __restrict__ approx,
+                                                         const float* __restrict__ delta,
+                                                         const float* __restrict__ cent_rm, uint32_t nlist,
+                                                         uint32_t dp, const float* __restrict__ rows, uint32_t n,
+                                                         uint32_t* __restrict__ out) {
+    const uint32_t r = blockIdx.x * 4 + wave_index();
+    if (r >= n) return;
+    const int lane = lane_id();
+    const float* ar = approx + (size_t)r * nlist;
+    const float* dr = delta + (size_t)r * nlist;
+    constexpr int kPre = 8;
+    float lm = __builtin_inff();
+    for (uint32_t c0 = 0; c0 < nlist; c0 += 64 * kPre) {
+        float hv[kPre];
+#pragma unroll
+        for (int j = 0; j < kPre; ++j) {
+            const uint32_t c = c0 + j * 64 + lane;
+            hv[j] = c < nlist ? nan_last(ar[c] + dr[c]) : __builtin_inff();
+        }
+#pragma unroll
+        for (int j = 0; j < kPre; ++j) lm = hv[j] < lm ? hv[j] : lm;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float x = __shfl_xor(lm, o);
+        lm = x < lm ? x : lm;
+    }
+    const float tau = lm;
+    float bd = __builtin_inff();
+    uint32_t bc = 0xFFFFFFFFu;
+    const float4* x4 = (const float4*)(rows + (size_t)r * dp);  // wave-uniform row
+    for (uint32_t c0 = 0; c0 < nlist; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        const bool cand = c < nlist && !(ar[c] - dr[c] > tau);
+        if (__ballot(cand) == 0) continue;
+        if (cand) {
+            const float4* c4 = (const float4*)(cent_rm + (size_t)c * dp);
+            float acc = 0.0f;
+            for (uint32_t t0 = 0; t0 < dp / 4; t0 += 8) {  // dp / 4 is a multiple of 16
+                float4 xv[8], cv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xv[u] = x4[t0 + u], cv[u] = c4[t0 + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc = acc4<M>(acc, xv[u], cv[u]);
+            }
+            const float d = nan_last(dist_finish<M>(acc));
+            if (d < bd || (d == bd && c < bc)) {
+                bd = d;
+                bc = c;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float od = __shfl_xor(bd, o);
+        const uint32_t oc = (uint32_t)__shfl_xor((int)bc, o);
+        if (od < bd || (od == bd && oc < bc)) {
+            bd = od;
+            bc = oc;
+        }
+    }
+    if (lane == 0) out[r] = bc < nlist ? bc : 0u;
+}
+
 // ============================================================================
 // Probe inversion (one workgroup): sort the batch's (query, probe) pairs by list,
 // give every pair its range of partial-result slots, and emit scan work items
@@ -1666,6 +1737,14 @@ void launch_select_rerank(int metric, int regs, const float* approx, const float
         default: VDB_SR(16); break;
     }
 #undef VDB_SR
+}
+
+void launch_assign_rerank(int metric, const float* approx, const float* delta, const float* cent_rm,
+                          uint32_t nlist, uint32_t dp, const float* rows, uint32_t n, uint32_t* out, hipStream_t s) {
+    const uint32_t g = cdiv(n, 4);
+    if (!g) return;
+    if (metric == kL2) ivf_assign_rerank<kL2><<<g, 256, 0, s>>>(approx, delta, cent_rm, nlist, dp, rows, n, out);
+    else ivf_assign_rerank<kIP><<<g, 256, 0, s>>>(approx, delta, cent_rm, nlist, dp, rows, n, out);
 }
 
 void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint32_t* count_local, uint32_t B,

@@ -59,6 +59,9 @@ uint32_t rerank_rows(uint32_t dp, int regs);
 void launch_select_rerank(int metric, int regs, const float* approx, const float* delta, const float* cent_rm,
                           uint32_t nlist, uint32_t dp, const float* qpad, uint32_t B, uint32_t P, uint32_t* cand,
                           uint32_t* probes, hipStream_t s);
+// assign_to_lists from the MFMA bounds: exact argmin (ties to the lowest centroid).
+void launch_assign_rerank(int metric, const float* approx, const float* delta, const float* cent_rm,
+                          uint32_t nlist, uint32_t dp, const float* rows, uint32_t n, uint32_t* out, hipStream_t s);
 void launch_select(int regs, const float* cd, uint32_t nlist, uint32_t B, uint32_t P, uint32_t* probes,
                    hipStream_t s);
 void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint32_t* count_local,
