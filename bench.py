@@ -302,6 +302,8 @@ def run(vdb, args, device, rank, world):
         key = f"{args.nvec}x{args.dim}/{args.nlist}/{args.nprobe}/{B}/{k}/N{world}"
         if args.emulate_shard > 1:
             key += f"/shard0of{args.emulate_shard}"
+        if args.opt:  # knobs can change the traffic (never the results)
+            key += "/" + ",".join(sorted(args.opt))
         if tj.get("workload") == key:
             traffic = tj.get("hbm_bytes_per_scan_launch")
     except (OSError, ValueError):
@@ -347,6 +349,7 @@ def run(vdb, args, device, rank, world):
             "distances_per_batch": int(prof["pair_vectors"] / max(prof["batches"], 1)),
         },
         "build": build_info,
+        **({"list_cache": idx.cache_stats()} if any(o.startswith("list_cache_bytes=") for o in args.opt) else {}),
         "engine_options": dict(o.split("=", 1) for o in args.opt),
         **({"emulated_shard": f"rank 0 of {args.emulate_shard} (partial results; diagnostic, not a bench line)"}
            if args.emulate_shard > 1 else {}),

@@ -47,6 +47,15 @@ class _Config(ctypes.Structure):
                 ("use_gpu", ctypes.c_int32), ("max_gpu_memory", ctypes.c_uint64), ("device", ctypes.c_int32)]
 
 
+class CacheStats(ctypes.Structure):
+    _fields_ = [("capacity_bytes", ctypes.c_uint64), ("resident_bytes", ctypes.c_uint64),
+                ("resident_lists", ctypes.c_uint64), ("loads", ctypes.c_uint64), ("evictions", ctypes.c_uint64),
+                ("bytes_loaded", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
 class Profile(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("scan_launches", ctypes.c_uint64), ("scan_ms", ctypes.c_double),
                 ("coarse_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("scan_vectors", ctypes.c_uint64),
@@ -110,6 +119,7 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_set_coarse_mode": (ctypes.c_int, [vp, i32]),
         "vdb_ivf_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int64]),
         "vdb_ivf_coalesce_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+        "vdb_ivf_cache_stats": (ctypes.c_int, [vp, ctypes.POINTER(CacheStats)]),
         "vdb_ivf_profile_enable": (ctypes.c_int, [vp, i32]),
         "vdb_ivf_profile_reset": (ctypes.c_int, [vp]),
         "vdb_ivf_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(Profile)]),
@@ -338,6 +348,12 @@ class IVFFlatIndex:
         b, r = ctypes.c_uint64(0), ctypes.c_uint64(0)
         _check(lib().vdb_ivf_coalesce_stats(self._h, ctypes.byref(b), ctypes.byref(r)))
         return b.value, r.value
+
+    def cache_stats(self) -> dict:
+        """List-cache tier counters (option list_cache_bytes; capacity 0 = tier off)."""
+        st = CacheStats()
+        _check(lib().vdb_ivf_cache_stats(self._h, ctypes.byref(st)))
+        return st.as_dict()
 
     def profile_enable(self, on: bool = True):
         _check(lib().vdb_ivf_profile_enable(self._h, int(on)))

@@ -16,6 +16,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <map>
 #include <memory>
 #include <thread>
 #include <cstdio>
@@ -75,12 +76,13 @@ template <class T>
 struct DevBuf {
     T* p = nullptr;
     size_t cap = 0;
+    bool host = false;  // page-locked host memory the device reads and writes directly
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() { release(); }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) (void)(host ? hipHostFree(p) : hipFree(p));
         p = nullptr;
         cap = 0;
     }
@@ -88,13 +90,17 @@ struct DevBuf {
         if (n <= cap && p) return p;
         release();
         size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-        HIPCHECK(hipMalloc(&p, bytes));
+        if (host)
+            HIPCHECK(hipHostMalloc((void**)&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
+        else
+            HIPCHECK(hipMalloc(&p, bytes));
         cap = std::max<size_t>(n, 1);
         return p;
     }
     void swap(DevBuf& o) {
         std::swap(p, o.p);
         std::swap(cap, o.cap);
+        std::swap(host, o.host);
     }
 };
 
@@ -175,6 +181,25 @@ struct vdb_ivf {
     uint32_t diag = 0;                          // scan diagnostics (results invalid when set)
     uint32_t segs_item_opt = 0;   // segments per wide item (0 = 4: one per wave, taken dynamically)
     uint32_t narrow_blocks = 64;  // persistent narrow-scan workgroups beside the wide scan (1/8 shard: +1.5 % vs 512)
+
+    // List-cache tier (option list_cache_bytes > 0), the reference's residency model
+    // (load_list_to_gpu on first touch under a byte cap, evict_list_from_gpu,
+    // ivf_flat_index.cpp:387-471) for indexes larger than HBM: the arena then lives in
+    // page-locked host memory and HBM holds a cache of whole lists. Before a batch is
+    // planned, every list it probes is made resident (DMA of its blocks), evicting the
+    // least recently used lists the batch does not probe; the scan reads the cache
+    // through the same directory (d_block_off), so the kernels are unchanged.
+    static constexpr uint64_t kAbsent = ~0ull;
+    uint64_t cache_blocks = 0;  // capacity in 64-vector blocks (0: tier off, the arena is in HBM)
+    DevBuf<float4> cache;
+    DevBuf<uint64_t> cache_ids;
+    std::vector<uint64_t> cache_off;        // per list: cache block offset or kAbsent
+    std::vector<uint64_t> last_use;         // per list: batch tick of the last probe
+    std::map<uint64_t, uint64_t> free_ext;  // free cache extents: block offset -> blocks
+    uint64_t use_tick = 0, cache_used = 0;
+    uint64_t cache_loads = 0, cache_evictions = 0, cache_bytes_in = 0;
+    DevBuf<uint32_t> probe_stage;  // pinned: the batch's probes, read by the host
+    DevBuf<uint64_t> dir_stage;    // pinned: directory upload source
 
     // Search workspaces: a ring of slots so that searches issued on different streams
     // run concurrently (one batch's small kernels and scan tail overlap the next
@@ -383,7 +408,7 @@ struct vdb_ivf {
             cl[l] = owned[l] ? (uint32_t)count[l] : 0u;
             ns[l] = (uint32_t)cdiv(cl[l], (uint64_t)seg_blocks * 64);
         }
-        HIPCHECK(hipMemcpyAsync(d_block_off.ensure(nlist), block_off.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+        upload_scan_directory(stream);
         HIPCHECK(hipMemcpyAsync(d_count_local.ensure(nlist), cl.data(), nlist * 4, hipMemcpyHostToDevice, stream));
         HIPCHECK(hipMemcpyAsync(d_count_global.ensure(nlist), cg.data(), nlist * 4, hipMemcpyHostToDevice, stream));
         HIPCHECK(hipMemcpyAsync(d_nseg.ensure(nlist), ns.data(), nlist * 4, hipMemcpyHostToDevice, stream));
@@ -397,6 +422,9 @@ struct vdb_ivf {
     // Rebuild the arena so list l holds `keep[l]` of its current blocks at new
     // offsets sized for `new_count[l]` vectors (0 for lists this handle drops).
     void relayout(const std::vector<uint64_t>& new_count, const std::vector<uint8_t>& new_owned) {
+        relayout(new_count, new_owned, arena.host);
+    }
+    void relayout(const std::vector<uint64_t>& new_count, const std::vector<uint8_t>& new_owned, bool host_arena) {
         quiesce();
         std::vector<uint64_t> new_off(nlist, 0), old_off(nlist, 0);
         std::vector<uint32_t> nblocks(nlist, 0);
@@ -411,6 +439,7 @@ struct vdb_ivf {
         }
         DevBuf<float4> na;
         DevBuf<uint64_t> ni;
+        na.host = ni.host = host_arena;
         // one slack block past the last list: the scan prefetches one chunk and one
         // block of ids beyond the segment it streams
         const size_t vec4 = (size_t)(blocks + 1) * d4 * 64;
@@ -436,6 +465,139 @@ struct vdb_ivf {
         arena_blocks = blocks;
         block_off = new_off;
         owned = new_owned;
+        cache_reset();  // list contents or offsets changed: nothing cached stays valid
+    }
+
+    // ---- list-cache tier ----
+    bool tiered() const { return cache_blocks > 0; }
+    uint64_t list_blocks(uint32_t l) const { return cdiv(count[l], 64); }
+    static uint64_t block_bytes(uint32_t dp_) { return 64ull * ((uint64_t)dp_ * 4 + 8); }
+
+    void cache_reset() {
+        cache_off.assign(nlist, kAbsent);
+        last_use.assign(nlist, 0);
+        free_ext.clear();
+        if (cache_blocks) free_ext[0] = cache_blocks;
+        cache_used = 0;
+    }
+
+    uint64_t cache_alloc(uint64_t nb) {  // first fit
+        for (auto it = free_ext.begin(); it != free_ext.end(); ++it) {
+            if (it->second < nb) continue;
+            const uint64_t off = it->first, len = it->second;
+            free_ext.erase(it);
+            if (len > nb) free_ext[off + nb] = len - nb;
+            cache_used += nb;
+            return off;
+        }
+        return kAbsent;
+    }
+
+    void cache_free(uint32_t l) {
+        const uint64_t nb = list_blocks(l);
+        auto it = free_ext.emplace(cache_off[l], nb).first;
+        cache_off[l] = kAbsent;
+        cache_used -= nb;
+        auto nx = std::next(it);
+        if (nx != free_ext.end() && it->first + it->second == nx->first) {
+            it->second += nx->second;
+            free_ext.erase(nx);
+        }
+        if (it != free_ext.begin()) {
+            auto pv = std::prev(it);
+            if (pv->first + pv->second == it->first) {
+                pv->second += it->second;
+                free_ext.erase(it);
+            }
+        }
+    }
+
+    // Scan directory: home offsets, or cache offsets in the tier (absent lists: 0,
+    // never read: a list is made resident before any batch that probes it is planned).
+    void upload_scan_directory(hipStream_t s) {
+        const uint64_t* src = block_off.data();
+        if (tiered()) {
+            uint64_t* st = dir_stage.ensure(nlist);
+            for (uint32_t l = 0; l < nlist; ++l) st[l] = cache_off[l] == kAbsent ? 0 : cache_off[l];
+            src = st;
+        }
+        HIPCHECK(hipMemcpyAsync(d_block_off.ensure(nlist), src, nlist * 8, hipMemcpyHostToDevice, s));
+        if (!tiered()) HIPCHECK(hipStreamSynchronize(s));  // src is the host vector
+    }
+
+    // Make `lists` resident (ids may repeat; lists not stored here or empty are
+    // skipped). False if together they exceed the cache. Copies are ordered on s.
+    bool make_resident(const uint32_t* lists, size_t n, hipStream_t s) {
+        ++use_tick;
+        std::vector<uint8_t> in_set(nlist, 0);
+        std::vector<uint32_t> want, miss;
+        uint64_t need = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const uint32_t l = lists[i];
+            if (l >= nlist || in_set[l] || !owned[l] || count[l] == 0) continue;
+            in_set[l] = 1;
+            want.push_back(l);
+            need += list_blocks(l);
+            last_use[l] = use_tick;
+            if (cache_off[l] == kAbsent) miss.push_back(l);
+        }
+        if (need > cache_blocks) return false;
+        if (miss.empty()) return true;
+        quiesce();  // searches on other streams may still read the lists evicted below
+        auto by_size = [&](uint32_t a, uint32_t b) { return count[a] != count[b] ? count[a] > count[b] : a < b; };
+        std::vector<uint32_t> victims;
+        for (uint32_t l = 0; l < nlist; ++l)
+            if (cache_off[l] != kAbsent && !in_set[l]) victims.push_back(l);
+        std::sort(victims.begin(), victims.end(),
+                  [&](uint32_t a, uint32_t b) { return last_use[a] != last_use[b] ? last_use[a] < last_use[b] : a < b; });
+        std::sort(miss.begin(), miss.end(), by_size);
+        size_t vi = 0;
+        for (size_t m = 0; m < miss.size(); ++m) {
+            const uint32_t l = miss[m];
+            uint64_t off;
+            while ((off = cache_alloc(list_blocks(l))) == kAbsent && vi < victims.size()) {
+                cache_free(victims[vi++]);
+                ++cache_evictions;
+            }
+            if (off == kAbsent) {
+                // fragmented: keep only this batch's lists, packed from offset 0 (they fit)
+                for (uint32_t v = 0; v < nlist; ++v)
+                    if (cache_off[v] != kAbsent) cache_free(v);
+                miss = want;
+                std::sort(miss.begin(), miss.end(), by_size);
+                m = (size_t)-1;
+                continue;
+            }
+            cache_off[l] = off;
+            const uint64_t nb = list_blocks(l);
+            HIPCHECK(hipMemcpyAsync(cache.p + off * d4 * 64, arena.p + block_off[l] * d4 * 64, nb * d4 * 64 * sizeof(float4),
+                                    hipMemcpyHostToDevice, s));
+            HIPCHECK(hipMemcpyAsync(cache_ids.p + off * 64, arena_ids.p + block_off[l] * 64, nb * 64 * 8,
+                                    hipMemcpyHostToDevice, s));
+            ++cache_loads;
+            cache_bytes_in += nb * block_bytes(dp);
+        }
+        upload_scan_directory(s);
+        return true;
+    }
+
+    // Turn the tier on (bytes > 0: HBM cache of that many bytes, arena moved to host
+    // memory) or off (arena back in HBM).
+    void set_list_cache(uint64_t bytes) {
+        quiesce();
+        const uint64_t nb = bytes / block_bytes(dp);
+        require(bytes == 0 || nb > 0, "list_cache_bytes is below one block of 64 vectors");
+        cache.release();
+        cache_ids.release();
+        cache_blocks = 0;
+        if ((nb > 0) != arena.host) relayout(count, owned, nb > 0);  // moves the arena
+        cache_blocks = nb;
+        if (nb) {  // one slack block: the scan prefetches past a segment's end
+            cache.ensure((nb + 1) * d4 * 64);
+            cache_ids.ensure((nb + 1) * 64);
+        }
+        cache_reset();
+        upload_directory();
     }
 
     // Row-major [n][dim] device input -> zero-padded [n][dp] (or the input itself).
@@ -665,7 +827,9 @@ struct vdb_ivf {
     }
 
     // ---- search: ivf_flat_index.cpp:205-256, one batch of B queries ----
-    void run_batch(SearchSlot& w, const float* d_q, uint32_t B, uint32_t P, uint32_t k, float* out_d_,
+    // Returns false (nothing merged, caller retries with fewer queries) when the tier's
+    // cache cannot hold every list the batch probes.
+    bool run_batch(SearchSlot& w, const float* d_q, uint32_t B, uint32_t P, uint32_t k, float* out_d_,
                    uint64_t* out_i_, hipStream_t s, const uint32_t* req_start, uint32_t b0) {
         const int regs_k = vdbk::topk_regs(k);
         const int regs_p = vdbk::topk_regs(P);
@@ -686,6 +850,14 @@ struct vdb_ivf {
             vdbk::launch_select(regs_p, w.cd.p, nlist, B, P, w.probes.p, s);
         }
         if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
+        if (tiered()) {
+            HIPCHECK(hipMemcpyAsync(probe_stage.ensure(BP), w.probes.p, (size_t)BP * 4, hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            if (!make_resident(probe_stage.p, BP, s)) {
+                if (ev) --events_used;
+                return false;
+            }
+        }
         const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
         const uint64_t max_wide = max_items / 4 + BP + 1;
         const bool wide = regs_k == 1 && wide_scan && vdbk::scan_wide_fits(d4, k);
@@ -693,7 +865,7 @@ struct vdb_ivf {
         vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? 1 : 0, segs_item, w.items.p, w.items_w.p,
                           w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
-        const vdbk::ScanArgs sa{arena.p, arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
+        const vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
                                 wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item};
         if (wide) {
@@ -720,6 +892,7 @@ struct vdb_ivf {
                                w.carry_i.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->end, s));
         HIPCHECK(hipGetLastError());
+        return true;
     }
 
     // req_start: null (one reference search() call) or, for a coalesced batch of calls,
@@ -746,10 +919,13 @@ struct vdb_ivf {
         if (w.used) HIPCHECK(hipStreamWaitEvent(s, w.done, 0));
         // Probe-slot contents live for one search call (cpp:210-211).
         HIPCHECK(hipMemsetAsync(w.carry_i.p, 0xFF, (size_t)P * k * 8, s));
-        for (uint32_t b0 = 0; b0 < n; b0 += bmax) {
-            const uint32_t B = std::min(bmax, n - b0);
-            run_batch(w, d_q + (size_t)b0 * dim, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s, req_start,
-                      b0);
+        for (uint32_t b0 = 0, B = std::min(bmax, n); b0 < n; b0 += B, B = std::min(B, n - b0)) {
+            // (list-cache tier: a batch whose probed lists overflow the cache is halved)
+            while (!run_batch(w, d_q + (size_t)b0 * dim, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s,
+                              req_start, b0)) {
+                require(B > 1, "list_cache_bytes cannot hold the lists one query probes", VDB_ERR_OUT_OF_MEMORY);
+                B = (B + 1) / 2;
+            }
         }
         HIPCHECK(hipEventRecord(w.done, s));
         w.used = true;
@@ -1076,21 +1252,35 @@ int vdb_ivf_warmup(vdb_ivf* h, const uint32_t* lists, uint32_t n) {
     return guarded([&] {
         require(h && (lists || n == 0), "null argument");
         for (uint32_t i = 0; i < n; ++i) require(lists[i] < h->nlist, "list id out of range");
-        // Every list is already HBM-resident (the reference loads on first touch,
-        // ivf_flat_index.cpp:387-444); nothing to move.
+        // Without the list-cache tier every list is already HBM-resident. In the tier,
+        // each list is loaded like load_list_to_gpu (ivf_flat_index.cpp:387-444): one
+        // that cannot fit the cache is skipped (the reference returns false).
+        std::lock_guard<std::mutex> g(h->mu);
+        if (!h->tiered()) return;
+        h->set_device();
+        for (uint32_t i = 0; i < n; ++i) (void)h->make_resident(lists + i, 1, h->stream);
+        HIPCHECK(hipStreamSynchronize(h->stream));
     });
 }
 
 int vdb_ivf_evict(vdb_ivf* h, uint32_t list) {
     return guarded([&] {
         require(h && list < h->nlist, "list id out of range");
-        // Residency is permanent; eviction is accepted as a no-op.
+        // Without the tier residency is permanent and eviction is a no-op; in the tier
+        // the list leaves the cache (evict_list_from_gpu, ivf_flat_index.cpp:447-471).
+        std::lock_guard<std::mutex> g(h->mu);
+        if (!h->tiered() || h->cache_off[list] == vdb_ivf::kAbsent) return;
+        h->set_device();
+        h->quiesce();
+        h->cache_free(list);
     });
 }
 
 uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* h) {
     if (!h) return 0;
-    return h->arena_blocks * 64 * ((uint64_t)h->dp * 4 + 8) + (uint64_t)h->nlist * h->dp * 8;
+    const uint64_t cent = (uint64_t)h->nlist * h->dp * 8;
+    if (h->tiered()) return h->cache_used * vdb_ivf::block_bytes(h->dp) + cent;  // resident lists
+    return h->arena_blocks * vdb_ivf::block_bytes(h->dp) + cent;
 }
 
 uint64_t vdb_ivf_ntotal(const vdb_ivf* h) { return h ? h->total : 0; }
@@ -1172,6 +1362,10 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "narrow_blocks") {
             require(value > 0 && value <= 4096, "narrow_blocks out of range");
             h->narrow_blocks = (uint32_t)value;
+        } else if (n == "list_cache_bytes") {
+            require(value >= 0, "list_cache_bytes out of range");
+            h->set_device();
+            h->set_list_cache((uint64_t)value);
         } else if (n == "diag") {
             h->diag = (uint32_t)value;  // timing experiments only: results are invalid when non-zero
         } else if (n == "batch") {
@@ -1182,6 +1376,21 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else {
             throw VdbError(VDB_ERR_INVALID_ARGUMENT, "unknown option " + n);
         }
+    });
+}
+
+int vdb_ivf_cache_stats(vdb_ivf* h, vdb_ivf_cache_stats_t* out) {
+    return guarded([&] {
+        require(h && out, "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        out->capacity_bytes = h->cache_blocks * vdb_ivf::block_bytes(h->dp);
+        out->resident_bytes = h->cache_used * vdb_ivf::block_bytes(h->dp);
+        out->loads = h->cache_loads;
+        out->evictions = h->cache_evictions;
+        out->bytes_loaded = h->cache_bytes_in;
+        uint64_t n = 0;
+        for (uint32_t l = 0; l < h->nlist && h->tiered(); ++l) n += h->cache_off[l] != vdb_ivf::kAbsent;
+        out->resident_lists = n;
     });
 }
 

@@ -59,7 +59,8 @@ typedef struct vdb_ivf_config {
     uint32_t nlist;
     int32_t metric;
     int32_t use_gpu;          /* accepted for API parity; the engine always runs on the GPU */
-    uint64_t max_gpu_memory;  /* 0 = no cap. The whole index stays HBM-resident (288 GB/GPU). */
+    uint64_t max_gpu_memory;  /* accepted, not a cap: the whole index stays HBM-resident (288 GB/GPU); the
+                                 reference-style capped residency is the "list_cache_bytes" option */
     int32_t device;           /* HIP device ordinal */
 } vdb_ivf_config;
 
@@ -133,9 +134,25 @@ int vdb_merge_ranks_packed_device(const void* d_records, uint32_t nranks, uint32
 /* Host-only: the LPT owner of every list for `world` ranks (no GPU needed). */
 int vdb_shard_plan(const uint64_t* list_sizes, uint32_t nlist, uint32_t world, uint32_t* owner);
 
-/* List residency (the whole index is HBM-resident; these keep the API). */
+/* List residency. By default the whole index is HBM-resident (288 GB per GPU) and
+ * these keep the API. With the list-cache tier (option "list_cache_bytes" > 0) the
+ * lists live in page-locked host memory and HBM caches whole lists under that byte
+ * cap, like the reference's load_list_to_gpu / evict_list_from_gpu
+ * (engine/ivf_flat_index.cpp:387-471, ivf_flat_index.h:60-61): warmup loads lists
+ * (one that cannot fit is skipped), evict drops one, and a search loads the lists
+ * each batch probes first (least recently used lists make room). Results are the
+ * same in both modes. */
 int vdb_ivf_warmup(vdb_ivf* index, const uint32_t* lists, uint32_t n);
 int vdb_ivf_evict(vdb_ivf* index, uint32_t list);
+typedef struct vdb_ivf_cache_stats_t {
+    uint64_t capacity_bytes;  /* 0: tier off */
+    uint64_t resident_bytes;
+    uint64_t resident_lists;
+    uint64_t loads;           /* lists copied host -> HBM */
+    uint64_t evictions;       /* lists evicted to make room (not counting vdb_ivf_evict) */
+    uint64_t bytes_loaded;
+} vdb_ivf_cache_stats_t;
+int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
 
 uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* index);
 uint64_t vdb_ivf_ntotal(const vdb_ivf* index);
@@ -160,7 +177,10 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * "wide_stride" (prime dispatch stride of wide items; 1 = plan order), "batch",
  * "stale_slots" (as vdb_ivf_set_batch / vdb_ivf_set_stale_slots), "seg_vectors" (0 = auto, or
  * 64/128/256/512/1024: list vectors per scan segment), "coalesce" (0/1), "coalesce_max_queries",
- * "coalesce_window_us" (0: no waiting; calls arriving while the device is busy batch up). */
+ * "coalesce_window_us" (0: no waiting; calls arriving while the device is busy batch up),
+ * "list_cache_bytes" (0 = every list HBM-resident; > 0 = the list-cache tier above with an
+ * HBM cache of that many bytes; a search whose single query probes more fails with
+ * VDB_ERR_OUT_OF_MEMORY, a batch probing more is split). */
 int vdb_ivf_set_option(vdb_ivf* index, const char* name, int64_t value);
 /* Host-API coalescing counters: device batches run and search() calls they served. */
 int vdb_ivf_coalesce_stats(vdb_ivf* index, uint64_t* batches, uint64_t* requests);

@@ -1,0 +1,121 @@
+"""GPU: the list-cache tier (option list_cache_bytes), the reference's residency model
+(load_list_to_gpu on first touch under a byte cap, evict_list_from_gpu, warmup_lists,
+get_gpu_memory_usage: ivf_flat_index.cpp:387-471, 690-709). Lists live in page-locked
+host memory and HBM caches whole lists; results must stay bit-identical to the oracle
+whatever the cache holds: with evictions, batches split because their probed lists
+overflow the cache, fragmented caches repacked, empty lists (stale slots), the tier
+switched on before or after add, and switched off again."""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import load_vdb
+from test_gpu_parity import assert_same, bits
+
+vdb = load_vdb()
+pytestmark = pytest.mark.gpu
+
+D, NLIST, NPROBE, K = 64, 64, 8, 10
+BLOCK_BYTES = 64 * (D * 4 + 8)  # one 64-vector block of the arena (dp = 64 here)
+
+
+def fixture():
+    X, Q, ids = oracle.reference_test_data(20000, 300, D, seed=5)
+    o = oracle.OracleIndex(D, NLIST, 0)
+    o.train(X[:5000])
+    o.add(X, ids)
+    blocks = np.array([(o.list_count(l) + 63) // 64 for l in range(NLIST)])
+    need = max(int(blocks[o.select_nprobe(q, NPROBE)].sum()) for q in Q)  # one query's probed lists
+    return X, Q, ids, o, blocks, need
+
+
+def make(o, X, ids, cache_bytes, before_add):
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST))
+    g.centroids = o.centroids
+    if before_add:
+        g.set_option("list_cache_bytes", cache_bytes)
+        g.add(X, ids)
+    else:
+        g.add(X, ids)
+        g.set_option("list_cache_bytes", cache_bytes)
+    return g
+
+
+@pytest.mark.parametrize("before_add", [True, False])
+def test_cache_tier_matches_oracle_under_eviction(before_add):
+    X, Q, ids, o, blocks, need = fixture()
+    cap = (need + 8) * BLOCK_BYTES          # barely more than one query's lists
+    g = make(o, X, ids, cap, before_add)
+    Dr, Ir = o.search(Q, NPROBE, K)
+    for batch in (256, 16, 1):              # 256 and 16 overflow the cache and are split
+        g.set_batch(batch)
+        assert_same(*g.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
+    st = g.cache_stats()
+    assert st["capacity_bytes"] == (cap // BLOCK_BYTES) * BLOCK_BYTES
+    assert st["loads"] > NLIST and st["evictions"] > 0
+    assert 0 < st["resident_bytes"] <= st["capacity_bytes"]
+    assert g.get_gpu_memory_usage() == st["resident_bytes"] + NLIST * D * 8
+    for l in (0, 17, NLIST - 1):            # host-resident arena still exports lists
+        assert np.array_equal(g.get_list(l)[1], o.get_list(l)[1])
+
+
+def test_cache_tier_large_cache_hits_and_off_again():
+    X, Q, ids, o, blocks, need = fixture()
+    g = make(o, X, ids, int(blocks.sum() + 1) * BLOCK_BYTES, True)   # everything fits
+    Dr, Ir = o.search(Q, NPROBE, K)
+    assert_same(*g.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
+    loads = g.cache_stats()["loads"]
+    assert loads <= NLIST
+    assert_same(*g.search(Q, nprobe=NPROBE, k=K), Dr, Ir)  # second pass: all hits
+    st = g.cache_stats()
+    assert st["loads"] == loads and st["evictions"] == 0
+    g.set_option("list_cache_bytes", 0)                      # arena back in HBM
+    assert g.cache_stats()["capacity_bytes"] == 0
+    assert_same(*g.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
+
+
+def test_warmup_evict_and_too_small_cache():
+    X, Q, ids, o, blocks, need = fixture()
+    big = int(np.argmax(blocks))
+    cap = (int(blocks.max()) + 2) * BLOCK_BYTES
+    g = make(o, X, ids, cap, True)
+    g.warmup_lists([big])
+    st = g.cache_stats()
+    assert st["resident_lists"] == 1 and st["resident_bytes"] == int(blocks[big]) * BLOCK_BYTES
+    small = [l for l in np.argsort(blocks)[:3].tolist() if blocks[l] > 0]
+    g.warmup_lists(small)                   # LRU: the big list makes room when needed
+    st = g.cache_stats()
+    assert st["resident_lists"] >= len(small)
+    g.evict_list(small[0])
+    assert g.cache_stats()["resident_lists"] == st["resident_lists"] - 1
+    g.evict_list(small[0])                  # evicting a non-resident list is a no-op
+    if need > cap // BLOCK_BYTES:
+        with pytest.raises(vdb.VdbError, match="list_cache_bytes"):
+            g.search(Q, nprobe=NPROBE, k=K)
+    with pytest.raises(vdb.VdbError):
+        g.set_option("list_cache_bytes", BLOCK_BYTES - 1)   # below one block
+
+
+def test_cache_tier_empty_lists_stale_slots():
+    """Quirk A1 (empty probed lists keep the previous query's slot) across split batches."""
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((3000, 16)).astype(np.float32)
+    Q = rng.standard_normal((300, 16)).astype(np.float32)
+    ids = np.arange(3000, dtype=np.uint64)
+    C = np.concatenate([X[:10], 6.0 + rng.standard_normal((6, 16)).astype(np.float32) * 0.1])
+    C[10:] *= np.where(rng.random((6, 1)) < 0.5, -1, 1).astype(np.float32)
+    o = oracle.OracleIndex(16, 16, 0)
+    o.centroids = C
+    o.add(X, ids)
+    assert any(o.list_count(l) == 0 for l in range(16))
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(16, 16))
+    g.centroids = C
+    g.add(X, ids)
+    dp = 64                                  # 16 dims pad to one 64-float row
+    blocks = sorted(((o.list_count(l) + 63) // 64 for l in range(16)), reverse=True)
+    g.set_option("list_cache_bytes", (sum(blocks[:12]) + 1) * 64 * (dp * 4 + 8))
+    Dr, Ir = o.search(Q, 12, 8)
+    for batch in (256, 7):
+        g.set_batch(batch)
+        assert_same(*g.search(Q, nprobe=12, k=8), Dr, Ir)
+    assert np.all(bits(Dr) == bits(g.search(Q, nprobe=12, k=8)[0]))
