@@ -151,6 +151,7 @@ def main():
     ap.add_argument("--emulate-shard", type=int, default=0, metavar="W",
                     help="diagnostic: one process keeps rank 0's LPT shard of W and runs its partial search "
                          "(the per-GPU work of a W-GPU node, without the all-gather); not a bench line")
+    ap.add_argument("--prewarm", action="store_true", help="warm every list up front (list-cache tier)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning knob (vdb_ivf_set_option), e.g. wide_stride=1; results never change")
     args = ap.parse_args()
@@ -178,6 +179,8 @@ def run(vdb, args, device, rank, world):
     for o in args.opt:
         name, val = o.split("=", 1)
         idx.set_option(name, int(val))
+    if args.prewarm:  # list-cache tier: load every list up front, in list order (vdb.QueryService/Warmup)
+        idx.warmup_lists(list(range(args.nlist)))
     if args.emulate_shard > 1 and world == 1:
         idx.set_shard(0, args.emulate_shard)
     B, k = args.batch, args.k

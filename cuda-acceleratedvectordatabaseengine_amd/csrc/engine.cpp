@@ -197,6 +197,7 @@ struct vdb_ivf {
     std::vector<uint64_t> last_use;         // per list: batch tick of the last probe
     std::map<uint64_t, uint64_t> free_ext;  // free cache extents: block offset -> blocks
     uint64_t use_tick = 0, cache_used = 0;
+    uint64_t resident_n = 0, storable_n = 0;  // cached lists / non-empty lists stored here
     uint64_t cache_loads = 0, cache_evictions = 0, cache_bytes_in = 0;
     DevBuf<uint32_t> probe_stage;  // pinned: the batch's probes, read by the host
     DevBuf<uint64_t> dir_stage;    // pinned: directory upload source
@@ -402,10 +403,12 @@ struct vdb_ivf {
             while (seg_blocks > 1 && local / ((uint64_t)seg_blocks * 64) < 4096) seg_blocks >>= 1;
         }
         std::vector<uint32_t> cl(nlist), cg(nlist), ns(nlist);
+        storable_n = 0;
         for (uint32_t l = 0; l < nlist; ++l) {
             require(count[l] < (1ull << 32), "list longer than 2^32 vectors", VDB_ERR_UNSUPPORTED);
             cg[l] = (uint32_t)count[l];
             cl[l] = owned[l] ? (uint32_t)count[l] : 0u;
+            storable_n += cl[l] > 0;
             ns[l] = (uint32_t)cdiv(cl[l], (uint64_t)seg_blocks * 64);
         }
         upload_scan_directory(stream);
@@ -479,6 +482,7 @@ struct vdb_ivf {
         free_ext.clear();
         if (cache_blocks) free_ext[0] = cache_blocks;
         cache_used = 0;
+        resident_n = 0;
     }
 
     uint64_t cache_alloc(uint64_t nb) {  // first fit
@@ -498,6 +502,7 @@ struct vdb_ivf {
         auto it = free_ext.emplace(cache_off[l], nb).first;
         cache_off[l] = kAbsent;
         cache_used -= nb;
+        --resident_n;
         auto nx = std::next(it);
         if (nx != free_ext.end() && it->first + it->second == nx->first) {
             it->second += nx->second;
@@ -569,6 +574,7 @@ struct vdb_ivf {
                 continue;
             }
             cache_off[l] = off;
+            ++resident_n;
             const uint64_t nb = list_blocks(l);
             HIPCHECK(hipMemcpyAsync(cache.p + off * d4 * 64, arena.p + block_off[l] * d4 * 64, nb * d4 * 64 * sizeof(float4),
                                     hipMemcpyHostToDevice, s));
@@ -850,7 +856,7 @@ struct vdb_ivf {
             vdbk::launch_select(regs_p, w.cd.p, nlist, B, P, w.probes.p, s);
         }
         if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
-        if (tiered()) {
+        if (tiered() && resident_n < storable_n) {  // (everything cached: no host round trip)
             HIPCHECK(hipMemcpyAsync(probe_stage.ensure(BP), w.probes.p, (size_t)BP * 4, hipMemcpyDeviceToHost, s));
             HIPCHECK(hipStreamSynchronize(s));
             if (!make_resident(probe_stage.p, BP, s)) {
