@@ -180,6 +180,7 @@ struct vdb_ivf {
     uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)
     uint32_t diag = 0;                          // scan diagnostics (results invalid when set)
     uint32_t segs_item_opt = 0;   // segments per wide item (0 = 4: one per wave, taken dynamically)
+    bool fused_scan = true;       // narrow items inside the wide scan's grid (option fused_scan; +2-3 %)
     uint32_t narrow_blocks = 64;  // persistent narrow-scan workgroups beside the wide scan (1/8 shard: +1.5 % vs 512)
 
     // List-cache tier (option list_cache_bytes > 0), the reference's residency model
@@ -218,7 +219,7 @@ struct vdb_ivf {
         hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
         bool used = false;
     };
-    static constexpr int kSlots = 2;
+    static constexpr int kSlots = 3;
     SearchSlot slots[kSlots];
     uint32_t next_slot = 0;
     DevBuf<float> out_d, qin;  // host-API staging (synchronous calls)
@@ -871,10 +872,14 @@ struct vdb_ivf {
         vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? 1 : 0, segs_item, w.items.p, w.items_w.p,
                           w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
-        const vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
+        vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
-                                wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item};
-        if (wide) {
+                                wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item, 0};
+        if (wide && fused_scan) {
+            // one persistent grid takes both queues (no side stream, no fork/join)
+            sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks, vdbk::kPersistentBlocks / 2));
+            vdbk::launch_scan_wide(metric, (uint32_t)std::max<uint64_t>(max_wide, (max_items + 3) / 4), sa, s);
+        } else if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));
             HIPCHECK(hipStreamWaitEvent(w.side, w.fork, 0));
@@ -1365,6 +1370,8 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "segs_per_item") {
             require(value == 0 || (value >= 4 && value <= 64), "segs_per_item is 0 (auto) or 4..64");
             h->segs_item_opt = (uint32_t)value;
+        } else if (n == "fused_scan") {
+            h->fused_scan = value != 0;
         } else if (n == "narrow_blocks") {
             require(value > 0 && value <= 4096, "narrow_blocks out of range");
             h->narrow_blocks = (uint32_t)value;

@@ -1050,6 +1050,20 @@ __global__ __launch_bounds__(256) void ivf_scan_narrow(ScanArgs a) {
     }
 }
 
+// Narrow items pulled by one wave until the queue is empty (the fused wide scan).
+// (Inlined at both call sites: a real call would spill the wide path's registers.)
+template <int M>
+__device__ __forceinline__ void drain_narrow(const ScanArgs& a) {
+    const uint32_t n_narrow = a.counters[0];
+    for (;;) {
+        uint32_t idx = 0;
+        if (lane_id() == 0) idx = atomicAdd(&a.work[0], 1u);
+        idx = __builtin_amdgcn_readfirstlane(idx);
+        if (idx >= n_narrow) break;
+        scan_narrow<1, M>(a, a.items[idx]);
+    }
+}
+
 // ivf_scan_wide: the large lists. Workgroup b takes wide item b: 4 consecutive
 // segments (one per wave) x up to 16 of the list's queries, staged once in LDS.
 template <int M>
@@ -1068,6 +1082,10 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_wide(ScanArgs a) {
     // map is a permutation.
     uint32_t stride = a.wide_stride;
     if (stride > 1 && n_wide % stride == 0) stride = stride == 40009u ? 40013u : 40009u;
+    // Fused launch: narrow items (HBM-bound) run beside the wide ones (often VALU-bound)
+    // inside this one persistent grid, no second stream: the last a.fused workgroups
+    // start on the narrow queue, and every wave drains it once the wide queue is empty.
+    if (a.fused && blockIdx.x + a.fused >= gridDim.x) drain_narrow<M>(a);
     __shared__ uint32_t s_next;
     __shared__ uint32_t s_seg;  // next segment of the current item
     for (;;) {
@@ -1115,6 +1133,7 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_wide(ScanArgs a) {
         }
         __syncthreads();  // qlds is restaged by the next wide item
     }
+    if (a.fused) drain_narrow<M>(a);
 }
 
 // Offer n contiguous (dist, id) entries to a wave top-k: 64 x kPre entries per round,
@@ -1763,7 +1782,9 @@ void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes
                            const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                            const uint2* l1_items, const uint32_t* counters, const float* part_d,
                            const uint64_t* part_i, uint32_t k, float* l1_d, uint64_t* l1_i, hipStream_t s) {
-    const uint32_t g = launch_grid(grid_items, 4);
+    // grid-stride over the batch's actual item count (counters[2]): a small grid, so a
+    // merge issued while another batch's scan holds the CUs has few workgroups to place
+    const uint32_t g = std::min<uint32_t>(launch_grid(grid_items, 4), kMergeBlocks);
     if (!grid_items) return;
 #define VDB_MP(R) ivf_merge_partials<R><<<g, 256, 0, s>>>(probes, count_global, nseg_qp, part_base_qp, l1base_qp, l1_items, counters, part_d, part_i, k, l1_d, l1_i)
     switch (regs) {

@@ -17,6 +17,7 @@ namespace vdbk {
 constexpr int kMaxSegBlocks = 16;          // 64-vector blocks per scan segment (the runtime
                                            // size is 1..8, chosen per shard size by the engine)
 constexpr int kTilePipe = 16;              // float4 tiles of a list vector in flight per lane (scan)
+constexpr uint32_t kMergeBlocks = 256;  // level-1 partial merge: workgroups (grid-stride)
 constexpr int kTilePipeNarrow = 4;         // the same for narrow items (queries held in SGPRs)
 constexpr int kTileAlign = kTilePipe;      // D4 is padded to whole pipeline rounds
 constexpr int kMergeFan = 32;              // segment partials folded per level-1 merge wave
@@ -95,6 +96,8 @@ struct ScanArgs {
     uint32_t seg_blocks;   // 64-vector blocks per list segment (one wave's unit of a scan item)
     uint32_t diag;         // diagnostics only (0 in production): 1 skip top-k upkeep, 2 one query pair
     uint32_t segs_item;    // segments per wide item (>= 4; the 4 waves take them dynamically)
+    uint32_t fused;        // ivf_scan_wide also drains the narrow queue (R = 1); the last `fused`
+                           // workgroups start on narrow items (0: narrow items on their own kernel)
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k);

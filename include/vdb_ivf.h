@@ -178,7 +178,8 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * "stale_slots" (as vdb_ivf_set_batch / vdb_ivf_set_stale_slots), "seg_vectors" (0 = auto, or
  * 64/128/256/512/1024: list vectors per scan segment), "coalesce" (0/1), "coalesce_max_queries",
  * "coalesce_window_us" (0: no waiting; calls arriving while the device is busy batch up),
- * "list_cache_bytes" (0 = every list HBM-resident; > 0 = the list-cache tier above with an
+ * "fused_scan" (1, default: one persistent scan grid takes both the wide and the narrow
+ * items; 0: narrow items on a second stream), "list_cache_bytes" (0 = every list HBM-resident; > 0 = the list-cache tier above with an
  * HBM cache of that many bytes; a search whose single query probes more fails with
  * VDB_ERR_OUT_OF_MEMORY, a batch probing more is split). */
 int vdb_ivf_set_option(vdb_ivf* index, const char* name, int64_t value);

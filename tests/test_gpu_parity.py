@@ -285,9 +285,10 @@ def test_hub_lists_wide_items(k, seg):
     g.set_option("seg_vectors", seg)   # segment size never changes results
     for batch in (64, 130):
         g.set_batch(batch)
-        for stride, spi in ((40009, 0), (1, 4), (7, 12)):   # dispatch order / item size never change results
-            g.set_option("wide_stride", stride)
-            g.set_option("segs_per_item", spi)
+        for stride, spi, fused in ((40009, 0, 1), (1, 4, 0), (7, 12, 1)):   # dispatch order / item size /
+            g.set_option("wide_stride", stride)                            # fused narrow+wide grid never
+            g.set_option("segs_per_item", spi)                             # change results
+            g.set_option("fused_scan", fused)
             assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))
 
 
