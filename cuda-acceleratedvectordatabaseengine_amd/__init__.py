@@ -22,7 +22,7 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libvdb_ivf.so")
+LIB_PATH = os.environ.get("VDB_IVF_LIB") or os.path.join(_HERE, "lib", "libvdb_ivf.so")  # override: A/B builds
 CPP_LIB_PATH = os.path.join(_HERE, "lib", "libvdb_ivf_cpp.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "vdb_ivf.h")
 

@@ -6,7 +6,8 @@ of the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, "HBM"), so
 value is doubled. rocprofv3 reports FETCH_SIZE in KiB.
 
 usage: tools/pmc_traffic.py <pmc-output-dir> <batches> <workload-key> [out.json]
-The scan phase of one batch is one ivf_scan_wide + one ivf_scan_narrow dispatch; the
+The scan phase of one batch is one ivf_scan_wide dispatch (plus ivf_scan_narrow when the
+fused scan is off); the
 bytes of all scan dispatches are summed and divided by the number of batches.
 """
 import csv
