@@ -225,6 +225,115 @@ __global__ __launch_bounds__(256) void ivf_coarse_mfma(const float* __restrict__
     }
 }
 
+// The same bounds for large row counts (assignment at add / Lloyd, big search batches),
+// register-blocked: one wave computes a 32-row x 32-centroid output as 2 x 2 MFMA tiles,
+// so every float4 it loads feeds 8 MFMAs instead of 4 (the 16 x 16 wave above is bound
+// by L1 traffic, not by the matrix cores). A workgroup's 4 waves share the 32 rows and
+// take 4 adjacent 32-centroid tiles. Lane (r, h) holds dims 4h .. 4h + 3 of each
+// 16-dim step of rows r and 16 + r of both operands, as above.
+template <int M>
+__global__ __launch_bounds__(256) void ivf_coarse_mfma2x2(const float* __restrict__ cent_rm, uint32_t nlist,
+                                                          uint32_t dp, const float* __restrict__ qpad, uint32_t B,
+                                                          float* __restrict__ approx, float* __restrict__ delta) {
+    constexpr int G = 4;  // 16-dim steps per prefetch group (dp / 16 is a multiple of 4)
+    const int lane = lane_id();
+    const uint32_t ct = blockIdx.x * 4 + wave_index();  // 32-centroid tile
+    const uint32_t qt = blockIdx.y;                      // 32-row tile
+    if (ct * 32 >= nlist) return;
+    const int r = lane & 15, h = lane >> 4;
+    const float4* qa[2];
+    const float4* cb[2];
+    bool qok[2], cok[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const uint32_t qrow = qt * 32 + i * 16 + r, crow = ct * 32 + i * 16 + r;
+        qok[i] = qrow < B;
+        cok[i] = crow < nlist;
+        qa[i] = (const float4*)(qpad + (size_t)(qok[i] ? qrow : 0) * dp) + h;
+        cb[i] = (const float4*)(cent_rm + (size_t)(cok[i] ? crow : 0) * dp) + h;
+    }
+    f4v acc[2][2];
+    float qn[2] = {0.f, 0.f}, cn[2] = {0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+    const uint32_t steps = dp / 16;
+    float4 a[2][G], b[2][G];
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i][g] = qa[i][(size_t)g * 4], b[i][g] = cb[i][(size_t)g * 4];
+    for (uint32_t s0 = 0; s0 < steps; s0 += G) {
+        float4 an[2][G], bn[2][G];
+        const uint32_t nx = s0 + G < steps ? s0 + G : s0;  // the last group re-loads itself
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) an[i][g] = qa[i][(size_t)(nx + g) * 4], bn[i][g] = cb[i][(size_t)(nx + g) * 4];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float4 x[2], y[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                x[i] = qok[i] ? a[i][g] : make_float4(0.f, 0.f, 0.f, 0.f);
+                y[i] = cok[i] ? b[i][g] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    f4v& ac = acc[i][j];
+                    ac = __builtin_amdgcn_mfma_f32_16x16x4f32(x[i].x, y[j].x, ac, 0, 0, 0);
+                    ac = __builtin_amdgcn_mfma_f32_16x16x4f32(x[i].y, y[j].y, ac, 0, 0, 0);
+                    ac = __builtin_amdgcn_mfma_f32_16x16x4f32(x[i].z, y[j].z, ac, 0, 0, 0);
+                    ac = __builtin_amdgcn_mfma_f32_16x16x4f32(x[i].w, y[j].w, ac, 0, 0, 0);
+                }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                qn[i] = qn[i] + (x[i].x * x[i].x + x[i].y * x[i].y) + (x[i].z * x[i].z + x[i].w * x[i].w);
+                cn[i] = cn[i] + (y[i].x * y[i].x + y[i].y * y[i].y) + (y[i].z * y[i].z + y[i].w * y[i].w);
+                a[i][g] = an[i][g];
+                b[i][g] = bn[i][g];
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        qn[i] += __shfl_xor(qn[i], 16);
+        qn[i] += __shfl_xor(qn[i], 32);
+        cn[i] += __shfl_xor(cn[i], 16);
+        cn[i] += __shfl_xor(cn[i], 32);
+    }
+    const float K = 4.0f * (float)(dp + 4) * 5.9604645e-8f;  // 4 (n + 4) u, as ivf_coarse_mfma
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t c = ct * 32 + j * 16 + (lane & 15);
+        const float ca = sqrtf(cn[j]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int row = (lane >> 4) * 4 + reg;
+                const float qrn = __shfl(qn[i], row);
+                const uint32_t q = qt * 32 + i * 16 + row;
+                if (q < B && c < nlist) {
+                    const float qa_ = sqrtf(qrn);
+                    float ap, dl;
+                    if constexpr (M == kL2) {
+                        ap = (qrn + cn[j]) - 2.0f * acc[i][j][reg];
+                        dl = K * ((qa_ + ca) * (qa_ + ca)) + 1e-30f;
+                    } else {
+                        ap = -acc[i][j][reg];
+                        dl = K * (qa_ * ca) + 1e-30f;
+                    }
+                    approx[(size_t)q * nlist + c] = ap;
+                    delta[(size_t)q * nlist + c] = dl;
+                }
+            }
+    }
+}
+
 // Sequential exact distance of wave-uniform query row q against this lane's centroid
 // row (the reference's loop order, cpp:308-318). Rows are zero padded to dp.
 template <int M>
@@ -1701,6 +1810,12 @@ void launch_select(int regs, const float* cd, uint32_t nlist, uint32_t B, uint32
 
 void launch_coarse_mfma(int metric, const float* cent_rm, uint32_t nlist, uint32_t dp, const float* qpad,
                         uint32_t B, float* approx, float* delta, hipStream_t s) {
+    if (B >= kMfmaBlockedRows) {  // enough 32-row tiles to fill the chip: the register-blocked kernel
+        dim3 g2(cdiv(cdiv(nlist, 32), 4), cdiv(B, 32));
+        if (metric == kL2) ivf_coarse_mfma2x2<kL2><<<g2, 256, 0, s>>>(cent_rm, nlist, dp, qpad, B, approx, delta);
+        else ivf_coarse_mfma2x2<kIP><<<g2, 256, 0, s>>>(cent_rm, nlist, dp, qpad, B, approx, delta);
+        return;
+    }
     dim3 grid(cdiv(cdiv(nlist, 16), 4), cdiv(B, 16));
     const bool g8 = (dp / 16) % 8 == 0;  // dp is a multiple of 64, so steps are a multiple of 4
     if (metric == kL2) {

@@ -17,6 +17,7 @@ namespace vdbk {
 constexpr int kMaxSegBlocks = 16;          // 64-vector blocks per scan segment (the runtime
                                            // size is 1..8, chosen per shard size by the engine)
 constexpr int kTilePipe = 16;              // float4 tiles of a list vector in flight per lane (scan)
+constexpr uint32_t kMfmaBlockedRows = 1024;  // coarse bounds: 2x2-blocked MFMA kernel from this many rows
 constexpr uint32_t kMergeBlocks = 256;  // level-1 partial merge: workgroups (grid-stride)
 constexpr int kTilePipeNarrow = 4;         // the same for narrow items (queries held in SGPRs)
 constexpr int kTileAlign = kTilePipe;      // D4 is padded to whole pipeline rounds

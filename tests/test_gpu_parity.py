@@ -425,6 +425,34 @@ def test_mfma_coarse_near_ties():
         assert probes_ref.shape == (len(Q), nprobe)
 
 
+@pytest.mark.parametrize("metric", [0, 1])
+def test_blocked_mfma_bounds_large_batches(metric):
+    """From 1024 rows the coarse bounds come from the 2x2 register-blocked MFMA kernel:
+    a search batch of 1500 queries and an add() of near-tie rows (centroid copies with
+    ulp jitter, ragged 32-row / 32-centroid tiles) must still give the reference's
+    probe sets and argmin (ties to the lowest centroid)."""
+    rng = np.random.default_rng(17 + metric)
+    dim, nlist = 80, 333                               # dp 128, nlist not a multiple of 32
+    base = rng.standard_normal((111, dim)).astype(np.float32)
+    C = np.repeat(base, 3, axis=0)
+    C[1::3] = (C[1::3].view(np.int32) + rng.integers(-1, 2, size=C[1::3].shape).astype(np.int32)).view(np.float32)
+    X = np.concatenate([np.repeat(C, 5, axis=0),                       # exact copies: distance 0 ties
+                        rng.standard_normal((3001, dim)).astype(np.float32)])
+    ids = rng.permutation(len(X)).astype(np.uint64)
+    Q = np.concatenate([C[rng.integers(0, nlist, 700)] + 1e-4 * rng.standard_normal((700, dim)).astype(np.float32),
+                        rng.standard_normal((800, dim)).astype(np.float32)])
+    o = oracle.OracleIndex(dim, nlist, metric)
+    o.centroids = C
+    o.add(X, ids)
+    g = mirror_from_oracle(o, dim, nlist, metric)
+    g.add(X, ids)
+    for l in range(nlist):
+        assert np.array_equal(g.get_list(l)[1], o.get_list(l)[1]), f"list {l} membership differs"
+    g.set_batch(4096)                                  # one internal batch of 1500 rows
+    for nprobe in (1, 5):
+        assert_same(*g.search(Q, nprobe=nprobe, k=10), *o.search(Q, nprobe, 10, threads=16))
+
+
 def test_nan_query_is_contained():
     """A NaN query must not make the engine read outside its lists (no crash), and
     the other queries of the batch keep their exact results."""
