@@ -50,7 +50,7 @@ class _Config(ctypes.Structure):
 class CacheStats(ctypes.Structure):
     _fields_ = [("capacity_bytes", ctypes.c_uint64), ("resident_bytes", ctypes.c_uint64),
                 ("resident_lists", ctypes.c_uint64), ("loads", ctypes.c_uint64), ("evictions", ctypes.c_uint64),
-                ("bytes_loaded", ctypes.c_uint64)]
+                ("bytes_loaded", ctypes.c_uint64), ("file_bytes_read", ctypes.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -120,6 +120,7 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int64]),
         "vdb_ivf_coalesce_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "vdb_ivf_cache_stats": (ctypes.c_int, [vp, ctypes.POINTER(CacheStats)]),
+        "vdb_ivf_open_lists": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "vdb_ivf_profile_enable": (ctypes.c_int, [vp, i32]),
         "vdb_ivf_profile_reset": (ctypes.c_int, [vp]),
         "vdb_ivf_profile_read": (ctypes.c_int, [vp, ctypes.POINTER(Profile)]),
@@ -348,6 +349,11 @@ class IVFFlatIndex:
         b, r = ctypes.c_uint64(0), ctypes.c_uint64(0)
         _check(lib().vdb_ivf_coalesce_stats(self._h, ctypes.byref(b), ctypes.byref(r)))
         return b.value, r.value
+
+    def open_lists(self, path: str):
+        """Serve the lists from an index file written by save() through the list-cache
+        tier (set_option("list_cache_bytes", n) first); the handle becomes read-only."""
+        _check(lib().vdb_ivf_open_lists(self._h, path.encode()))
 
     def cache_stats(self) -> dict:
         """List-cache tier counters (option list_cache_bytes; capacity 0 = tier off)."""

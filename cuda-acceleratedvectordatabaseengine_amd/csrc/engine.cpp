@@ -16,6 +16,8 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <fcntl.h>
+#include <unistd.h>
 #include <map>
 #include <memory>
 #include <thread>
@@ -203,6 +205,17 @@ struct vdb_ivf {
     DevBuf<uint32_t> probe_stage;  // pinned: the batch's probes, read by the host
     DevBuf<uint64_t> dir_stage;    // pinned: directory upload source
 
+    // File home for the tier (vdb_ivf_open_lists): the lists stay in an index file written
+    // by vdb_ivf_save and are read into the cache on demand (pread -> pinned staging ->
+    // HBM -> pad + interleave kernels), instead of living in host memory.
+    int home_fd = -1;
+    std::vector<uint64_t> file_off;  // per list: file offset of its ids (vectors follow)
+    DevBuf<float> fstage[2];         // pinned: row-major vectors of a chunk
+    DevBuf<uint64_t> istage[2];      // pinned: ids of a chunk
+    hipEvent_t fstage_done[2] = {nullptr, nullptr};
+    DevBuf<float> drows, dpad;       // device: a chunk's rows, then zero-padded to dp
+    uint64_t file_bytes_read = 0;
+
     // Search workspaces: a ring of slots so that searches issued on different streams
     // run concurrently (one batch's small kernels and scan tail overlap the next
     // batch's scan). A call takes the next slot; its stream first waits for the
@@ -241,6 +254,9 @@ struct vdb_ivf {
 
     ~vdb_ivf() {
         stop_coalescer();
+        if (home_fd >= 0) ::close(home_fd);
+        for (auto& e : fstage_done)
+            if (e) (void)hipEventDestroy(e);
         for (auto& e : events) {
             (void)hipEventDestroy(e.begin);
             (void)hipEventDestroy(e.coarse_end);
@@ -577,15 +593,107 @@ struct vdb_ivf {
             cache_off[l] = off;
             ++resident_n;
             const uint64_t nb = list_blocks(l);
+            ++cache_loads;
+            cache_bytes_in += nb * block_bytes(dp);
+            if (file_home()) {
+                load_list_from_file(l, off, s);
+                continue;
+            }
             HIPCHECK(hipMemcpyAsync(cache.p + off * d4 * 64, arena.p + block_off[l] * d4 * 64, nb * d4 * 64 * sizeof(float4),
                                     hipMemcpyHostToDevice, s));
             HIPCHECK(hipMemcpyAsync(cache_ids.p + off * 64, arena_ids.p + block_off[l] * 64, nb * 64 * 8,
                                     hipMemcpyHostToDevice, s));
-            ++cache_loads;
-            cache_bytes_in += nb * block_bytes(dp);
         }
         upload_scan_directory(s);
         return true;
+    }
+
+    bool file_home() const { return home_fd >= 0; }
+
+    void pread_all(void* dst, size_t bytes, uint64_t off) {
+        char* p = (char*)dst;
+        while (bytes) {
+            const ssize_t r = ::pread(home_fd, p, bytes, (off_t)off);
+            require(r > 0, "short read from the list file", VDB_ERR_STATE);
+            p += r;
+            bytes -= (size_t)r;
+            off += (uint64_t)r;
+            file_bytes_read += (uint64_t)r;
+        }
+    }
+
+    // One list from the file into cache blocks [off, off + blocks): chunks of whole
+    // 64-row blocks, each read into one of two pinned buffers (the other one's copy
+    // is in flight), copied to HBM, padded to dp and interleaved into the block layout.
+    void load_list_from_file(uint32_t l, uint64_t off, hipStream_t s) {
+        const uint64_t n = count[l];
+        const uint64_t rows = std::max<uint64_t>(64, ((32ull << 20) / ((uint64_t)dim * 4)) / 64 * 64);
+        for (int i = 0; i < 2; ++i) {
+            if (!fstage_done[i]) HIPCHECK(hipEventCreateWithFlags(&fstage_done[i], hipEventDisableTiming));
+            fstage[i].host = istage[i].host = true;
+            fstage[i].ensure(rows * dim);
+            istage[i].ensure(rows);
+        }
+        drows.ensure(rows * dim);
+        dpad.ensure(rows * dp);
+        const uint64_t ids_at = file_off[l], vec_at = file_off[l] + n * 8;
+        for (uint64_t r0 = 0, c = 0; r0 < n; r0 += rows, ++c) {
+            const int i = (int)(c & 1);
+            const uint64_t m = std::min(rows, n - r0);
+            HIPCHECK(hipEventSynchronize(fstage_done[i]));  // this buffer's previous copy has landed
+            pread_all(istage[i].p, m * 8, ids_at + r0 * 8);
+            pread_all(fstage[i].p, m * dim * 4, vec_at + r0 * dim * 4);
+            const uint64_t b = off + r0 / 64;
+            HIPCHECK(hipMemcpyAsync(cache_ids.p + b * 64, istage[i].p, m * 8, hipMemcpyHostToDevice, s));
+            HIPCHECK(hipMemcpyAsync(drows.p, fstage[i].p, m * dim * 4, hipMemcpyHostToDevice, s));
+            HIPCHECK(hipEventRecord(fstage_done[i], s));
+            vdbk::launch_pad_rows(drows.p, m, dim, dp, dpad.p, s);
+            vdbk::launch_interleave(dpad.p, m, dp, cache.p + b * d4 * 64, s);
+            HIPCHECK(hipGetLastError());
+        }
+    }
+
+    // Serve the lists from an index file (vdb_ivf_save format) through the tier.
+    void open_lists(const char* path) {
+        require(tiered(), "open_lists needs the list-cache tier (set list_cache_bytes first)", VDB_ERR_STATE);
+        quiesce();
+        const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+        require(fd >= 0, std::string("cannot open ") + path, VDB_ERR_STATE);
+        if (home_fd >= 0) ::close(home_fd);
+        home_fd = fd;
+        char magic[8];
+        uint32_t hdr[4];
+        pread_all(magic, 8, 0);
+        pread_all(hdr, sizeof(hdr), 8);
+        if (std::memcmp(magic, "VDBIVF01", 8) != 0 || hdr[0] != dim || hdr[1] != nlist || (int)hdr[2] != metric) {
+            ::close(home_fd);
+            home_fd = -1;
+            throw VdbError(VDB_ERR_INVALID_ARGUMENT, "index file does not match this index's configuration");
+        }
+        std::vector<float> c((size_t)nlist * dim);
+        pread_all(c.data(), c.size() * 4, 24);
+        HIPCHECK(hipMemcpy2DAsync(cent_rm.p, dp * 4, c.data(), dim * 4, dim * 4, nlist, hipMemcpyHostToDevice, stream));
+        refresh_centroid_layout();
+        uint64_t at = 24 + (uint64_t)c.size() * 4;
+        file_off.assign(nlist, 0);
+        total = 0;
+        for (uint32_t l = 0; l < nlist; ++l) {
+            uint64_t cnt = 0;
+            pread_all(&cnt, 8, at);
+            file_off[l] = at + 8;
+            count[l] = cnt;
+            total += cnt;
+            at += 8 + cnt * 8 + cnt * (uint64_t)dim * 4;
+        }
+        arena.release();  // no home copy in memory: the file is the home
+        arena_ids.release();
+        arena_blocks = 0;
+        block_off.assign(nlist, 0);
+        owned.assign(nlist, 1);
+        rank = 0;
+        world = 1;
+        cache_reset();
+        upload_directory();
     }
 
     // Turn the tier on (bytes > 0: HBM cache of that many bytes, arena moved to host
@@ -594,10 +702,11 @@ struct vdb_ivf {
         quiesce();
         const uint64_t nb = bytes / block_bytes(dp);
         require(bytes == 0 || nb > 0, "list_cache_bytes is below one block of 64 vectors");
+        require(nb > 0 || !file_home(), "lists served from a file need the list-cache tier", VDB_ERR_STATE);
         cache.release();
         cache_ids.release();
         cache_blocks = 0;
-        if ((nb > 0) != arena.host) relayout(count, owned, nb > 0);  // moves the arena
+        if (!file_home() && (nb > 0) != arena.host) relayout(count, owned, nb > 0);  // moves the arena
         cache_blocks = nb;
         if (nb) {  // one slack block: the scan prefetches past a segment's end
             cache.ensure((nb + 1) * d4 * 64);
@@ -734,6 +843,8 @@ struct vdb_ivf {
     // ---- add: ivf_flat_index.cpp:148-202 ----
     void add(const float* d_v, const uint64_t* d_ids, uint64_t n) {
         if (n == 0) return;
+        require(!file_home(), "lists are served from a file (vdb_ivf_open_lists): the index is read-only",
+                VDB_ERR_STATE);
         DevBuf<float> tmp;
         const float* vpad = padded_rows(d_v, n, tmp);
         DevBuf<uint32_t> asg;
@@ -744,6 +855,8 @@ struct vdb_ivf {
     // Append rows to the given lists, keeping input order within each list
     // (cpp:160-192). `asg` holds one list id per row (device).
     void append(const float* vpad, const uint64_t* d_ids, const uint32_t* asg, uint64_t n) {
+        require(!file_home(), "lists are served from a file (vdb_ivf_open_lists): the index is read-only",
+                VDB_ERR_STATE);
         DevBuf<uint32_t> skeys, order, counts;
         group_by_key(asg, n, skeys, order);
         std::vector<uint32_t> added = key_counts(asg, n, counts);
@@ -776,7 +889,13 @@ struct vdb_ivf {
         // Lists this handle no longer scans must have been stored here before.
         for (uint32_t l = 0; l < nlist; ++l)
             require(!new_owned[l] || owned[l] || count[l] == 0, "shard needs a list this handle dropped", VDB_ERR_STATE);
-        relayout(count, new_owned);
+        if (file_home()) {  // nothing in memory to move: the file holds every list
+            quiesce();
+            owned = new_owned;
+            cache_reset();
+        } else {
+            relayout(count, new_owned);
+        }
         rank = r;
         world = w;
         upload_directory();
@@ -1313,6 +1432,11 @@ int vdb_ivf_get_list(vdb_ivf* h, uint32_t list, float* vectors, uint64_t* ids) {
         const uint64_t c = h->count[list];
         if (c == 0) return;
         require(h->owned[list], "list is not stored on this shard", VDB_ERR_STATE);
+        if (h->file_home()) {  // the file holds the list row-major, as returned
+            if (ids) h->pread_all(ids, c * 8, h->file_off[list]);
+            if (vectors) h->pread_all(vectors, c * h->dim * 4, h->file_off[list] + c * 8);
+            return;
+        }
         DevBuf<float> dv;
         DevBuf<uint64_t> di;
         vdbk::launch_export_list(h->arena.p, h->arena_ids.p, h->block_off[list], (uint32_t)c, h->dim, h->d4,
@@ -1404,6 +1528,16 @@ int vdb_ivf_cache_stats(vdb_ivf* h, vdb_ivf_cache_stats_t* out) {
         uint64_t n = 0;
         for (uint32_t l = 0; l < h->nlist && h->tiered(); ++l) n += h->cache_off[l] != vdb_ivf::kAbsent;
         out->resident_lists = n;
+        out->file_bytes_read = h->file_bytes_read;
+    });
+}
+
+int vdb_ivf_open_lists(vdb_ivf* h, const char* path) {
+    return guarded([&] {
+        require(h && path, "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        h->open_lists(path);
     });
 }
 

@@ -151,8 +151,17 @@ typedef struct vdb_ivf_cache_stats_t {
     uint64_t loads;           /* lists copied host -> HBM */
     uint64_t evictions;       /* lists evicted to make room (not counting vdb_ivf_evict) */
     uint64_t bytes_loaded;
+    uint64_t file_bytes_read; /* lists served from a file: bytes read from it */
 } vdb_ivf_cache_stats_t;
 int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
+/* The tier's home on disk (ListPrefetcher::register_list_file / prefetch_lists,
+ * engine/prefetcher.h:139-183; list files of format/storage.h): serve this handle's lists
+ * from an index file written by vdb_ivf_save, without reading them into memory.
+ * Centroids and list sizes are read at once; a list is read (pread -> pinned staging ->
+ * HBM -> pad + interleave on the device) when a batch first probes it or on
+ * vdb_ivf_warmup, and evicted like any cached list. Needs "list_cache_bytes" > 0 set
+ * first; the handle becomes read-only (add fails with VDB_ERR_STATE). */
+int vdb_ivf_open_lists(vdb_ivf* index, const char* path);
 
 uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* index);
 uint64_t vdb_ivf_ntotal(const vdb_ivf* index);

@@ -119,3 +119,42 @@ def test_cache_tier_empty_lists_stale_slots():
         g.set_batch(batch)
         assert_same(*g.search(Q, nprobe=12, k=8), Dr, Ir)
     assert np.all(bits(Dr) == bits(g.search(Q, nprobe=12, k=8)[0]))
+
+
+@pytest.mark.parametrize("dim", [64, 70])
+def test_lists_served_from_file(tmp_path, dim):
+    """The tier's home on disk (vdb_ivf_open_lists): a saved index is served without
+    loading its lists; they are read, padded and interleaved on demand. Results,
+    get_list and the read-only contract must hold; dim 70 exercises row padding."""
+    X, Q, ids = oracle.reference_test_data(20000, 200, dim, seed=9)
+    o = oracle.OracleIndex(dim, NLIST, 0)
+    o.train(X[:5000])
+    o.add(X, ids)
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    g.centroids = o.centroids
+    g.add(X, ids)
+    path = str(tmp_path / "index.vdb")
+    g.save(path)
+    del g
+    h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    dp = 128 if dim > 64 else 64
+    blocks = np.array([(o.list_count(l) + 63) // 64 for l in range(NLIST)])
+    need = max(int(blocks[o.select_nprobe(q, NPROBE)].sum()) for q in Q)
+    h.set_option("list_cache_bytes", (need + 8) * 64 * (dp * 4 + 8))
+    h.open_lists(path)
+    assert h.get_total_vectors() == len(X)
+    assert np.array_equal(bits(h.centroids), bits(o.centroids))
+    Dr, Ir = o.search(Q, NPROBE, K)
+    for batch in (256, 1):
+        h.set_batch(batch)
+        assert_same(*h.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
+    st = h.cache_stats()
+    assert st["loads"] > 0 and st["evictions"] > 0 and st["file_bytes_read"] > 0
+    for l in (0, 31, NLIST - 1):
+        v, i = h.get_list(l)
+        ov, oi = o.get_list(l)
+        assert np.array_equal(i, oi) and np.array_equal(bits(v), bits(ov))
+    with pytest.raises(vdb.VdbError, match="read-only"):
+        h.add(X[:10], ids[:10])
+    h.warmup_lists(list(range(NLIST)))       # LRU keeps what fits; results unchanged
+    assert_same(*h.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
