@@ -78,6 +78,51 @@ def build_index(vdb, args, device, rank, world):
     return idx, {"train_s": round(t1 - t0, 3), "add_s": round(t2 - t1, 3)}
 
 
+def build_index_sharded(vdb, args, device, rank, world):
+    """Sharded build for an index larger than one GPU (configs[3]: 100M x 768 = 307 GB).
+
+    The database is generated chunk by chunk (the same counter-based draws as one
+    whole-array generation). Pass 1 assigns every chunk (exact argmin, assign_to_lists,
+    ivf_flat_index.cpp:259-295) into a resident list-id array; the final list sizes give
+    the LPT plan (plan_shard); pass 2 regenerates each chunk and appends only the lists
+    this rank owns. `world` here is the number of shards (ranks, or --emulate-shard)."""
+    dim, n = args.dim, args.nvec
+    stream = torch.cuda.current_stream().cuda_stream
+    chunk = min(n, args.build_chunk)
+    data = torch.empty((chunk, dim), dtype=torch.float32, device=device)
+    ids = torch.empty(chunk, dtype=torch.int64, device=device)
+    asg = torch.empty(n, dtype=torch.int32, device=device)
+    idx = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, args.nlist, vdb.Metric.L2, device=device.index))
+    t0 = time.perf_counter()
+    ntrain = min(args.train, n)
+    vdb.gen_normal_device(data.data_ptr(), ntrain * dim, seed=12345, offset=0, stream=stream)
+    torch.cuda.synchronize()
+    idx.train_device(data.data_ptr(), ntrain)
+    t1 = time.perf_counter()
+    for a in range(0, n, chunk):
+        m = min(chunk, n - a)
+        vdb.gen_normal_device(data.data_ptr(), m * dim, seed=12345, offset=a * dim, stream=stream)
+        torch.cuda.synchronize()
+        idx.assign_device(data.data_ptr(), m, asg[a:].data_ptr())
+        log(rank, f"[bench] assigned {a + m} of {n} ({time.perf_counter() - t1:.1f}s)")
+    sizes = torch.bincount(asg, minlength=args.nlist).cpu().numpy().astype(np.uint64)
+    t2 = time.perf_counter()
+    idx.plan_shard(rank, world, sizes)
+    for a in range(0, n, chunk):
+        m = min(chunk, n - a)
+        vdb.gen_normal_device(data.data_ptr(), m * dim, seed=12345, offset=a * dim, stream=stream)
+        torch.arange(a, a + m, dtype=torch.int64, device=device, out=ids[:m])
+        torch.cuda.synchronize()
+        idx.add_to_lists_device(data.data_ptr(), ids.data_ptr(), asg[a:].data_ptr(), m)
+    t3 = time.perf_counter()
+    del data, ids, asg
+    torch.cuda.empty_cache()
+    log(rank, f"[bench] sharded build: train {t1 - t0:.2f}s assign {t2 - t1:.2f}s append {t3 - t2:.2f}s; "
+              f"shard {rank}/{world} {idx.get_gpu_memory_usage() / 2**30:.1f} GiB, largest list {int(sizes.max())}")
+    return idx, {"train_s": round(t1 - t0, 3), "assign_s": round(t2 - t1, 3), "append_s": round(t3 - t2, 3),
+                 "sharded_build": f"shard {rank} of {world}"}
+
+
 def cpu_baseline(vdb, idx, args, queries_host, budget_s):
     """Time the oracle (reference CPU path restatement) on a bounded query sample.
 
@@ -153,10 +198,20 @@ def main():
     ap.add_argument("--emulate-shard", type=int, default=0, metavar="W",
                     help="diagnostic: one process keeps rank 0's LPT shard of W and runs its partial search "
                          "(the per-GPU work of a W-GPU node, without the all-gather); not a bench line")
+    ap.add_argument("--cfg", choices=["cfg2", "cfg3", "cfg4"], default=None,
+                    help="BASELINE.json configs preset: cfg2 1M/256/16, cfg3 10M/4096/32 (default), "
+                         "cfg4 100M/16384/64 (sharded build; on one GPU only with --emulate-shard 8)")
+    ap.add_argument("--sharded-build", action="store_true",
+                    help="assign pass, then each rank stores only its LPT lists (an index larger than one GPU)")
+    ap.add_argument("--build-chunk", type=int, default=10_000_000, help="rows generated per build chunk")
     ap.add_argument("--prewarm", action="store_true", help="warm every list up front (list-cache tier)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning knob (vdb_ivf_set_option), e.g. wide_stride=1; results never change")
     args = ap.parse_args()
+    if args.cfg:
+        args.nvec, args.nlist, args.nprobe = {"cfg2": (1_000_000, 256, 16), "cfg3": (10_000_000, 4096, 32),
+                                              "cfg4": (100_000_000, 16384, 64)}[args.cfg]
+        args.sharded_build |= args.cfg == "cfg4"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.inflight <= 0:
@@ -179,13 +234,17 @@ def main():
 
 
 def run(vdb, args, device, rank, world):
-    idx, build_info = build_index(vdb, args, device, rank, world)
+    if args.sharded_build:
+        shards = world if world > 1 else max(args.emulate_shard, 1)
+        idx, build_info = build_index_sharded(vdb, args, device, rank if world > 1 else 0, shards)
+    else:
+        idx, build_info = build_index(vdb, args, device, rank, world)
     for o in args.opt:
         name, val = o.split("=", 1)
         idx.set_option(name, int(val))
     if args.prewarm:  # list-cache tier: load every list up front, in list order (vdb.QueryService/Warmup)
         idx.warmup_lists(list(range(args.nlist)))
-    if args.emulate_shard > 1 and world == 1:
+    if args.emulate_shard > 1 and world == 1 and not args.sharded_build:
         idx.set_shard(0, args.emulate_shard)
     B, k = args.batch, args.k
     nq = (args.warmup + args.steps + args.prof_steps) * B
@@ -195,7 +254,7 @@ def run(vdb, args, device, rank, world):
     out_d = torch.empty((nq, k), dtype=torch.float32, device=device)
     out_i = torch.empty((nq, k), dtype=torch.int64, device=device)
     check = None
-    if world > 1:
+    if world > 1 and not args.sharded_build:
         # Reference for the end-to-end check: the whole (unsharded) index answers the
         # first timed batches on this rank before it keeps only its LPT shard.
         nchk = min(args.check_batches, args.steps) * B

@@ -102,6 +102,9 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_search": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp]),
         "vdb_ivf_search_device": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp, vp]),
         "vdb_ivf_set_shard": (ctypes.c_int, [vp, u32, u32]),
+        "vdb_ivf_plan_shard": (ctypes.c_int, [vp, u32, u32, vp]),
+        "vdb_ivf_assign_device": (ctypes.c_int, [vp, vp, u64, vp]),
+        "vdb_ivf_add_to_lists_device": (ctypes.c_int, [vp, vp, vp, vp, u64]),
         "vdb_ivf_save": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "vdb_ivf_load": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "vdb_merge_ranks_device": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp, vp]),
@@ -248,6 +251,14 @@ class IVFFlatIndex:
     def add_device(self, vec_ptr: int, ids_ptr: int, n: int):
         _check(lib().vdb_ivf_add_device(self._h, ctypes.c_void_p(vec_ptr), ctypes.c_void_p(ids_ptr), n))
 
+    def assign_device(self, vec_ptr: int, n: int, lists_ptr: int):
+        """Exact nearest-centroid list of n device rows into u32 lists_ptr (assign_to_lists, cpp:259-295)."""
+        _check(lib().vdb_ivf_assign_device(self._h, ctypes.c_void_p(vec_ptr), n, ctypes.c_void_p(lists_ptr)))
+
+    def add_to_lists_device(self, vec_ptr: int, ids_ptr: int, lists_ptr: int, n: int):
+        _check(lib().vdb_ivf_add_to_lists_device(self._h, ctypes.c_void_p(vec_ptr), ctypes.c_void_p(ids_ptr),
+                                                 ctypes.c_void_p(lists_ptr), n))
+
     @property
     def centroids(self) -> np.ndarray:
         out = np.empty((self.config.nlist, self.dimension), dtype=np.float32)
@@ -297,6 +308,13 @@ class IVFFlatIndex:
     # ---- sharding ----
     def set_shard(self, rank: int, world: int):
         _check(lib().vdb_ivf_set_shard(self._h, rank, world))
+
+    def plan_shard(self, rank: int, world: int, final_sizes):
+        """Sharded build: fix this rank's lists from the final list sizes before any add."""
+        s = np.ascontiguousarray(final_sizes, dtype=np.uint64)
+        if len(s) != self.config.nlist:
+            raise ValueError("final_sizes needs one entry per list")
+        _check(lib().vdb_ivf_plan_shard(self._h, rank, world, _ptr(s)))
 
     # ---- residency / stats ----
     def warmup_lists(self, list_ids):

@@ -901,6 +901,23 @@ struct vdb_ivf {
         upload_directory();
     }
 
+    // Sharded build, for an index larger than one GPU (100M x 768 = 307 GB): the final
+    // list sizes (from an assignment pass) fix this handle's lists before any add, so
+    // appends store only the owned lists' rows and count the rest. The plan is the same
+    // LPT as set_shard, so a later set_shard(r, w) keeps the same lists.
+    void plan_shard(uint32_t r, uint32_t w, const uint64_t* final_sizes) {
+        require(total == 0, "plan_shard needs an empty index (call it between train and add)", VDB_ERR_STATE);
+        require(!file_home(), "lists are served from a file (vdb_ivf_open_lists)", VDB_ERR_STATE);
+        std::vector<uint32_t> owner(nlist);
+        vdb_shard_plan(final_sizes, nlist, w, owner.data());
+        std::vector<uint8_t> new_owned(nlist);
+        for (uint32_t l = 0; l < nlist; ++l) new_owned[l] = owner[l] == r;
+        relayout(count, new_owned);
+        rank = r;
+        world = w;
+        upload_directory();
+    }
+
     EventSet& next_events() {
         if (events_used == events.size()) {
             EventSet e;
@@ -1209,6 +1226,45 @@ int vdb_ivf_add_to_lists(vdb_ivf* h, const float* v, const uint64_t* ids, const 
         HIPCHECK(hipMemcpyAsync(dl.ensure(n), lists, n * 4, hipMemcpyHostToDevice, h->stream));
         h->append(h->padded_rows(dv.p, n, tmp), di.p, dl.p, n);
         HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int vdb_ivf_assign_device(vdb_ivf* h, const float* d_v, uint64_t n, uint32_t* d_lists) {
+    return guarded([&] {
+        require(h && ((d_v && d_lists) || n == 0), "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        if (n == 0) return;
+        DevBuf<float> tmp;
+        h->assign(h->padded_rows(d_v, n, tmp), n, d_lists);
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int vdb_ivf_add_to_lists_device(vdb_ivf* h, const float* d_v, const uint64_t* d_ids, const uint32_t* d_lists,
+                                uint64_t n) {
+    return guarded([&] {
+        require(h && ((d_v && d_ids && d_lists) || n == 0), "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        if (n == 0) return;
+        // The grouping kernels index per-list arrays by these ids: check them first.
+        std::vector<uint32_t> hl(n);
+        HIPCHECK(hipMemcpyAsync(hl.data(), d_lists, n * 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHECK(hipStreamSynchronize(h->stream));
+        for (uint64_t i = 0; i < n; ++i) require(hl[i] < h->nlist, "list id out of range");
+        DevBuf<float> tmp;
+        h->append(h->padded_rows(d_v, n, tmp), d_ids, d_lists, n);
+        HIPCHECK(hipStreamSynchronize(h->stream));
+    });
+}
+
+int vdb_ivf_plan_shard(vdb_ivf* h, uint32_t rank, uint32_t world, const uint64_t* final_sizes) {
+    return guarded([&] {
+        require(h && final_sizes && world > 0 && rank < world, "invalid shard");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        h->plan_shard(rank, world, final_sizes);
     });
 }
 

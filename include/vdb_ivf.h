@@ -100,6 +100,12 @@ int vdb_ivf_add_device(vdb_ivf* index, const float* d_vectors, const uint64_t* d
  * Used by vdb_ivf_load and for indexes whose assignment was computed elsewhere. */
 int vdb_ivf_add_to_lists(vdb_ivf* index, const float* vectors, const uint64_t* ids, const uint32_t* lists,
                          uint64_t n);
+/* Exact assignment only (assign_to_lists, engine/ivf_flat_index.cpp:259-295): one list id
+ * per row into a device array, nothing stored. With add_to_lists_device it splits `add`
+ * (cpp:148-202) into two passes, so a sharded build can learn the final list sizes first. */
+int vdb_ivf_assign_device(vdb_ivf* index, const float* d_vectors, uint64_t n, uint32_t* d_lists);
+int vdb_ivf_add_to_lists_device(vdb_ivf* index, const float* d_vectors, const uint64_t* d_ids,
+                                const uint32_t* d_lists, uint64_t n);
 /* Persist / restore centroids and lists (IVFFlatIndex::save/load, engine/ivf_flat_index.h:66-67,
  * declared but never defined in the reference; this engine's own file format). */
 int vdb_ivf_save(vdb_ivf* index, const char* path);
@@ -121,6 +127,10 @@ int vdb_ivf_search_device(vdb_ivf* index, const float* d_queries, uint32_t n, ui
  * (size-balanced LPT over list lengths, identical on every rank), and free the
  * rest of the list arena. Emptiness of non-owned lists is still tracked. */
 int vdb_ivf_set_shard(vdb_ivf* index, uint32_t rank, uint32_t world);
+/* Sharded build of an index larger than one GPU (100M x 768 over 8 GPUs): on an empty,
+ * trained index, fix this rank's lists from the final list sizes (the same LPT plan as
+ * set_shard); later adds store only those lists' rows and count the others. */
+int vdb_ivf_plan_shard(vdb_ivf* index, uint32_t rank, uint32_t world, const uint64_t* final_sizes);
 /* Combine per-rank partials gathered as [nranks][n][k] into final [n][k]. */
 int vdb_merge_ranks_device(const float* d_dist, const uint64_t* d_ids, uint32_t nranks, uint32_t n,
                            uint32_t k, float* d_out_dist, uint64_t* d_out_ids, void* stream);

@@ -265,6 +265,55 @@ def test_two_shards_merge_equals_single():
     assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), Dr, Ir)
 
 
+def test_sharded_build_equals_single():
+    """cfg4 flow (an index larger than one GPU): assign pass -> final sizes -> plan_shard ->
+    add_to_lists in chunks; each rank holds only its lists, the merge equals the oracle."""
+    import torch
+    dev = torch.device("cuda:0")
+    X, Q, ids = oracle.reference_test_data(9000, 40, 48, seed=6)
+    o = oracle.OracleIndex(48, 24, 0)
+    o.train(X[:3000])
+    o.add(X, ids)
+    Dr, Ir = o.search(Q, 7, 10)
+    Xd = torch.from_numpy(X).to(dev)
+    idd = torch.from_numpy(ids.view(np.int64)).to(dev)
+    chunks = [(0, 4000), (4000, 4001), (4001, 9000)]
+    world, parts = 3, []
+    for r in range(world):
+        g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(48, 24, vdb.Metric.L2))
+        g.train(X[:3000])
+        asg = torch.empty(9000, dtype=torch.int32, device=dev)
+        for a, b in chunks:  # pass 1: assignment only
+            g.assign_device(Xd[a:].data_ptr(), b - a, asg[a:].data_ptr())
+        torch.cuda.synchronize()
+        sizes = np.bincount(asg.cpu().numpy(), minlength=24).astype(np.uint64)
+        assert np.array_equal(sizes, np.array([len(o.get_list(l)[1]) for l in range(24)], np.uint64))
+        g.plan_shard(r, world, sizes)
+        for a, b in chunks:  # pass 2: store this rank's lists only
+            g.add_to_lists_device(Xd[a:].data_ptr(), idd[a:].data_ptr(), asg[a:].data_ptr(), b - a)
+        assert np.array_equal(g.list_sizes(), sizes) and g.get_total_vectors() == 9000
+        owner = vdb.shard_plan(sizes, world)
+        for l in range(24):
+            if owner[l] == r and sizes[l]:
+                gv, gi = g.get_list(l)
+                ov, oi = o.get_list(l)
+                assert np.array_equal(gi, oi) and np.array_equal(bits(gv), bits(ov))
+        D, I = g.search(Q, nprobe=7, k=10)
+        Do, Io = o.search_shard(Q, 7, 10, (owner == r).astype(np.uint8))
+        assert_same(D, I, Do, Io)
+        parts.append((D, I))
+        with pytest.raises(vdb.VdbError):
+            g.plan_shard(r, world, sizes)  # only on an empty index
+    pd = torch.from_numpy(np.stack([p[0] for p in parts])).to(dev)
+    pi = torch.from_numpy(np.stack([p[1] for p in parts]).view(np.int64)).to(dev)
+    od = torch.empty((40, 10), dtype=torch.float32, device=dev)
+    oi = torch.empty((40, 10), dtype=torch.int64, device=dev)
+    vdb.merge_ranks_device(pd.data_ptr(), pi.data_ptr(), world, 40, 10, od.data_ptr(), oi.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), Dr, Ir)
+
+
 @pytest.mark.parametrize("seg", [0, 64, 512])
 @pytest.mark.parametrize("k", [10, 64, 65])
 def test_hub_lists_wide_items(k, seg):
