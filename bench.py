@@ -167,6 +167,38 @@ def cpu_baseline(vdb, idx, args, queries_host, budget_s):
     }
 
 
+def shard_parity(vdb, idx, args, queries_host, rank, world):
+    """Parity of one shard at full size: the oracle's shard search (oracle_search_shard:
+    owned probed lists scanned, the others kept as counts for the empty-list rule,
+    ivf_flat_index.cpp:225) against this handle's partial results for the same call."""
+    sys.path.insert(0, ROOT)
+    import oracle  # test infrastructure: the checker only
+
+    o = oracle.OracleIndex(args.dim, args.nlist, 0)
+    o.centroids = idx.centroids
+    sample = queries_host[: args.shard_check]
+    sizes = idx.list_sizes()
+    owned = vdb.shard_plan(sizes, world) == rank
+    probed = set()
+    for q in sample:
+        probed.update(o.select_nprobe(q, args.nprobe).tolist())
+    loaded = 0
+    for l in range(args.nlist):
+        if owned[l] and l in probed and sizes[l]:
+            v, i = o.list_buffers(l, int(sizes[l]))
+            idx.get_list_into(l, v, i)
+            loaded += int(sizes[l])
+        else:
+            o.set_list_count(l, int(sizes[l]))
+    t0 = time.perf_counter()
+    D, I = o.search_shard(sample, args.nprobe, args.k, owned.astype(np.uint8))
+    t_cpu = time.perf_counter() - t0
+    Dg, Ig = idx.search(sample, nprobe=args.nprobe, k=args.k)
+    same = bool(np.array_equal(I, Ig) and np.array_equal(D.view(np.uint32), Dg.view(np.uint32)))
+    return {"queries": len(sample), "shard": f"{rank} of {world}", "vectors_exported": loaded,
+            "oracle_s": round(t_cpu, 2), "bit_identical": same}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -204,6 +236,8 @@ def main():
     ap.add_argument("--sharded-build", action="store_true",
                     help="assign pass, then each rank stores only its LPT lists (an index larger than one GPU)")
     ap.add_argument("--build-chunk", type=int, default=10_000_000, help="rows generated per build chunk")
+    ap.add_argument("--shard-check", type=int, default=0, metavar="Q",
+                    help="with --emulate-shard: check Q queries of this shard bit for bit against the oracle")
     ap.add_argument("--prewarm", action="store_true", help="warm every list up front (list-cache tier)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning knob (vdb_ivf_set_option), e.g. wide_stride=1; results never change")
@@ -425,6 +459,9 @@ def run(vdb, args, device, rank, world):
     if world == 1 and rank == 0 and not args.no_cpu and args.emulate_shard <= 1:
         qh = queries[: args.cpu_queries].cpu().numpy()
         result["cpu_baseline"] = cpu_baseline(vdb, idx, args, qh, args.cpu_budget)
+    if world == 1 and args.emulate_shard > 1 and args.shard_check > 0:
+        qh = queries[: args.shard_check].cpu().numpy()
+        result["shard_parity"] = shard_parity(vdb, idx, args, qh, 0, args.emulate_shard)
     if rank == 0:
         print(json.dumps(result), flush=True)
 

@@ -62,6 +62,7 @@ def lib():
             "oracle_get_list": (None, [vp, ctypes.c_uint32, _f32p, _u64p]),
             "oracle_set_list": (None, [vp, ctypes.c_uint32, _f32p, _u64p, ctypes.c_uint64]),
             "oracle_total_vectors": (ctypes.c_uint64, [vp]),
+            "oracle_list_set_count": (None, [vp, ctypes.c_uint32, ctypes.c_uint64]),
             "oracle_list_resize": (None, [vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(_f32p), ctypes.POINTER(_u64p)]),
             "oracle_gen_normal": (None, [ctypes.c_uint32, ctypes.c_uint64, _f32p]),
         }
@@ -176,6 +177,10 @@ class OracleIndex:
         v = np.ascontiguousarray(vectors, dtype=np.float32).reshape(-1, self.dim)
         i = np.ascontiguousarray(ids, dtype=np.uint64)
         lib().oracle_set_list(self._h, l, _p(v, _f32p), _p(i, _u64p), v.shape[0])
+
+    def set_list_count(self, l: int, count: int):
+        """List l is stored on another shard: keep its count (emptiness) and no rows."""
+        lib().oracle_list_set_count(self._h, l, count)
 
     def list_buffers(self, l: int, count: int):
         """Resize list l to `count` vectors and return writable numpy views of its

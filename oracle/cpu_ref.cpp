@@ -14,6 +14,8 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <random>
@@ -105,6 +107,10 @@ struct oracle_ivf {
     // search_list_cpu, cpp:339-384, with k already min(k, count) as search passes it.
     void scan_list(uint32_t l, const float* q, uint32_t k, std::vector<Cand>& out) const {
         const List& L = lists[l];
+        if (L.ids.size() != L.count) {  // a count-only list (oracle_list_set_count) has no rows to scan
+            std::fprintf(stderr, "oracle: list %u holds no rows (count-only)\n", l);
+            std::abort();
+        }
         std::vector<Cand> cand;
         cand.reserve(L.count);
         for (uint64_t i = 0; i < L.count; ++i)
@@ -380,6 +386,16 @@ void oracle_list_resize(oracle_ivf* h, uint32_t l, uint64_t count, float** vecto
     L.ids.resize(count);
     *vectors = L.vectors.data();
     *ids = L.ids.data();
+}
+
+void oracle_list_set_count(oracle_ivf* h, uint32_t l, uint64_t count) {
+    // A list stored on another shard: only its emptiness is read (the empty-list skip,
+    // cpp:225), so keep its count and no rows; oracle_search_shard never scans it.
+    List& L = h->lists[l];
+    h->total = h->total - L.count + count;
+    L.count = count;
+    std::vector<float>().swap(L.vectors);
+    std::vector<uint64_t>().swap(L.ids);
 }
 
 uint64_t oracle_total_vectors(oracle_ivf* h) { return h->total; }

@@ -61,6 +61,8 @@ void oracle_get_list(oracle_ivf* h, uint32_t list, float* vectors, uint64_t* ids
 void oracle_set_list(oracle_ivf* h, uint32_t list, const float* vectors, const uint64_t* ids,
                      uint64_t count);
 /* Resize list storage and hand back pointers so a caller can fill it in place. */
+/* Count-only list (stored on another shard): emptiness is kept, no rows. */
+void oracle_list_set_count(oracle_ivf* h, uint32_t list, uint64_t count);
 void oracle_list_resize(oracle_ivf* h, uint32_t list, uint64_t count, float** vectors,
                         uint64_t** ids);
 uint64_t oracle_total_vectors(oracle_ivf* h);

@@ -140,6 +140,29 @@ def test_shard_decomposition(world):
     assert np.array_equal(Im, I) and np.array_equal(bits(Dm), bits(D))
 
 
+def test_count_only_lists_keep_shard_results():
+    """bench.py --shard-check: lists of other shards kept as counts only (no rows) give the
+    same shard partials as fully stored lists, empty lists (stale slots) included."""
+    X, Q, ids = oracle.reference_test_data(3000, 30, 16, seed=9)
+    o = oracle.OracleIndex(16, 40, 0)
+    o.centroids = np.concatenate([X[:32], np.full((8, 16), 50.0, np.float32)])  # 8 empty lists
+    o.add(X, ids)
+    owned = (np.arange(40) % 3 == 0).astype(np.uint8)
+    D, I = o.search_shard(Q, 36, 10, owned)
+    c = oracle.OracleIndex(16, 40, 0)
+    c.centroids = o.centroids
+    for l in range(40):
+        v, i = o.get_list(l)
+        if owned[l]:
+            bv, bi = c.list_buffers(l, len(i))
+            bv[...] = v
+            bi[...] = i
+        else:
+            c.set_list_count(l, len(i))
+    Dc, Ic = c.search_shard(Q, 36, 10, owned)
+    assert np.array_equal(Ic, I) and np.array_equal(bits(Dc), bits(D))
+
+
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))), ids=os.path.basename)
 def test_golden_fixture(path):
     f = np.load(path)
