@@ -181,7 +181,8 @@ struct vdb_ivf {
     uint32_t seg_blocks = 8;  // current segment size (blocks of 64 vectors; upload_directory sets it)
     uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)
     uint32_t diag = 0;                          // scan diagnostics (results invalid when set)
-    uint32_t segs_item_opt = 0;   // segments per wide item (0 = 4: one per wave, taken dynamically)
+    uint32_t segs_item_opt = 0;   // segments per wide item (0: one per wave, taken dynamically)
+    uint32_t wide_group = 16;     // queries per wide item at most: 16 (4-wave workgroups) or 32 (8-wave)
     bool fused_scan = true;       // narrow items inside the wide scan's grid (option fused_scan; +2-3 %)
     uint32_t narrow_blocks = 64;  // persistent narrow-scan workgroups beside the wide scan (1/8 shard: +1.5 % vs 512)
 
@@ -1003,9 +1004,11 @@ struct vdb_ivf {
         }
         const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
         const uint64_t max_wide = max_items / 4 + BP + 1;
-        const bool wide = regs_k == 1 && wide_scan && vdbk::scan_wide_fits(d4, k);
-        const uint32_t segs_item = segs_item_opt ? segs_item_opt : 4u;  // 8+ adds tail latency, no throughput
-        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? 1 : 0, segs_item, w.items.p, w.items_w.p,
+        const int waves = wide_group == 32 ? 8 : 4;  // workgroup shape of the wide scan
+        const bool wide = regs_k == 1 && wide_scan && vdbk::scan_wide_fits(d4, k, waves);
+        // segments per item: one per wave (more adds tail latency, no throughput)
+        const uint32_t segs_item = segs_item_opt ? segs_item_opt : (uint32_t)waves;
+        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? (int)wide_group : 0, segs_item, w.items.p, w.items_w.p,
                           w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
         vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
@@ -1013,8 +1016,10 @@ struct vdb_ivf {
                                 wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item, 0};
         if (wide && fused_scan) {
             // one persistent grid takes both queues (no side stream, no fork/join)
-            sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks, vdbk::kPersistentBlocks / 2));
-            vdbk::launch_scan_wide(metric, (uint32_t)std::max<uint64_t>(max_wide, (max_items + 3) / 4), sa, s);
+            // (narrow_blocks counts 4-wave workgroups: as many waves start on the narrow queue)
+            const uint32_t grid_cap = waves == 8 ? vdbk::kPersistentBlocks / 2 : vdbk::kPersistentBlocks;
+            sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks * 4 / waves, grid_cap / 2));
+            vdbk::launch_scan_wide(metric, (uint32_t)std::max<uint64_t>(max_wide, (max_items + 3) / 4), sa, s, waves);
         } else if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));
@@ -1022,7 +1027,7 @@ struct vdb_ivf {
             vdbk::launch_scan_narrow(metric, regs_k, std::min<uint32_t>((uint32_t)((max_items + 3) / 4), narrow_blocks), sa,
                                      w.side);
             HIPCHECK(hipEventRecord(w.join, w.side));
-            vdbk::launch_scan_wide(metric, (uint32_t)max_wide, sa, s);
+            vdbk::launch_scan_wide(metric, (uint32_t)max_wide, sa, s, waves);
             HIPCHECK(hipStreamWaitEvent(s, w.join, 0));
         } else {
             vdbk::launch_scan_narrow(metric, regs_k, (uint32_t)((max_items + 3) / 4), sa, s);
@@ -1550,6 +1555,9 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "segs_per_item") {
             require(value == 0 || (value >= 4 && value <= 64), "segs_per_item is 0 (auto) or 4..64");
             h->segs_item_opt = (uint32_t)value;
+        } else if (n == "wide_group") {
+            require(value == 16 || value == 32, "wide_group is 16 or 32");
+            h->wide_group = (uint32_t)value;
         } else if (n == "fused_scan") {
             h->fused_scan = value != 0;
         } else if (n == "narrow_blocks") {

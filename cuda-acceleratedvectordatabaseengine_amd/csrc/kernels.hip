@@ -651,15 +651,16 @@ __device__ uint32_t plan_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
 
 // Query groups of one list with m (query, probe) pairs and ns segments. A list of at
 // least kWideMinSeg segments (with top-k in one register) is scanned by wide items:
-// ceil(m / kWideGroup) balanced groups x ceil(ns / segs_item) segment ranges, so each list is
-// read ceil(m / 16) times per batch. Other lists: narrow items of <= gn pairs x ns.
+// ceil(m / wg) balanced groups x ceil(ns / segs_item) segment ranges, so each list is
+// read ceil(m / wg) times per batch (wg = 16, or 32 with 8-wave workgroups; 0 = no wide
+// items). Other lists: narrow items of <= gn pairs x ns.
 struct ListGroups {
     uint32_t wide, narrow;
 };
-__device__ __forceinline__ ListGroups list_groups(uint32_t m, uint32_t ns, uint32_t gn, bool wide) {
+__device__ __forceinline__ ListGroups list_groups(uint32_t m, uint32_t ns, uint32_t gn, uint32_t wg) {
     ListGroups g;
-    if (wide && ns >= (uint32_t)kWideMinSeg) {
-        g.wide = (m + kWideGroup - 1) / kWideGroup;
+    if (wg && ns >= (uint32_t)kWideMinSeg) {
+        g.wide = (m + wg - 1) / wg;
         g.narrow = 0;
     } else {
         g.wide = 0;
@@ -701,7 +702,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     __shared__ uint32_t s_nvalid;
     const uint32_t tid = threadIdx.x;
     const uint32_t BP = B * P;
-    const bool wide = wide_on != 0;
+    const uint32_t wide = wide_on;  // wide group size (0: no wide items)
 
     if (tid == 0) s_nvalid = 0;
     for (uint32_t i = tid; i < NP; i += blockDim.x) {
@@ -1027,6 +1028,11 @@ __device__ __forceinline__ f2 dist_term2(f2 acc, f2 q, f2 x) {
 // like the scalar ops); every query's sum still runs in d order. Per query only the
 // k-th distance lives in registers; the top-k lists live in LDS (tk_d / tk_i), and
 // the insertion code exists once, looping over the queries that have candidates.
+#ifndef VDB_BIG_GROUP_PREFETCH
+#define VDB_BIG_GROUP_PREFETCH 0  // 1 spills ~100 VGPRs in the 16-pair instantiation (measured with -Rpass-analysis)
+#endif
+constexpr bool kBigGroupPrefetch = VDB_BIG_GROUP_PREFETCH != 0;
+
 template <int GP, int M>
 __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds, float* tk_d,
                                                uint64_t* tk_i, const uint32_t seg) {
@@ -1057,24 +1063,41 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
     // tile, the pairs at immediate offsets. Each pair's registers are refilled with
     // the next tile's pair as soon as they are consumed, so every LDS read has a whole
     // tile of arithmetic to land in.
-    float4 qb[GP][2];
-    {
+    // More than 8 pairs: the register copy of a tile's pairs takes 4·GP float4, so either
+    // fewer list tiles stay in flight (kBigGroupPrefetch) or each pair is read from LDS
+    // where it is used.
+    constexpr bool kDirect = GP > 8 && !kBigGroupPrefetch;
+    constexpr int QB = kDirect ? 1 : GP;
+    float4 qb[QB][2];
+    if constexpr (!kDirect) {
         const float4* src = qlds;
 #pragma unroll
         for (int p = 0; p < GP; ++p) qb[p][0] = src[2 * p], qb[p][1] = src[2 * p + 1];
     }
     auto compute = [&](const float4 x, uint32_t t, auto) {
-        const float4* nxt = qlds + (size_t)(t + 1 == d4 ? 0 : t + 1) * GP * 2;
         const f2 xlo = {x.x, x.y}, xhi = {x.z, x.w};
+        if constexpr (kDirect) {
+            const float4* cur = qlds + (size_t)t * GP * 2;
 #pragma unroll
-        for (int p = 0; p < GP; ++p) {
-            const float4 lo = qb[p][0], hi = qb[p][1];
-            acc[p] = dist_term2<M, 0>(acc[p], f2{lo.x, lo.y}, xlo);
-            acc[p] = dist_term2<M, 1>(acc[p], f2{lo.z, lo.w}, xlo);
-            acc[p] = dist_term2<M, 0>(acc[p], f2{hi.x, hi.y}, xhi);
-            acc[p] = dist_term2<M, 1>(acc[p], f2{hi.z, hi.w}, xhi);
-            qb[p][0] = nxt[2 * p];
-            qb[p][1] = nxt[2 * p + 1];
+            for (int p = 0; p < GP; ++p) {
+                const float4 lo = cur[2 * p], hi = cur[2 * p + 1];
+                acc[p] = dist_term2<M, 0>(acc[p], f2{lo.x, lo.y}, xlo);
+                acc[p] = dist_term2<M, 1>(acc[p], f2{lo.z, lo.w}, xlo);
+                acc[p] = dist_term2<M, 0>(acc[p], f2{hi.x, hi.y}, xhi);
+                acc[p] = dist_term2<M, 1>(acc[p], f2{hi.z, hi.w}, xhi);
+            }
+        } else {
+            const float4* nxt = qlds + (size_t)(t + 1 == d4 ? 0 : t + 1) * GP * 2;
+#pragma unroll
+            for (int p = 0; p < GP; ++p) {
+                const float4 lo = qb[p][0], hi = qb[p][1];
+                acc[p] = dist_term2<M, 0>(acc[p], f2{lo.x, lo.y}, xlo);
+                acc[p] = dist_term2<M, 1>(acc[p], f2{lo.z, lo.w}, xlo);
+                acc[p] = dist_term2<M, 0>(acc[p], f2{hi.x, hi.y}, xhi);
+                acc[p] = dist_term2<M, 1>(acc[p], f2{hi.z, hi.w}, xhi);
+                qb[p][0] = nxt[2 * p];
+                qb[p][1] = nxt[2 * p + 1];
+            }
         }
     };
     auto finish = [&](uint32_t j, uint64_t id) {
@@ -1119,7 +1142,9 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
 #pragma unroll
         for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
     };
-    stream_blocks<kTilePipe>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
+    // more than 8 pairs: fewer tiles in flight (the pairs' query registers take the rest)
+    constexpr int T = GP <= 8 ? kTilePipe : (kBigGroupPrefetch ? kTilePipe / 4 : kTilePipe / 2);
+    stream_blocks<T>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
     for (int g = 0; g < np; ++g) {
         const uint32_t part = a.part_base_sorted[it.pair_start + g] + seg;
         if (lane < k) {
@@ -1173,17 +1198,20 @@ __device__ __forceinline__ void drain_narrow(const ScanArgs& a) {
     }
 }
 
-// ivf_scan_wide: the large lists. Workgroup b takes wide item b: 4 consecutive
-// segments (one per wave) x up to 16 of the list's queries, staged once in LDS.
-template <int M>
-__global__ __launch_bounds__(256, 2) void ivf_scan_wide(ScanArgs a) {
+// ivf_scan_wide: the large lists. W = 4: two 4-wave workgroups per CU, items of up to
+// 16 queries; W = 8: one 8-wave workgroup per CU, items of up to 32 queries (half the
+// re-reads of lists probed by many queries, twice the VALU work per byte). A workgroup
+// takes one wide item at a time: its segments x its queries, staged once in LDS.
+template <int M, int W>
+__global__ __launch_bounds__(64 * W, W == 4 ? 2 : 1) void ivf_scan_wide(ScanArgs a) {
+    constexpr int GW = 4 * W;  // queries per item at most
     // Dynamic LDS: [d4][gpv][2] float4 of staged query pairs (tile-major), then per wave
-    // kWideGroup x k top-k ids (u64), then the same for distances (f32).
+    // GW x k top-k ids (u64), then the same for distances (f32).
     extern __shared__ __attribute__((aligned(16))) float4 qlds[];
     const uint32_t d4 = a.d4;
-    uint64_t* tk_i = (uint64_t*)(qlds + (size_t)(kWideGroup / 2) * d4 * 2) + (size_t)wave_index() * kWideGroup * a.k;
-    float* tk_d = (float*)((uint64_t*)(qlds + (size_t)(kWideGroup / 2) * d4 * 2) + (size_t)4 * kWideGroup * a.k) +
-                  (size_t)wave_index() * kWideGroup * a.k;
+    uint64_t* tk_i = (uint64_t*)(qlds + (size_t)(GW / 2) * d4 * 2) + (size_t)wave_index() * GW * a.k;
+    float* tk_d = (float*)((uint64_t*)(qlds + (size_t)(GW / 2) * d4 * 2) + (size_t)W * GW * a.k) +
+                  (size_t)wave_index() * GW * a.k;
     const uint32_t n_wide = a.counters[3];
     // Items of one list are adjacent in the plan; dispatching them in a strided order
     // mixes lists of many queries (VALU-heavy) with lists of few (HBM-heavy) on the
@@ -1208,7 +1236,7 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_wide(ScanArgs a) {
         const int np = (int)it.npairs;
         const int gp = (np + 1) / 2;
         if (threadIdx.x == 0) s_seg = 0;  // visible after the staging barrier below
-        const int gpv = (a.diag & 2) ? 1 : gp;  // every pair count 1..8 has its own instantiation
+        const int gpv = (a.diag & 2) ? 1 : gp;  // every pair count 1..GW/2 has its own instantiation
                                                 // (DIAGNOSTIC diag&2: one pair only, results invalid)
         for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
             const uint32_t t = e / gpv, p = e - t * gpv;
@@ -1237,7 +1265,21 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_wide(ScanArgs a) {
                 case 5: scan_wide_wave<5, M>(a, it, qlds, tk_d, tk_i, sg); break;
                 case 6: scan_wide_wave<6, M>(a, it, qlds, tk_d, tk_i, sg); break;
                 case 7: scan_wide_wave<7, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                default: scan_wide_wave<8, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                case 8: scan_wide_wave<8, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                default:
+                    if constexpr (W == 8) {
+                        switch (gpv) {
+                            case 9: scan_wide_wave<9, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                            case 10: scan_wide_wave<10, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                            case 11: scan_wide_wave<11, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                            case 12: scan_wide_wave<12, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                            case 13: scan_wide_wave<13, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                            case 14: scan_wide_wave<14, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                            case 15: scan_wide_wave<15, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                            default: scan_wide_wave<16, M>(a, it, qlds, tk_d, tk_i, sg); break;
+                        }
+                    }
+                    break;
             }
         }
         __syncthreads();  // qlds is restaged by the next wide item
@@ -1888,7 +1930,7 @@ void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint3
                  uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats, hipStream_t s) {
     uint32_t np = 1;
     while (np < B * P) np <<= 1;
-    ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, wide ? 1u : 0u, segs_item, items,
+    ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, (uint32_t)wide, segs_item, items,
                                        items_w, counters, sorted_pair, part_base_sorted, part_base_qp, nseg_qp,
                                        l1base_qp, l1_items, stats);
 }
@@ -1914,11 +1956,14 @@ void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes
 
 static constexpr size_t kWideStaticLds = 64;  // ivf_scan_wide's static LDS (the queue slot), rounded up
 
-size_t scan_wide_lds(uint32_t d4, uint32_t k) {
-    return (size_t)(kWideGroup / 2) * d4 * 2 * sizeof(float4) + (size_t)4 * kWideGroup * k * (sizeof(float) + sizeof(uint64_t));
+size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves) {
+    const size_t gw = 4 * (size_t)waves;
+    return (gw / 2) * d4 * 2 * sizeof(float4) + (size_t)waves * gw * k * (sizeof(float) + sizeof(uint64_t));
 }
 
-bool scan_wide_fits(uint32_t d4, uint32_t k) { return k <= 64 && scan_wide_lds(d4, k) <= kLdsBytes - kWideStaticLds; }
+bool scan_wide_fits(uint32_t d4, uint32_t k, int waves) {
+    return k <= 64 && scan_wide_lds(d4, k, waves) <= kLdsBytes - kWideStaticLds;
+}
 
 void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
     if (!grid_blocks) return;
@@ -1939,23 +1984,31 @@ void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanAr
 #undef VDB_SN
 }
 
-void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
+void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves) {
     if (!grid_blocks) return;
     static const bool raised = [] {
-        // wide items stage up to 16 queries in LDS: allow the whole 160 KB of a CU
+        // wide items stage up to 16 (32) queries in LDS: allow the whole 160 KB of a CU
         const int dyn = (int)(kLdsBytes - kWideStaticLds);
-        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kL2>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kIP>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-        (void)hipFuncSetAttribute((const void*)ivf_scan_wide<kCos>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+        const void* fns[] = {(const void*)ivf_scan_wide<kL2, 4>, (const void*)ivf_scan_wide<kIP, 4>,
+                             (const void*)ivf_scan_wide<kCos, 4>, (const void*)ivf_scan_wide<kL2, 8>,
+                             (const void*)ivf_scan_wide<kIP, 8>, (const void*)ivf_scan_wide<kCos, 8>};
+        for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
         (void)hipGetLastError();
         return true;
     }();
     (void)raised;
-    const size_t lds = scan_wide_lds(a.d4, a.k);
+    const size_t lds = scan_wide_lds(a.d4, a.k, waves);
+    if (waves == 8) {  // one 8-wave workgroup per CU
+        const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks / 2);
+        if (metric == kL2) ivf_scan_wide<kL2, 8><<<g, 512, lds, s>>>(a);
+        else if (metric == kIP) ivf_scan_wide<kIP, 8><<<g, 512, lds, s>>>(a);
+        else ivf_scan_wide<kCos, 8><<<g, 512, lds, s>>>(a);
+        return;
+    }
     const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
-    if (metric == kL2) ivf_scan_wide<kL2><<<g, 256, lds, s>>>(a);
-    else if (metric == kIP) ivf_scan_wide<kIP><<<g, 256, lds, s>>>(a);
-    else ivf_scan_wide<kCos><<<g, 256, lds, s>>>(a);
+    if (metric == kL2) ivf_scan_wide<kL2, 4><<<g, 256, lds, s>>>(a);
+    else if (metric == kIP) ivf_scan_wide<kIP, 4><<<g, 256, lds, s>>>(a);
+    else ivf_scan_wide<kCos, 4><<<g, 256, lds, s>>>(a);
 }
 
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const uint32_t* nseg_qp,

@@ -100,10 +100,11 @@ struct ScanArgs {
     uint32_t fused;        // ivf_scan_wide also drains the narrow queue (R = 1); the last `fused`
                            // workgroups start on narrow items (0: narrow items on their own kernel)
 };
-size_t scan_wide_lds(uint32_t d4, uint32_t k);   // dynamic LDS of a wide-item block
-bool scan_wide_fits(uint32_t d4, uint32_t k);
+size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
+bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);
 void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
-void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
+// waves 4: items of <= 16 queries, two workgroups per CU; 8: items of <= 32, one per CU
+void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves = 4);
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                        const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,

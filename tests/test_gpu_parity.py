@@ -334,11 +334,14 @@ def test_hub_lists_wide_items(k, seg):
     g.set_option("seg_vectors", seg)   # segment size never changes results
     for batch in (64, 130):
         g.set_batch(batch)
-        for stride, spi, fused in ((40009, 0, 1), (1, 4, 0), (7, 12, 1)):   # dispatch order / item size /
-            g.set_option("wide_stride", stride)                            # fused narrow+wide grid never
-            g.set_option("segs_per_item", spi)                             # change results
+        for wg, stride, spi, fused in ((16, 40009, 0, 1), (16, 1, 4, 0), (16, 7, 12, 1),  # item shape /
+                                       (32, 1, 0, 1), (32, 40009, 4, 0), (32, 7, 12, 1)):  # dispatch order /
+            g.set_option("wide_group", wg)                                 # fused narrow+wide grid never
+            g.set_option("wide_stride", stride)                            # change results
+            g.set_option("segs_per_item", spi)
             g.set_option("fused_scan", fused)
             assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))
+    g.set_option("wide_group", 16)
 
 
 def test_launches_beyond_2_32_workitems():

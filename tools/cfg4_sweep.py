@@ -54,7 +54,7 @@ def main():
                               "wall_ms": round(wall, 3)}), flush=True)
             for n_, _ in opts:  # back to defaults
                 idx.set_option(n_, {"seg_vectors": 0, "segs_per_item": 0, "wide_stride": 1, "diag": 0,
-                                    "fused_scan": 1, "narrow_blocks": 64}[n_])
+                                    "fused_scan": 1, "narrow_blocks": 64, "wide_group": 16}[n_])
 
 
 if __name__ == "__main__":
