@@ -74,7 +74,7 @@ def build_index(vdb, args, device, rank, world):
     t2 = time.perf_counter()
     del data, ids
     torch.cuda.empty_cache()
-    log(rank, f"[bench] train {t1 - t0:.2f}s add {t2 - t1:.2f}s; index {idx.get_gpu_memory_usage() / 2**30:.1f} GiB on rank 0")
+    log(rank, f"[bench] train {t1 - t0:.2f}s add {t2 - t1:.2f}s; index {idx.gpu_bytes_allocated() / 2**30:.1f} GiB on rank 0")
     return idx, {"train_s": round(t1 - t0, 3), "add_s": round(t2 - t1, 3)}
 
 
@@ -118,52 +118,101 @@ def build_index_sharded(vdb, args, device, rank, world):
     del data, ids, asg
     torch.cuda.empty_cache()
     log(rank, f"[bench] sharded build: train {t1 - t0:.2f}s assign {t2 - t1:.2f}s append {t3 - t2:.2f}s; "
-              f"shard {rank}/{world} {idx.get_gpu_memory_usage() / 2**30:.1f} GiB, largest list {int(sizes.max())}")
+              f"shard {rank}/{world} {idx.gpu_bytes_allocated() / 2**30:.1f} GiB, largest list {int(sizes.max())}")
     return idx, {"train_s": round(t1 - t0, 3), "assign_s": round(t2 - t1, 3), "append_s": round(t3 - t2, 3),
                  "sharded_build": f"shard {rank} of {world}"}
 
 
-def cpu_baseline(vdb, idx, args, queries_host, budget_s):
-    """Time the oracle (reference CPU path restatement) on a bounded query sample.
+def host_cpu_share():
+    """Cores this process may use: the cgroup CPU quota (the GPU box gives one GPU's job a
+    share of the host, while os.cpu_count() shows the whole machine), else os.cpu_count()."""
+    n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        n = min(n, int(env))
+    return n
 
-    The sample runs in calls of `--cpu-call` queries; the GPU engine answers the same
-    calls (host API, untimed) so the bit-for-bit check sees the same call boundaries
-    (probe-slot reuse is per call, ivf_flat_index.cpp:210-211)."""
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(vdb, idx, args, queries_host, budget_s):
+    """Time the oracle (reference CPU path restatement) on bounded query samples, the two
+    numbers BASELINE.md promises: (1) one core, as the reference's serial query loop
+    (ivf_flat_index.cpp:214), in calls of `--cpu-call` queries; (2) all cores this job may
+    use (OpenMP over queries, bit-identical per query), one call of `--cpu-queries-mt`
+    queries. The GPU answers the same calls (host API, untimed) and must match bit for bit;
+    call boundaries matter (probe-slot reuse is per call, ivf_flat_index.cpp:210-211). The
+    method follows gpu_vs_cpu_test.cpp:170-185: warm-up search, then the timed searches."""
     sys.path.insert(0, ROOT)
     import oracle  # test infrastructure: the CPU baseline leg only
 
     o = oracle.OracleIndex(args.dim, args.nlist, 0)
     o.centroids = idx.centroids
-    sample = queries_host[: args.cpu_queries]
+    n_mt = min(args.cpu_queries_mt, len(queries_host))
+    sample = queries_host[: max(args.cpu_queries, n_mt)]
     probed = set()
     for q in sample:
         probed.update(o.select_nprobe(q, args.nprobe).tolist())
     sizes = idx.list_sizes()
+    t_exp = time.perf_counter()
     for l in sorted(probed):  # only probed lists are ever read for these queries
         v, i = o.list_buffers(l, int(sizes[l]))
         if len(i):
             idx.get_list_into(l, v, i)
+    t_exp = time.perf_counter() - t_exp
     o.search(sample[:2], args.nprobe, args.k)  # warm-up, as gpu_vs_cpu_test.cpp:171-172
     done, t_cpu = 0, 0.0
-    Ds, Is = [], []
     parity = True
-    while done < len(sample) and t_cpu < budget_s:
-        chunk = sample[done:done + args.cpu_call]
+    single = sample[: args.cpu_queries]
+    while done < len(single) and t_cpu < budget_s:
+        chunk = single[done:done + args.cpu_call]
         t0 = time.perf_counter()
         D, I = o.search(chunk, args.nprobe, args.k, threads=1)
         t_cpu += time.perf_counter() - t0
         Dg, Ig = idx.search(chunk, nprobe=args.nprobe, k=args.k)
         parity &= bool(np.array_equal(I, Ig) and np.array_equal(D.view(np.uint32), Dg.view(np.uint32)))
         done += len(chunk)
+    threads = host_cpu_share()
+    mt = None
+    if n_mt > 0:
+        qs = sample[:n_mt]
+        t0 = time.perf_counter()
+        Dm, Im = o.search(qs, args.nprobe, args.k, threads=threads)
+        t_mt = time.perf_counter() - t0
+        Dg, Ig = idx.search(qs, nprobe=args.nprobe, k=args.k)
+        parity_mt = bool(np.array_equal(Im, Ig) and np.array_equal(Dm.view(np.uint32), Dg.view(np.uint32)))
+        mt = {"value": round(n_mt / t_mt, 3), "unit": "queries/s", "cores": threads,
+              "sample": f"{n_mt} queries in one search() call, OpenMP over queries, {t_mt:.1f}s",
+              "parity_with_gpu": parity_mt}
+        parity &= parity_mt
     return {
         "value": round(done / t_cpu, 3),
         "unit": "queries/s",
         "cores": 1,
         "kind": "port",
         "sample": f"{done} queries of the timed workload (same index, nprobe {args.nprobe}, k {args.k}), "
-                  f"oracle/cpu_ref.cpp single-threaded, {t_cpu:.1f}s",
+                  f"oracle/cpu_ref.cpp single-threaded in calls of {args.cpu_call}, {t_cpu:.1f}s",
         "parity_with_gpu": parity,
-        "host_threads_available": os.cpu_count(),
+        "all_cores": mt,
+        "cpu_model": cpu_model(),
+        "host_threads_visible": os.cpu_count(),
+        "lists_exported_s": round(t_exp, 1),
     }
 
 
@@ -199,6 +248,17 @@ def shard_parity(vdb, idx, args, queries_host, rank, world):
             "oracle_s": round(t_cpu, 2), "bit_identical": same}
 
 
+def launch_ranks(n):
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -211,7 +271,8 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--train", type=int, default=100_000)
-    ap.add_argument("--cpu-queries", type=int, default=256)
+    ap.add_argument("--cpu-queries", type=int, default=256, help="single-core CPU sample (bounded by --cpu-budget)")
+    ap.add_argument("--cpu-queries-mt", type=int, default=128, help="all-cores CPU sample (one call)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--cpu-call", type=int, default=4, help="queries per oracle search() call")
     ap.add_argument("--no-cpu", action="store_true")
@@ -242,6 +303,10 @@ def main():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning knob (vdb_ivf_set_option), e.g. wide_stride=1; results never change")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # One process per GPU: launch the N ranks as children before anything touches
+        # the GPU, wait for them, and exit with their status.
+        sys.exit(launch_ranks(args.gpus))
     if args.cfg:
         args.nvec, args.nlist, args.nprobe = {"cfg2": (1_000_000, 256, 16), "cfg3": (10_000_000, 4096, 32),
                                               "cfg4": (100_000_000, 16384, 64)}[args.cfg]
@@ -252,7 +317,14 @@ def main():
         args.inflight = 3 if world > 1 else 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", 0 if args.same_device else local_rank)
+    ndev = torch.cuda.device_count()  # (does not initialise the GPU)
+    if world > 1 and ndev < world:
+        # fewer GPUs than ranks: a rehearsal of the N-rank protocol on the GPUs present,
+        # with the exchange staged through host memory (RCCL wants one rank per GPU)
+        args.same_device = True
+        args.dist_backend = "gloo"
+    args.rehearsal = world > 1 and args.same_device
+    device = torch.device("cuda", local_rank % max(ndev, 1) if args.same_device else local_rank)
     torch.cuda.set_device(device)
     if world > 1:
         if args.dist_backend == "nccl":
@@ -451,6 +523,8 @@ def run(vdb, args, device, rank, world):
         "build": build_info,
         **({"list_cache": idx.cache_stats()} if any(o.startswith("list_cache_bytes=") for o in args.opt) else {}),
         "engine_options": dict(o.split("=", 1) for o in args.opt),
+        **({"rehearsal": f"{world} ranks on {torch.cuda.device_count()} GPU(s), host-staged exchange: "
+                         "protocol check, not a scaling number"} if args.rehearsal else {}),
         **({"emulated_shard": f"rank 0 of {args.emulate_shard} (partial results; diagnostic, not a bench line)"}
            if args.emulate_shard > 1 else {}),
     }

@@ -114,6 +114,7 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_warmup": (ctypes.c_int, [vp, vp, u32]),
         "vdb_ivf_evict": (ctypes.c_int, [vp, u32]),
         "vdb_ivf_gpu_bytes": (u64, [vp]),
+        "vdb_ivf_gpu_bytes_allocated": (u64, [vp]),
         "vdb_ivf_ntotal": (u64, [vp]),
         "vdb_ivf_list_sizes": (ctypes.c_int, [vp, vp]),
         "vdb_ivf_get_list": (ctypes.c_int, [vp, u32, vp, vp]),
@@ -325,7 +326,12 @@ class IVFFlatIndex:
         _check(lib().vdb_ivf_evict(self._h, list_id))
 
     def get_gpu_memory_usage(self) -> int:
+        """Bytes of the GPU-resident lists, count * (dim * 4 + 8) each (ivf_flat_index.cpp:393-443)."""
         return int(lib().vdb_ivf_gpu_bytes(self._h))
+
+    def gpu_bytes_allocated(self) -> int:
+        """HBM really held for lists (padded 64-row blocks, whole cache in the tier) and centroids."""
+        return int(lib().vdb_ivf_gpu_bytes_allocated(self._h))
 
     def get_total_vectors(self) -> int:
         return int(lib().vdb_ivf_ntotal(self._h))

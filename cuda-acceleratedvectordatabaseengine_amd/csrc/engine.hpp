@@ -1,0 +1,1192 @@
+// engine.hpp — the index handle of the MI355X IVF-Flat engine (host side): one handle =
+// one index on one device; engine.cpp binds it to the C ABI of include/vdb_ivf.h and
+// group.cpp adds the multi-GPU forms (RCCL exchange, one handle per device).
+//
+// One handle = one index on one device. The whole index is HBM-resident in an
+// interleaved list arena (kernels.hpp); a search is a short sequence of kernels
+// per batch of queries, all enqueued on one stream with no host synchronisation:
+//   pad queries -> coarse distances -> probe selection -> probe inversion (plan)
+//   -> ivf_scan -> per-(query, probe) top-k -> per-query merge -> slot carry.
+// Build-side calls (train/add/set_shard) synchronise where the reference
+// algorithm needs a host decision (k-means++ draws from std::mt19937 on the host,
+// exactly as ivf_flat_index.cpp:53-92 does).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <map>
+#include <memory>
+#include <thread>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <queue>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "../../include/vdb_ivf.h"
+#include "kernels.hpp"
+
+namespace vdbe {
+
+extern thread_local std::string g_last_error;
+
+struct VdbError : std::runtime_error {
+    int code;
+    VdbError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+inline void check(hipError_t e, const char* what) {
+    if (e != hipSuccess) {
+        int code = (e == hipErrorOutOfMemory) ? VDB_ERR_OUT_OF_MEMORY : VDB_ERR_DEVICE;
+        (void)hipGetLastError();
+        throw VdbError(code, std::string(what) + ": " + hipGetErrorString(e));
+    }
+}
+#define HIPCHECK(x) check((x), #x)
+
+inline void check_nccl(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw VdbError(VDB_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r));
+}
+#define NCCLCHECK(x) check_nccl((x), #x)
+
+inline void require(bool ok, const std::string& msg, int code = VDB_ERR_INVALID_ARGUMENT) {
+    if (!ok) throw VdbError(code, msg);
+}
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return VDB_OK;
+    } catch (const VdbError& e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "host allocation failed";
+        return VDB_ERR_OUT_OF_MEMORY;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return VDB_ERR_DEVICE;
+    }
+}
+
+// Growable device buffer (capacity in elements).
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    bool host = false;  // page-locked host memory the device reads and writes directly
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)(host ? hipHostFree(p) : hipFree(p));
+        p = nullptr;
+        cap = 0;
+    }
+    T* ensure(size_t n) {
+        if (n <= cap && p) return p;
+        release();
+        size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        if (host)
+            HIPCHECK(hipHostMalloc((void**)&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
+        else
+            HIPCHECK(hipMalloc(&p, bytes));
+        cap = std::max<size_t>(n, 1);
+        return p;
+    }
+    void swap(DevBuf& o) {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
+        std::swap(host, o.host);
+    }
+};
+
+// Page-locked host buffer (fast device-to-host copies of build-time scratch).
+template <class T>
+struct PinnedBuf {
+    T* p = nullptr;
+    explicit PinnedBuf(size_t n) { HIPCHECK(hipHostMalloc((void**)&p, std::max<size_t>(n, 1) * sizeof(T))); }
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+struct EventSet {
+    hipEvent_t begin, coarse_end, scan_begin, scan_end, end;
+};
+
+// One host-API search() call waiting in the coalescing queue.
+struct PendingSearch {
+    const float* q;
+    uint32_t n, nprobe, k;
+    float* dist;
+    uint64_t* ids;
+    int rc = 1;  // 1 = pending, then a VDB_* code
+    std::string err;
+};
+
+// Request coalescing (the reference's intent: QueryServiceImpl::Config max_batch_size /
+// coalesce_window_ms, query_service.h:25-31, never implemented there): concurrent
+// vdb_ivf_search callers enqueue; one worker thread takes every compatible waiting call
+// (same nprobe and k), up to max_queries, and runs them as ONE device search whose
+// per-call slot semantics are kept exact (request boundaries, kernels' req_start).
+// While the device works on one batch, the next one accumulates.
+struct Coalescer {
+    std::mutex m;
+    std::condition_variable wake, done;
+    std::deque<PendingSearch*> queue;
+    std::thread worker;
+    bool stop = false;
+    uint64_t batches = 0, requests = 0;
+};
+
+}  // namespace vdbe
+
+using namespace vdbe;
+
+struct vdb_ivf {
+    uint32_t dim = 0, nlist = 0, dp = 0, d4 = 0;
+    int metric = 0;
+    int device = 0;
+    uint64_t max_gpu_memory = 0;
+    hipStream_t stream = nullptr;
+    mutable std::mutex mu;
+
+    DevBuf<float> cent_rm;   // [nlist][dp], zero pads
+    DevBuf<float4> cent_il;  // [ceil(nlist/64)][d4][64]
+
+    std::vector<uint64_t> count;      // per list, global (emptiness semantics)
+    std::vector<uint8_t> owned;       // lists this handle scans
+    std::vector<uint64_t> block_off;  // arena block offset per owned list
+    uint64_t arena_blocks = 0;
+    DevBuf<float4> arena;
+    DevBuf<uint64_t> arena_ids;
+    DevBuf<uint64_t> d_block_off;
+    DevBuf<uint32_t> d_count_local, d_count_global, d_nseg;
+    std::vector<uint64_t> nseg_prefix;  // sum of the j largest local segment counts
+    uint64_t total = 0;
+    uint32_t rank = 0, world = 1;
+    uint32_t batch = 256;
+    int stale = 1;
+    bool wide_scan = true;
+    int coarse_mode = 1;  // 1: MFMA bounds + exact re-rank (L2/IP); 0: exact VALU distances
+    uint32_t wide_stride = 1;  // wide-item dispatch permutation (1 = plan order; measured best)
+    uint32_t seg_blocks = 8;  // current segment size (blocks of 64 vectors; upload_directory sets it)
+    uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)
+    uint32_t diag = 0;                          // scan diagnostics (results invalid when set)
+    uint32_t segs_item_opt = 0;   // segments per wide item (0: one per wave, taken dynamically)
+    uint32_t wide_group = 16;     // queries per wide item at most: 16 (4-wave workgroups) or 32 (8-wave)
+    bool fused_scan = true;       // narrow items inside the wide scan's grid (option fused_scan; +2-3 %)
+    uint32_t narrow_blocks = 64;  // persistent narrow-scan workgroups beside the wide scan (1/8 shard: +1.5 % vs 512)
+
+    // List-cache tier (option list_cache_bytes > 0), the reference's residency model
+    // (load_list_to_gpu on first touch under a byte cap, evict_list_from_gpu,
+    // ivf_flat_index.cpp:387-471) for indexes larger than HBM: the arena then lives in
+    // page-locked host memory and HBM holds a cache of whole lists. Before a batch is
+    // planned, every list it probes is made resident (DMA of its blocks), evicting the
+    // least recently used lists the batch does not probe; the scan reads the cache
+    // through the same directory (d_block_off), so the kernels are unchanged.
+    static constexpr uint64_t kAbsent = ~0ull;
+    uint64_t cache_blocks = 0;  // capacity in 64-vector blocks (0: tier off, the arena is in HBM)
+    DevBuf<float4> cache;
+    DevBuf<uint64_t> cache_ids;
+    std::vector<uint64_t> cache_off;        // per list: cache block offset or kAbsent
+    std::vector<uint64_t> last_use;         // per list: batch tick of the last probe
+    std::map<uint64_t, uint64_t> free_ext;  // free cache extents: block offset -> blocks
+    uint64_t use_tick = 0, cache_used = 0;
+    uint64_t resident_n = 0, storable_n = 0;  // cached lists / non-empty lists stored here
+    uint64_t cache_loads = 0, cache_evictions = 0, cache_bytes_in = 0;
+    DevBuf<uint32_t> probe_stage;  // pinned: the batch's probes, read by the host
+    DevBuf<uint64_t> dir_stage;    // pinned: directory upload source
+    // Recorded after every cache load and directory upload, on the stream that made
+    // them. Every tier-mode batch waits for it before it plans and scans, so a search
+    // on another stream whose lists are all cached never reads blocks or directory
+    // entries still in flight (a miss quiesces the other streams first, so the latest
+    // recording covers every earlier load).
+    hipEvent_t tier_ev = nullptr;
+    bool tier_ev_used = false;
+
+    // File home for the tier (vdb_ivf_open_lists): the lists stay in an index file written
+    // by vdb_ivf_save and are read into the cache on demand (pread -> pinned staging ->
+    // HBM -> pad + interleave kernels), instead of living in host memory.
+    int home_fd = -1;
+    std::vector<uint64_t> file_off;  // per list: file offset of its ids (vectors follow)
+    DevBuf<float> fstage[2];         // pinned: row-major vectors of a chunk
+    DevBuf<uint64_t> istage[2];      // pinned: ids of a chunk
+    hipEvent_t fstage_done[2] = {nullptr, nullptr};
+    DevBuf<float> drows, dpad;       // device: a chunk's rows, then zero-padded to dp
+    uint64_t file_bytes_read = 0;
+
+    // Search workspaces: a ring of slots so that searches issued on different streams
+    // run concurrently (one batch's small kernels and scan tail overlap the next
+    // batch's scan). A call takes the next slot; its stream first waits for the
+    // slot's previous batch (slot.done), wherever that ran.
+    struct SearchSlot {
+        DevBuf<float> qpad, cd, cdelta, part_d, slot_d, carry_d;
+        DevBuf<uint64_t> part_i, slot_i, carry_i;
+        DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters, l1base, cand;
+        DevBuf<uint2> l1_items;
+        DevBuf<float> l1_d;
+        DevBuf<uint64_t> l1_i;
+        DevBuf<vdbk::ScanItem> items, items_w;
+        DevBuf<uint8_t> xrec, xgat;  // multi-GPU: this rank's packed partials, the gathered records
+        hipStream_t side = nullptr;  // narrow-item scan, concurrent with the wide items
+        hipStream_t gstream = nullptr;  // group member: the stream this slot's searches run on
+        hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
+        bool used = false;
+    };
+    static constexpr int kSlots = 3;
+    SearchSlot slots[kSlots];
+    uint32_t next_slot = 0;
+
+    // ---- multi-GPU: lists sharded over ranks (LPT), every rank runs the
+    // coarse step for the whole batch, scans its own lists and merges its slots into ONE
+    // packed record per batch (f32 dist[B][k] | pad | u64 ids[B][k]); one RCCL all-gather
+    // of the records over xGMI, then the on-device unique-id merge. The communicator is
+    // attached (one process per GPU, vdb_ivf_attach_comm) or owned by a group handle
+    // (one process, one member handle per device, vdb_ivf_create_group).
+    ncclComm_t comm = nullptr;
+    bool comm_owned = false;
+    uint32_t comm_rank = 0, comm_world = 1;
+    // Group handle: members[m] holds the lists owner[l] == m places on its device; the
+    // group itself holds only the host-API staging on members[0]'s device.
+    std::vector<std::unique_ptr<vdb_ivf>> members;
+    std::vector<uint32_t> owner;  // per list: member storing it, or kUnplaced
+    static constexpr uint32_t kUnplaced = 0xFFFFFFFFu;
+    bool group_rccl = false;      // members on distinct devices: RCCL; else device copies (rehearsal)
+    std::vector<hipEvent_t> gev;  // group call fences, 2 per member
+    bool is_group() const { return !members.empty(); }
+    DevBuf<float> out_d, qin;  // host-API staging (synchronous calls)
+    DevBuf<uint64_t> out_i;
+    DevBuf<uint32_t> d_req;    // coalesced calls: request start per query
+    std::unique_ptr<Coalescer> co;
+    std::mutex co_init_mu;
+    bool coalesce = true;
+    uint32_t coalesce_max_queries = 1024;
+    uint32_t coalesce_window_us = 0;
+    std::vector<float> hq_stage;
+    std::vector<float> hd_stage;
+    std::vector<uint64_t> hi_stage;
+    DevBuf<unsigned long long> stats;
+
+    bool prof = false;
+    std::vector<EventSet> events;
+    size_t events_used = 0;
+
+    ~vdb_ivf() {
+        stop_coalescer();
+        members.clear();  // each member waits for and frees its own device work
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (auto& sl : slots)
+            if (sl.gstream) (void)hipStreamSynchronize(sl.gstream);
+        if (comm) {
+            if (comm_owned) (void)ncclCommDestroy(comm);
+            comm = nullptr;
+        }
+        for (auto& e : gev) (void)hipEventDestroy(e);
+        if (home_fd >= 0) ::close(home_fd);
+        for (auto& e : fstage_done)
+            if (e) (void)hipEventDestroy(e);
+        if (tier_ev) (void)hipEventDestroy(tier_ev);
+        for (auto& e : events) {
+            (void)hipEventDestroy(e.begin);
+            (void)hipEventDestroy(e.coarse_end);
+            (void)hipEventDestroy(e.scan_begin);
+            (void)hipEventDestroy(e.scan_end);
+            (void)hipEventDestroy(e.end);
+        }
+        for (auto& sl : slots) {
+            if (sl.fork) (void)hipEventDestroy(sl.fork);
+            if (sl.join) (void)hipEventDestroy(sl.join);
+            if (sl.done) (void)hipEventDestroy(sl.done);
+            if (sl.side) (void)hipStreamDestroy(sl.side);
+            if (sl.gstream) (void)hipStreamDestroy(sl.gstream);
+        }
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    void set_device() { HIPCHECK(hipSetDevice(device)); }
+
+    // ---- host-API search: direct, or through the coalescing queue ----
+    void search_host(const float* q, uint32_t n, uint32_t nprobe, uint32_t k, float* dist, uint64_t* ids,
+                     const uint32_t* h_req_start) {
+        set_device();
+        HIPCHECK(hipMemcpyAsync(qin.ensure((size_t)n * dim), q, (size_t)n * dim * 4, hipMemcpyHostToDevice, stream));
+        const uint32_t* dr = nullptr;
+        if (h_req_start) {
+            HIPCHECK(hipMemcpyAsync(d_req.ensure(n), h_req_start, (size_t)n * 4, hipMemcpyHostToDevice, stream));
+            dr = d_req.p;
+        }
+        search_device(qin.p, n, nprobe, k, out_d.ensure((size_t)n * k), out_i.ensure((size_t)n * k), stream, dr);
+        HIPCHECK(hipMemcpyAsync(dist, out_d.p, (size_t)n * k * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipMemcpyAsync(ids, out_i.p, (size_t)n * k * 8, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+    }
+
+    void start_coalescer() {
+        if (co) return;
+        co.reset(new Coalescer());
+        co->worker = std::thread([this] { coalesce_loop(); });
+    }
+
+    void stop_coalescer() {
+        if (!co) return;
+        {
+            std::lock_guard<std::mutex> g(co->m);
+            co->stop = true;
+        }
+        co->wake.notify_all();
+        if (co->worker.joinable()) co->worker.join();
+        co.reset();
+    }
+
+    void coalesce_loop() {
+        Coalescer& c = *co;
+        for (;;) {
+            std::vector<PendingSearch*> run;
+            uint32_t nq = 0;
+            {
+                std::unique_lock<std::mutex> lk(c.m);
+                c.wake.wait(lk, [&] { return c.stop || !c.queue.empty(); });
+                if (c.queue.empty()) return;  // stop requested and nothing left
+                if (coalesce_window_us)
+                    c.wake.wait_for(lk, std::chrono::microseconds(coalesce_window_us), [&] {
+                        uint64_t t = 0;
+                        for (auto* r : c.queue) t += r->n;
+                        return c.stop || t >= coalesce_max_queries;
+                    });
+                const uint32_t P = c.queue.front()->nprobe, K = c.queue.front()->k;
+                for (auto it = c.queue.begin(); it != c.queue.end();) {
+                    PendingSearch* r = *it;
+                    if (r->nprobe == P && r->k == K && (run.empty() || nq + r->n <= coalesce_max_queries)) {
+                        run.push_back(r);
+                        nq += r->n;
+                        it = c.queue.erase(it);
+                    } else {
+                        ++it;
+                    }
+                }
+                c.batches++;
+                c.requests += run.size();
+            }
+            int rc = VDB_OK;
+            std::string err;
+            try {
+                std::lock_guard<std::mutex> g(mu);
+                if (run.size() == 1) {
+                    PendingSearch* r = run[0];
+                    search_host(r->q, r->n, r->nprobe, r->k, r->dist, r->ids, nullptr);
+                } else {
+                    const uint32_t K = run[0]->k;
+                    hq_stage.resize((size_t)nq * dim);
+                    hd_stage.resize((size_t)nq * K);
+                    hi_stage.resize((size_t)nq * K);
+                    std::vector<uint32_t> rs(nq);
+                    uint32_t o = 0;
+                    for (PendingSearch* r : run) {
+                        std::memcpy(hq_stage.data() + (size_t)o * dim, r->q, (size_t)r->n * dim * 4);
+                        for (uint32_t i = 0; i < r->n; ++i) rs[o + i] = o;
+                        o += r->n;
+                    }
+                    search_host(hq_stage.data(), nq, run[0]->nprobe, K, hd_stage.data(), hi_stage.data(), rs.data());
+                    o = 0;
+                    for (PendingSearch* r : run) {
+                        std::memcpy(r->dist, hd_stage.data() + (size_t)o * K, (size_t)r->n * K * 4);
+                        std::memcpy(r->ids, hi_stage.data() + (size_t)o * K, (size_t)r->n * K * 8);
+                        o += r->n;
+                    }
+                }
+            } catch (const VdbError& e) {
+                rc = e.code;
+                err = e.what();
+            } catch (const std::exception& e) {
+                rc = VDB_ERR_DEVICE;
+                err = e.what();
+            }
+            {
+                std::lock_guard<std::mutex> g(c.m);
+                for (PendingSearch* r : run) {
+                    r->err = err;
+                    r->rc = rc;
+                }
+            }
+            c.done.notify_all();
+        }
+    }
+
+    void search_coalesced(const float* q, uint32_t n, uint32_t nprobe, uint32_t k, float* dist, uint64_t* ids) {
+        PendingSearch r{q, n, nprobe, k, dist, ids};
+        {
+            // not `mu`: the worker holds that while the device runs a batch, and callers
+            // must be able to queue meanwhile
+            std::lock_guard<std::mutex> g(co_init_mu);
+            start_coalescer();
+        }
+        std::unique_lock<std::mutex> lk(co->m);
+        co->queue.push_back(&r);
+        co->wake.notify_one();
+        co->done.wait(lk, [&] { return r.rc != 1; });
+        if (r.rc != VDB_OK) throw VdbError(r.rc, r.err);
+    }
+
+    // Wait for every search still in flight on any stream before the index changes
+    // under it (buffers freed, lists moved, centroids rewritten).
+    void quiesce() {
+        for (auto& sl : slots)
+            if (sl.used) HIPCHECK(hipEventSynchronize(sl.done));
+    }
+
+    // Upload the list directory and recompute the segment-count prefix.
+    void upload_directory() {
+        quiesce();
+        // Segment size: the largest of 512/256/128/64 vectors that still cuts this
+        // handle's lists into >= 4096 segments, so a shard of an 8-GPU node keeps
+        // enough scan work items for load balance (measured on a 1/8 shard of the
+        // 10M x 768 index: 256 beats 512 by 5 % and 64 by 9 %).
+        uint64_t local = 0;
+        for (uint32_t l = 0; l < nlist; ++l) local += owned[l] ? count[l] : 0;
+        if (seg_blocks_opt) {
+            seg_blocks = seg_blocks_opt;
+        } else {
+            seg_blocks = 8;  // 512 vectors at most by default (1024 is an explicit option)
+            while (seg_blocks > 1 && local / ((uint64_t)seg_blocks * 64) < 4096) seg_blocks >>= 1;
+        }
+        std::vector<uint32_t> cl(nlist), cg(nlist), ns(nlist);
+        storable_n = 0;
+        for (uint32_t l = 0; l < nlist; ++l) {
+            require(count[l] < (1ull << 32), "list longer than 2^32 vectors", VDB_ERR_UNSUPPORTED);
+            cg[l] = (uint32_t)count[l];
+            cl[l] = owned[l] ? (uint32_t)count[l] : 0u;
+            storable_n += cl[l] > 0;
+            ns[l] = (uint32_t)cdiv(cl[l], (uint64_t)seg_blocks * 64);
+        }
+        upload_scan_directory(stream);
+        HIPCHECK(hipMemcpyAsync(d_count_local.ensure(nlist), cl.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemcpyAsync(d_count_global.ensure(nlist), cg.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemcpyAsync(d_nseg.ensure(nlist), ns.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+        std::vector<uint32_t> sorted(ns);
+        std::sort(sorted.begin(), sorted.end(), std::greater<uint32_t>());
+        nseg_prefix.assign(nlist + 1, 0);
+        for (uint32_t j = 0; j < nlist; ++j) nseg_prefix[j + 1] = nseg_prefix[j] + sorted[j];
+        HIPCHECK(hipStreamSynchronize(stream));  // host vectors above are stack-owned
+    }
+
+    // Rebuild the arena so list l holds `keep[l]` of its current blocks at new
+    // offsets sized for `new_count[l]` vectors (0 for lists this handle drops).
+    void relayout(const std::vector<uint64_t>& new_count, const std::vector<uint8_t>& new_owned) {
+        relayout(new_count, new_owned, arena.host);
+    }
+    void relayout(const std::vector<uint64_t>& new_count, const std::vector<uint8_t>& new_owned, bool host_arena) {
+        quiesce();
+        std::vector<uint64_t> new_off(nlist, 0), old_off(nlist, 0);
+        std::vector<uint32_t> nblocks(nlist, 0);
+        uint64_t blocks = 0;
+        for (uint32_t l = 0; l < nlist; ++l) {
+            new_off[l] = blocks;
+            if (new_owned[l]) blocks += cdiv(new_count[l], 64);
+            if (owned[l] && new_owned[l] && count[l] > 0) {
+                nblocks[l] = (uint32_t)cdiv(count[l], 64);
+                old_off[l] = block_off[l];
+            }
+        }
+        DevBuf<float4> na;
+        DevBuf<uint64_t> ni;
+        na.host = ni.host = host_arena;
+        // one slack block past the last list: the scan prefetches one chunk and one
+        // block of ids beyond the segment it streams
+        const size_t vec4 = (size_t)(blocks + 1) * d4 * 64;
+        na.ensure(vec4);
+        ni.ensure((size_t)(blocks + 1) * 64);
+        if (blocks) {
+            HIPCHECK(hipMemsetAsync(na.p, 0, vec4 * sizeof(float4), stream));
+            HIPCHECK(hipMemsetAsync(ni.p, 0xFF, (size_t)(blocks + 1) * 64 * 8, stream));
+        }
+        if (arena_blocks && blocks) {
+            DevBuf<uint64_t> doo, dno;
+            DevBuf<uint32_t> dnb;
+            HIPCHECK(hipMemcpyAsync(doo.ensure(nlist), old_off.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+            HIPCHECK(hipMemcpyAsync(dno.ensure(nlist), new_off.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+            HIPCHECK(hipMemcpyAsync(dnb.ensure(nlist), nblocks.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+            vdbk::launch_copy_lists(arena.p, arena_ids.p, doo.p, dno.p, dnb.p, nlist, d4, na.p, ni.p, stream);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipStreamSynchronize(stream));
+        }
+        HIPCHECK(hipStreamSynchronize(stream));
+        arena.swap(na);
+        arena_ids.swap(ni);
+        arena_blocks = blocks;
+        block_off = new_off;
+        owned = new_owned;
+        cache_reset();  // list contents or offsets changed: nothing cached stays valid
+    }
+
+    // ---- list-cache tier ----
+    bool tiered() const { return cache_blocks > 0; }
+    uint64_t list_blocks(uint32_t l) const { return cdiv(count[l], 64); }
+    static uint64_t block_bytes(uint32_t dp_) { return 64ull * ((uint64_t)dp_ * 4 + 8); }
+
+    void cache_reset() {
+        cache_off.assign(nlist, kAbsent);
+        last_use.assign(nlist, 0);
+        free_ext.clear();
+        if (cache_blocks) free_ext[0] = cache_blocks;
+        cache_used = 0;
+        resident_n = 0;
+    }
+
+    uint64_t cache_alloc(uint64_t nb) {  // first fit
+        for (auto it = free_ext.begin(); it != free_ext.end(); ++it) {
+            if (it->second < nb) continue;
+            const uint64_t off = it->first, len = it->second;
+            free_ext.erase(it);
+            if (len > nb) free_ext[off + nb] = len - nb;
+            cache_used += nb;
+            return off;
+        }
+        return kAbsent;
+    }
+
+    void cache_free(uint32_t l) {
+        const uint64_t nb = list_blocks(l);
+        auto it = free_ext.emplace(cache_off[l], nb).first;
+        cache_off[l] = kAbsent;
+        cache_used -= nb;
+        --resident_n;
+        auto nx = std::next(it);
+        if (nx != free_ext.end() && it->first + it->second == nx->first) {
+            it->second += nx->second;
+            free_ext.erase(nx);
+        }
+        if (it != free_ext.begin()) {
+            auto pv = std::prev(it);
+            if (pv->first + pv->second == it->first) {
+                pv->second += it->second;
+                free_ext.erase(it);
+            }
+        }
+    }
+
+    // Scan directory: home offsets, or cache offsets in the tier (absent lists: 0,
+    // never read: a list is made resident before any batch that probes it is planned).
+    void upload_scan_directory(hipStream_t s) {
+        const uint64_t* src = block_off.data();
+        if (tiered()) {
+            uint64_t* st = dir_stage.ensure(nlist);
+            for (uint32_t l = 0; l < nlist; ++l) st[l] = cache_off[l] == kAbsent ? 0 : cache_off[l];
+            src = st;
+        }
+        HIPCHECK(hipMemcpyAsync(d_block_off.ensure(nlist), src, nlist * 8, hipMemcpyHostToDevice, s));
+        if (!tiered()) {
+            HIPCHECK(hipStreamSynchronize(s));  // src is the host vector
+            return;
+        }
+        if (!tier_ev) HIPCHECK(hipEventCreateWithFlags(&tier_ev, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(tier_ev, s));  // covers the loads queued on s before it
+        tier_ev_used = true;
+    }
+
+    // Make `lists` resident (ids may repeat; lists not stored here or empty are
+    // skipped). False if together they exceed the cache. Copies are ordered on s.
+    bool make_resident(const uint32_t* lists, size_t n, hipStream_t s) {
+        ++use_tick;
+        std::vector<uint8_t> in_set(nlist, 0);
+        std::vector<uint32_t> want, miss;
+        uint64_t need = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const uint32_t l = lists[i];
+            if (l >= nlist || in_set[l] || !owned[l] || count[l] == 0) continue;
+            in_set[l] = 1;
+            want.push_back(l);
+            need += list_blocks(l);
+            last_use[l] = use_tick;
+            if (cache_off[l] == kAbsent) miss.push_back(l);
+        }
+        if (need > cache_blocks) return false;
+        if (miss.empty()) return true;
+        quiesce();  // searches on other streams may still read the lists evicted below
+        auto by_size = [&](uint32_t a, uint32_t b) { return count[a] != count[b] ? count[a] > count[b] : a < b; };
+        std::vector<uint32_t> victims;
+        for (uint32_t l = 0; l < nlist; ++l)
+            if (cache_off[l] != kAbsent && !in_set[l]) victims.push_back(l);
+        std::sort(victims.begin(), victims.end(),
+                  [&](uint32_t a, uint32_t b) { return last_use[a] != last_use[b] ? last_use[a] < last_use[b] : a < b; });
+        std::sort(miss.begin(), miss.end(), by_size);
+        size_t vi = 0;
+        for (size_t m = 0; m < miss.size(); ++m) {
+            const uint32_t l = miss[m];
+            uint64_t off;
+            while ((off = cache_alloc(list_blocks(l))) == kAbsent && vi < victims.size()) {
+                cache_free(victims[vi++]);
+                ++cache_evictions;
+            }
+            if (off == kAbsent) {
+                // fragmented: keep only this batch's lists, packed from offset 0 (they fit)
+                for (uint32_t v = 0; v < nlist; ++v)
+                    if (cache_off[v] != kAbsent) cache_free(v);
+                miss = want;
+                std::sort(miss.begin(), miss.end(), by_size);
+                m = (size_t)-1;
+                continue;
+            }
+            cache_off[l] = off;
+            ++resident_n;
+            const uint64_t nb = list_blocks(l);
+            ++cache_loads;
+            cache_bytes_in += nb * block_bytes(dp);
+            if (file_home()) {
+                load_list_from_file(l, off, s);
+                continue;
+            }
+            HIPCHECK(hipMemcpyAsync(cache.p + off * d4 * 64, arena.p + block_off[l] * d4 * 64, nb * d4 * 64 * sizeof(float4),
+                                    hipMemcpyHostToDevice, s));
+            HIPCHECK(hipMemcpyAsync(cache_ids.p + off * 64, arena_ids.p + block_off[l] * 64, nb * 64 * 8,
+                                    hipMemcpyHostToDevice, s));
+        }
+        upload_scan_directory(s);
+        return true;
+    }
+
+    bool file_home() const { return home_fd >= 0; }
+
+    void pread_all(void* dst, size_t bytes, uint64_t off) {
+        char* p = (char*)dst;
+        while (bytes) {
+            const ssize_t r = ::pread(home_fd, p, bytes, (off_t)off);
+            require(r > 0, "short read from the list file", VDB_ERR_STATE);
+            p += r;
+            bytes -= (size_t)r;
+            off += (uint64_t)r;
+            file_bytes_read += (uint64_t)r;
+        }
+    }
+
+    // One list from the file into cache blocks [off, off + blocks): chunks of whole
+    // 64-row blocks, each read into one of two pinned buffers (the other one's copy
+    // is in flight), copied to HBM, padded to dp and interleaved into the block layout.
+    void load_list_from_file(uint32_t l, uint64_t off, hipStream_t s) {
+        const uint64_t n = count[l];
+        const uint64_t rows = std::max<uint64_t>(64, ((32ull << 20) / ((uint64_t)dim * 4)) / 64 * 64);
+        for (int i = 0; i < 2; ++i) {
+            if (!fstage_done[i]) HIPCHECK(hipEventCreateWithFlags(&fstage_done[i], hipEventDisableTiming));
+            fstage[i].host = istage[i].host = true;
+            fstage[i].ensure(rows * dim);
+            istage[i].ensure(rows);
+        }
+        drows.ensure(rows * dim);
+        dpad.ensure(rows * dp);
+        const uint64_t ids_at = file_off[l], vec_at = file_off[l] + n * 8;
+        for (uint64_t r0 = 0, c = 0; r0 < n; r0 += rows, ++c) {
+            const int i = (int)(c & 1);
+            const uint64_t m = std::min(rows, n - r0);
+            HIPCHECK(hipEventSynchronize(fstage_done[i]));  // this buffer's previous copy has landed
+            pread_all(istage[i].p, m * 8, ids_at + r0 * 8);
+            pread_all(fstage[i].p, m * dim * 4, vec_at + r0 * dim * 4);
+            const uint64_t b = off + r0 / 64;
+            HIPCHECK(hipMemcpyAsync(cache_ids.p + b * 64, istage[i].p, m * 8, hipMemcpyHostToDevice, s));
+            HIPCHECK(hipMemcpyAsync(drows.p, fstage[i].p, m * dim * 4, hipMemcpyHostToDevice, s));
+            HIPCHECK(hipEventRecord(fstage_done[i], s));
+            vdbk::launch_pad_rows(drows.p, m, dim, dp, dpad.p, s);
+            vdbk::launch_interleave(dpad.p, m, dp, cache.p + b * d4 * 64, s);
+            HIPCHECK(hipGetLastError());
+        }
+    }
+
+    // Serve the lists from an index file (vdb_ivf_save format) through the tier.
+    void open_lists(const char* path) {
+        require(tiered(), "open_lists needs the list-cache tier (set list_cache_bytes first)", VDB_ERR_STATE);
+        quiesce();
+        const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+        require(fd >= 0, std::string("cannot open ") + path, VDB_ERR_STATE);
+        if (home_fd >= 0) ::close(home_fd);
+        home_fd = fd;
+        char magic[8];
+        uint32_t hdr[4];
+        pread_all(magic, 8, 0);
+        pread_all(hdr, sizeof(hdr), 8);
+        if (std::memcmp(magic, "VDBIVF01", 8) != 0 || hdr[0] != dim || hdr[1] != nlist || (int)hdr[2] != metric) {
+            ::close(home_fd);
+            home_fd = -1;
+            throw VdbError(VDB_ERR_INVALID_ARGUMENT, "index file does not match this index's configuration");
+        }
+        std::vector<float> c((size_t)nlist * dim);
+        pread_all(c.data(), c.size() * 4, 24);
+        HIPCHECK(hipMemcpy2DAsync(cent_rm.p, dp * 4, c.data(), dim * 4, dim * 4, nlist, hipMemcpyHostToDevice, stream));
+        refresh_centroid_layout();
+        uint64_t at = 24 + (uint64_t)c.size() * 4;
+        file_off.assign(nlist, 0);
+        total = 0;
+        for (uint32_t l = 0; l < nlist; ++l) {
+            uint64_t cnt = 0;
+            pread_all(&cnt, 8, at);
+            file_off[l] = at + 8;
+            count[l] = cnt;
+            total += cnt;
+            at += 8 + cnt * 8 + cnt * (uint64_t)dim * 4;
+        }
+        arena.release();  // no home copy in memory: the file is the home
+        arena_ids.release();
+        arena_blocks = 0;
+        block_off.assign(nlist, 0);
+        owned.assign(nlist, 1);
+        rank = 0;
+        world = 1;
+        cache_reset();
+        upload_directory();
+    }
+
+    // Turn the tier on (bytes > 0: HBM cache of that many bytes, arena moved to host
+    // memory) or off (arena back in HBM).
+    void set_list_cache(uint64_t bytes) {
+        quiesce();
+        const uint64_t nb = bytes / block_bytes(dp);
+        require(bytes == 0 || nb > 0, "list_cache_bytes is below one block of 64 vectors");
+        require(nb > 0 || !file_home(), "lists served from a file need the list-cache tier", VDB_ERR_STATE);
+        cache.release();
+        cache_ids.release();
+        cache_blocks = 0;
+        if (!file_home() && (nb > 0) != arena.host) relayout(count, owned, nb > 0);  // moves the arena
+        cache_blocks = nb;
+        if (nb) {  // one slack block: the scan prefetches past a segment's end
+            cache.ensure((nb + 1) * d4 * 64);
+            cache_ids.ensure((nb + 1) * 64);
+        }
+        cache_reset();
+        upload_directory();
+    }
+
+    // Row-major [n][dim] device input -> zero-padded [n][dp] (or the input itself).
+    const float* padded_rows(const float* d_v, uint64_t n, DevBuf<float>& tmp) {
+        if (dp == dim) return d_v;
+        vdbk::launch_pad_rows(d_v, n, dim, dp, tmp.ensure(n * dp), stream);
+        HIPCHECK(hipGetLastError());
+        return tmp.p;
+    }
+
+    // Caller holds mu. Host centroids [nlist][dim] in (zero pads kept).
+    void set_centroids_host(const float* c) {
+        quiesce();
+        HIPCHECK(hipMemcpy2DAsync(cent_rm.p, dp * 4, c, dim * 4, dim * 4, nlist, hipMemcpyHostToDevice, stream));
+        refresh_centroid_layout();
+        HIPCHECK(hipStreamSynchronize(stream));
+    }
+
+    // Caller holds mu. Append host rows to the given lists (input order per list).
+    void add_to_lists_host(const float* v, const uint64_t* ids, const uint32_t* lists, uint64_t n) {
+        if (n == 0) return;
+        for (uint64_t i = 0; i < n; ++i) require(lists[i] < nlist, "list id out of range");
+        DevBuf<float> dv, tmp;
+        DevBuf<uint64_t> di;
+        DevBuf<uint32_t> dl;
+        HIPCHECK(hipMemcpyAsync(dv.ensure(n * dim), v, n * dim * 4, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemcpyAsync(di.ensure(n), ids, n * 8, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemcpyAsync(dl.ensure(n), lists, n * 4, hipMemcpyHostToDevice, stream));
+        append(padded_rows(dv.p, n, tmp), di.p, dl.p, n);
+        HIPCHECK(hipStreamSynchronize(stream));
+    }
+
+    // Caller holds mu. Centroids row-major [nlist][dim] into host memory.
+    void export_centroids(float* c) {
+        HIPCHECK(hipMemcpy2DAsync(c, dim * 4, cent_rm.p, dp * 4, dim * 4, nlist, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+    }
+
+    // Caller holds mu. List l row-major (count x dim) with its ids, in add order.
+    void export_list(uint32_t l, float* vectors, uint64_t* ids) {
+        const uint64_t c = count[l];
+        if (c == 0) return;
+        require(owned[l], "list is not stored on this shard", VDB_ERR_STATE);
+        if (file_home()) {  // the file holds the list row-major, as returned
+            if (ids) pread_all(ids, c * 8, file_off[l]);
+            if (vectors) pread_all(vectors, c * dim * 4, file_off[l] + c * 8);
+            return;
+        }
+        DevBuf<float> dv;
+        DevBuf<uint64_t> di;
+        vdbk::launch_export_list(arena.p, arena_ids.p, block_off[l], (uint32_t)c, dim, d4, dv.ensure(c * dim),
+                                 di.ensure(c), stream);
+        HIPCHECK(hipGetLastError());
+        if (vectors) HIPCHECK(hipMemcpyAsync(vectors, dv.p, c * dim * 4, hipMemcpyDeviceToHost, stream));
+        if (ids) HIPCHECK(hipMemcpyAsync(ids, di.p, c * 8, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+    }
+
+    void refresh_centroid_layout() {
+        quiesce();
+        vdbk::launch_interleave(cent_rm.p, nlist, dp, cent_il.p, stream);
+        HIPCHECK(hipGetLastError());
+    }
+
+    // assign_to_lists (cpp:259-295): exact argmin with ties to the lowest centroid. For
+    // L2 / IP it is the coarse step's top-1: MFMA distance bounds, then the exact
+    // sequential distances of every centroid that can still be the minimum
+    // (ivf_assign_rerank: candidates whose lower bound <= the smallest upper bound; NaN
+    // orders last, so an all-NaN row goes to list 0 as with the strict '<').
+    // Rows are processed in chunks whose bound matrices fit a fixed workspace.
+    void assign(const float* vpad, uint64_t n, uint32_t* out) {
+        if (coarse_mode == 1 && metric != 2 && vdbk::rerank_rows(dp, 1) > 0) {
+            const uint64_t budget = 1024ull << 20;  // bytes of the two bound matrices per chunk
+            uint64_t chunk = std::max<uint64_t>(256, budget / ((uint64_t)nlist * 8) / 16 * 16);
+            chunk = std::min<uint64_t>(chunk, n);
+            DevBuf<float> ap, de;
+            ap.ensure(chunk * nlist);
+            de.ensure(chunk * nlist);
+            for (uint64_t r0 = 0; r0 < n; r0 += chunk) {
+                const uint32_t b = (uint32_t)std::min<uint64_t>(chunk, n - r0);
+                vdbk::launch_coarse_mfma(metric, cent_rm.p, nlist, dp, vpad + r0 * dp, b, ap.p, de.p, stream);
+                vdbk::launch_assign_rerank(metric, ap.p, de.p, cent_rm.p, nlist, dp, vpad + r0 * dp, b, out + r0, stream);
+                HIPCHECK(hipGetLastError());
+            }
+            HIPCHECK(hipStreamSynchronize(stream));  // the chunk buffers are freed on return
+            return;
+        }
+        vdbk::launch_assign(metric, vpad, n, dp, cent_il.p, nlist, out, stream);
+        HIPCHECK(hipGetLastError());
+    }
+
+    // Stable grouping of row indices by key (input order kept within a key).
+    void group_by_key(const uint32_t* keys, uint64_t n, DevBuf<uint32_t>& sorted_keys, DevBuf<uint32_t>& order) {
+        require(n < (1ull << 31), "batch larger than 2^31 vectors", VDB_ERR_UNSUPPORTED);
+        DevBuf<uint32_t> iota;
+        vdbk::launch_iota(iota.ensure(n), n, stream);
+        int bits = 1;
+        while ((1ull << bits) < nlist) ++bits;
+        size_t tb = 0;
+        HIPCHECK(vdbk::radix_sort_pairs(nullptr, tb, keys, sorted_keys.ensure(n), iota.p, order.ensure(n), n, bits, stream));
+        DevBuf<unsigned char> temp;
+        temp.ensure(tb);
+        HIPCHECK(vdbk::radix_sort_pairs(temp.p, tb, keys, sorted_keys.p, iota.p, order.p, n, bits, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+    }
+
+    std::vector<uint32_t> key_counts(const uint32_t* keys, uint64_t n, DevBuf<uint32_t>& d_counts) {
+        HIPCHECK(hipMemsetAsync(d_counts.ensure(nlist), 0, nlist * 4, stream));
+        vdbk::launch_histogram(keys, n, d_counts.p, stream);
+        HIPCHECK(hipGetLastError());
+        std::vector<uint32_t> h(nlist);
+        HIPCHECK(hipMemcpyAsync(h.data(), d_counts.p, nlist * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        return h;
+    }
+
+    // ---- train: ivf_flat_index.cpp:49-145 ----
+    void train(const float* d_v, uint64_t n) {
+        require(n > 0, "train needs at least one vector");
+        DevBuf<float> tmp, mind;
+        const float* vpad = padded_rows(d_v, n, tmp);
+        DevBuf<float4> v_il;
+        vdbk::launch_interleave(vpad, n, dp, v_il.ensure(cdiv(n, 64) * d4 * 64), stream);
+        HIPCHECK(hipGetLastError());
+
+        std::mt19937 gen(42);
+        std::uniform_int_distribution<uint64_t> pick(0, n - 1);
+        const uint64_t first = pick(gen);
+        HIPCHECK(hipMemcpyAsync(cent_rm.p, vpad + first * dp, dp * 4, hipMemcpyDeviceToDevice, stream));
+
+        vdbk::launch_mindist_init(mind.ensure(n), n, stream);
+        // The min-distance update (n x dim work) runs on the device; the two serial
+        // float sums of cpp:87 and cpp:95-96 (n dependent adds each, inherently
+        // sequential) run on the host over a pinned copy, in the reference's order.
+        PinnedBuf<float> hmind(n);
+        for (uint32_t c = 1; c < nlist; ++c) {
+            vdbk::launch_mindist_update(v_il.p, n, d4, cent_rm.p + (size_t)(c - 1) * dp, mind.p, stream);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipMemcpyAsync(hmind.p, mind.p, n * sizeof(float), hipMemcpyDeviceToHost, stream));
+            HIPCHECK(hipStreamSynchronize(stream));
+            const float* md = hmind.p;
+            float tot = 0.0f;
+            for (uint64_t v = 0; v < n; ++v) tot += md[v];
+            std::uniform_real_distribution<float> prob(0.0f, tot);
+            const float target = prob(gen);
+            float cumsum = 0.0f;
+            for (uint64_t v = 0; v < n; ++v) {
+                cumsum += md[v];
+                if (cumsum >= target) {
+                    HIPCHECK(hipMemcpyAsync(cent_rm.p + (size_t)c * dp, vpad + v * dp, dp * sizeof(float),
+                                            hipMemcpyDeviceToDevice, stream));
+                    break;
+                }
+            }
+        }
+
+        DevBuf<uint32_t> asg, skeys, order, counts, offsets;
+        asg.ensure(n);
+        for (int it = 0; it < 10; ++it) {
+            refresh_centroid_layout();
+            assign(vpad, n, asg.p);
+            group_by_key(asg.p, n, skeys, order);
+            std::vector<uint32_t> h = key_counts(asg.p, n, counts);
+            std::vector<uint32_t> off(nlist, 0);
+            for (uint32_t l = 1; l < nlist; ++l) off[l] = off[l - 1] + h[l - 1];
+            HIPCHECK(hipMemcpyAsync(offsets.ensure(nlist), off.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+            vdbk::launch_centroid_update(vpad, dp, order.p, offsets.p, counts.p, nlist, dim, cent_rm.p, stream);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipStreamSynchronize(stream));
+        }
+        refresh_centroid_layout();
+        HIPCHECK(hipStreamSynchronize(stream));
+    }
+
+    // ---- add: ivf_flat_index.cpp:148-202 ----
+    void add(const float* d_v, const uint64_t* d_ids, uint64_t n) {
+        if (n == 0) return;
+        require(!file_home(), "lists are served from a file (vdb_ivf_open_lists): the index is read-only",
+                VDB_ERR_STATE);
+        DevBuf<float> tmp;
+        const float* vpad = padded_rows(d_v, n, tmp);
+        DevBuf<uint32_t> asg;
+        assign(vpad, n, asg.ensure(n));
+        append(vpad, d_ids, asg.p, n);
+    }
+
+    // Append rows to the given lists, keeping input order within each list
+    // (cpp:160-192). `asg` holds one list id per row (device).
+    void append(const float* vpad, const uint64_t* d_ids, const uint32_t* asg, uint64_t n) {
+        require(!file_home(), "lists are served from a file (vdb_ivf_open_lists): the index is read-only",
+                VDB_ERR_STATE);
+        DevBuf<uint32_t> skeys, order, counts;
+        group_by_key(asg, n, skeys, order);
+        std::vector<uint32_t> added = key_counts(asg, n, counts);
+
+        std::vector<uint64_t> new_count(count);
+        for (uint32_t l = 0; l < nlist; ++l) new_count[l] += added[l];
+        const std::vector<uint64_t> old_count = count;
+        relayout(new_count, owned);
+
+        std::vector<uint64_t> group_start(nlist, 0), base(nlist, ~0ull);
+        for (uint32_t l = 1; l < nlist; ++l) group_start[l] = group_start[l - 1] + added[l - 1];
+        for (uint32_t l = 0; l < nlist; ++l)
+            if (owned[l]) base[l] = block_off[l] * 64 + old_count[l];
+        DevBuf<uint64_t> d_gs, d_base, dest;
+        HIPCHECK(hipMemcpyAsync(d_gs.ensure(nlist), group_start.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemcpyAsync(d_base.ensure(nlist), base.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+        vdbk::launch_slots_from_order(skeys.p, n, d_gs.p, d_base.p, dest.ensure(n), stream);
+        vdbk::launch_scatter_rows(vpad, d_ids, order.p, n, dp, dest.p, arena.p, arena_ids.p, stream);
+        HIPCHECK(hipGetLastError());
+        count = new_count;
+        total += n;
+        upload_directory();  // also waits for the stream before tmp buffers go
+    }
+
+    void set_shard(uint32_t r, uint32_t w) {
+        std::vector<uint32_t> owner(nlist);
+        vdb_shard_plan(count.data(), nlist, w, owner.data());
+        std::vector<uint8_t> new_owned(nlist);
+        for (uint32_t l = 0; l < nlist; ++l) new_owned[l] = owner[l] == r;
+        // Lists this handle no longer scans must have been stored here before.
+        for (uint32_t l = 0; l < nlist; ++l)
+            require(!new_owned[l] || owned[l] || count[l] == 0, "shard needs a list this handle dropped", VDB_ERR_STATE);
+        if (file_home()) {  // nothing in memory to move: the file holds every list
+            quiesce();
+            owned = new_owned;
+            cache_reset();
+        } else {
+            relayout(count, new_owned);
+        }
+        rank = r;
+        world = w;
+        upload_directory();
+    }
+
+    // Sharded build, for an index larger than one GPU (100M x 768 = 307 GB): the final
+    // list sizes (from an assignment pass) fix this handle's lists before any add, so
+    // appends store only the owned lists' rows and count the rest. The plan is the same
+    // LPT as set_shard, so a later set_shard(r, w) keeps the same lists.
+    void plan_shard(uint32_t r, uint32_t w, const uint64_t* final_sizes) {
+        require(total == 0, "plan_shard needs an empty index (call it between train and add)", VDB_ERR_STATE);
+        require(!file_home(), "lists are served from a file (vdb_ivf_open_lists)", VDB_ERR_STATE);
+        std::vector<uint32_t> owner(nlist);
+        vdb_shard_plan(final_sizes, nlist, w, owner.data());
+        std::vector<uint8_t> new_owned(nlist);
+        for (uint32_t l = 0; l < nlist; ++l) new_owned[l] = owner[l] == r;
+        relayout(count, new_owned);
+        rank = r;
+        world = w;
+        upload_directory();
+    }
+
+    EventSet& next_events() {
+        if (events_used == events.size()) {
+            EventSet e;
+            HIPCHECK(hipEventCreate(&e.begin));
+            HIPCHECK(hipEventCreate(&e.coarse_end));
+            HIPCHECK(hipEventCreate(&e.scan_begin));
+            HIPCHECK(hipEventCreate(&e.scan_end));
+            HIPCHECK(hipEventCreate(&e.end));
+            events.push_back(e);
+        }
+        return events[events_used++];
+    }
+
+    // Size every per-batch buffer of a slot for B queries up front; growing a buffer
+    // frees the old one, so first wait for the slot's previous batch.
+    void ensure_workspace(SearchSlot& w, uint32_t B, uint32_t P, uint32_t k) {
+        const size_t BP = (size_t)B * P;
+        const size_t max_items = (size_t)B * nseg_prefix[P];
+        const size_t max_l1 = max_items / vdbk::kMergeFan + BP;
+        const size_t max_wide = max_items / 4 + BP + 1;
+        const bool grow = w.items_w.cap < max_wide || w.qpad.cap < (size_t)B * dp || w.cd.cap < (size_t)B * nlist ||
+                          w.cdelta.cap < (size_t)B * nlist || w.cand.cap < (size_t)B * nlist ||
+                          w.probes.cap < BP || w.items.cap < max_items || w.part_d.cap < max_items * k ||
+                          w.slot_d.cap < BP * k || w.carry_d.cap < (size_t)P * k || w.l1_items.cap < max_l1 ||
+                          w.l1_d.cap < max_l1 * k;
+        if (!grow) return;
+        if (w.used) HIPCHECK(hipEventSynchronize(w.done));
+        w.qpad.ensure((size_t)B * dp);
+        w.cd.ensure((size_t)B * nlist);
+        w.cdelta.ensure((size_t)B * nlist);
+        w.cand.ensure((size_t)B * nlist);
+        w.probes.ensure(BP);
+        w.nseg_qp.ensure(BP);
+        w.pbqp.ensure(BP);
+        w.sorted_pair.ensure(BP);
+        w.pbs.ensure(BP);
+        w.counters.ensure(8);
+        w.l1base.ensure(BP);
+        w.l1_items.ensure(max_l1);
+        w.l1_d.ensure(max_l1 * k);
+        w.l1_i.ensure(max_l1 * k);
+        w.items.ensure(max_items);
+        w.items_w.ensure(max_wide);
+        w.part_d.ensure(max_items * k);
+        w.part_i.ensure(max_items * k);
+        w.slot_d.ensure(BP * k);
+        w.slot_i.ensure(BP * k);
+        w.carry_d.ensure((size_t)P * k);
+        w.carry_i.ensure((size_t)P * k);
+    }
+
+    // ---- search: ivf_flat_index.cpp:205-256, one batch of B queries ----
+    // Returns false (nothing merged, caller retries with fewer queries) when the tier's
+    // cache cannot hold every list the batch probes.
+    bool run_batch(SearchSlot& w, const float* d_q, uint32_t B, uint32_t P, uint32_t k, float* out_d_,
+                   uint64_t* out_i_, hipStream_t s, const uint32_t* req_start, uint32_t b0) {
+        const int regs_k = vdbk::topk_regs(k);
+        const int regs_p = vdbk::topk_regs(P);
+        const uint32_t group = (uint32_t)vdbk::scan_group(regs_k);
+        const uint32_t BP = B * P;
+        const uint64_t max_items = (uint64_t)B * nseg_prefix[P];
+        require(max_items < (1ull << 32), "batch too large", VDB_ERR_UNSUPPORTED);
+        EventSet* ev = prof ? &next_events() : nullptr;
+        if (ev) HIPCHECK(hipEventRecord(ev->begin, s));
+
+        vdbk::launch_pad_rows(d_q, B, dim, dp, w.qpad.p, s);
+        if (coarse_mode == 1 && metric != 2 && vdbk::rerank_rows(dp, regs_p) > 0) {
+            vdbk::launch_coarse_mfma(metric, cent_rm.p, nlist, dp, w.qpad.p, B, w.cd.p, w.cdelta.p, s);
+            vdbk::launch_select_rerank(metric, regs_p, w.cd.p, w.cdelta.p, cent_rm.p, nlist, dp, w.qpad.p, B, P,
+                                       w.cand.p, w.probes.p, s);
+        } else {
+            vdbk::launch_coarse(metric, cent_il.p, nlist, d4, w.qpad.p, B, w.cd.p, s);
+            vdbk::launch_select(regs_p, w.cd.p, nlist, B, P, w.probes.p, s);
+        }
+        if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
+        if (tiered() && resident_n < storable_n) {  // (everything cached: no host round trip)
+            HIPCHECK(hipMemcpyAsync(probe_stage.ensure(BP), w.probes.p, (size_t)BP * 4, hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            if (!make_resident(probe_stage.p, BP, s)) {
+                if (ev) --events_used;
+                return false;
+            }
+        }
+        // (tier: lists and directory entries another stream loaded must have landed)
+        if (tiered() && tier_ev_used) HIPCHECK(hipStreamWaitEvent(s, tier_ev, 0));
+        const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
+        const uint64_t max_wide = max_items / 4 + BP + 1;
+        const int waves = wide_group == 32 ? 8 : 4;  // workgroup shape of the wide scan
+        const bool wide = regs_k == 1 && wide_scan && vdbk::scan_wide_fits(d4, k, waves);
+        // segments per item: one per wave (more adds tail latency, no throughput)
+        const uint32_t segs_item = segs_item_opt ? segs_item_opt : (uint32_t)waves;
+        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? (int)wide_group : 0, segs_item, w.items.p, w.items_w.p,
+                          w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, s);
+        if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
+        vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
+                                w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
+                                wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item, 0};
+        if (wide && fused_scan) {
+            // one persistent grid takes both queues (no side stream, no fork/join)
+            // (narrow_blocks counts 4-wave workgroups: as many waves start on the narrow queue)
+            const uint32_t grid_cap = waves == 8 ? vdbk::kPersistentBlocks / 2 : vdbk::kPersistentBlocks;
+            sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks * 4 / waves, grid_cap / 2));
+            vdbk::launch_scan_wide(metric, (uint32_t)std::max<uint64_t>(max_wide, (max_items + 3) / 4), sa, s, waves);
+        } else if (wide) {
+            // narrow items on the side stream fill the CUs the wide items leave idle
+            HIPCHECK(hipEventRecord(w.fork, s));
+            HIPCHECK(hipStreamWaitEvent(w.side, w.fork, 0));
+            vdbk::launch_scan_narrow(metric, regs_k, std::min<uint32_t>((uint32_t)((max_items + 3) / 4), narrow_blocks), sa,
+                                     w.side);
+            HIPCHECK(hipEventRecord(w.join, w.side));
+            vdbk::launch_scan_wide(metric, (uint32_t)max_wide, sa, s, waves);
+            HIPCHECK(hipStreamWaitEvent(s, w.join, 0));
+        } else {
+            vdbk::launch_scan_narrow(metric, regs_k, (uint32_t)((max_items + 3) / 4), sa, s);
+        }
+        if (ev) HIPCHECK(hipEventRecord(ev->scan_end, s));
+        vdbk::launch_merge_partials(regs_k, (uint32_t)max_l1, w.probes.p, d_count_global.p, w.nseg_qp.p, w.pbqp.p, w.l1base.p,
+                                    w.l1_items.p, w.counters.p, w.part_d.p, w.part_i.p, k, w.l1_d.p, w.l1_i.p, s);
+        vdbk::launch_slot_merge(regs_k, w.probes.p, d_count_global.p, w.nseg_qp.p, w.pbqp.p, w.l1base.p, w.part_d.p, w.part_i.p,
+                                w.l1_d.p, w.l1_i.p, BP, k, w.slot_d.p, w.slot_i.p, s);
+        vdbk::launch_query_merge(regs_k, w.probes.p, d_count_global.p, w.slot_d.p, w.slot_i.p, w.carry_d.p, w.carry_i.p, B, P, k,
+                                 stale, req_start, b0, out_d_, out_i_, s);
+        if (stale)
+            vdbk::launch_carry(w.probes.p, d_count_global.p, B, P, k, w.slot_d.p, w.slot_i.p, req_start, b0, w.carry_d.p,
+                               w.carry_i.p, s);
+        if (ev) HIPCHECK(hipEventRecord(ev->end, s));
+        HIPCHECK(hipGetLastError());
+        return true;
+    }
+
+    // req_start: null (one reference search() call) or, for a coalesced batch of calls,
+    // per query the call-global index of its request's first query (device memory).
+    void search_device(const float* d_q, uint32_t n, uint32_t nprobe, uint32_t k, float* d_dist, uint64_t* d_ids,
+                       hipStream_t s, const uint32_t* req_start = nullptr) {
+        if (n == 0 || k == 0) return;
+        require(k <= (uint32_t)vdbk::kMaxK, "k above 1024 is not supported", VDB_ERR_UNSUPPORTED);
+        const uint32_t P = std::min(nprobe, nlist);  // cpp:218-222 reads out of bounds beyond nlist
+        if (P == 0) {
+            vdbk::launch_fill_empty((uint64_t)n * k, d_dist, d_ids, s);
+            HIPCHECK(hipGetLastError());
+            return;
+        }
+        require(P <= (uint32_t)vdbk::kMaxK, "nprobe above 1024 is not supported", VDB_ERR_UNSUPPORTED);
+        if (!stats.p) {
+            stats.ensure(8);
+            HIPCHECK(hipMemsetAsync(stats.p, 0, 64, s));
+        }
+        const uint32_t bmax = std::max<uint32_t>(1, std::min<uint32_t>(batch, vdbk::kPlanMaxPairs / P));
+        SearchSlot& w = slots[next_slot];
+        next_slot = (next_slot + 1) % kSlots;
+        ensure_workspace(w, std::min(bmax, n), P, k);
+        if (w.used) HIPCHECK(hipStreamWaitEvent(s, w.done, 0));
+        // Probe-slot contents live for one search call (cpp:210-211).
+        HIPCHECK(hipMemsetAsync(w.carry_i.p, 0xFF, (size_t)P * k * 8, s));
+        for (uint32_t b0 = 0, B = std::min(bmax, n); b0 < n; b0 += B, B = std::min(B, n - b0)) {
+            // (list-cache tier: a batch whose probed lists overflow the cache is halved)
+            while (!run_batch(w, d_q + (size_t)b0 * dim, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s,
+                              req_start, b0)) {
+                require(B > 1, "list_cache_bytes cannot hold the lists one query probes", VDB_ERR_OUT_OF_MEMORY);
+                B = (B + 1) / 2;
+            }
+        }
+        HIPCHECK(hipEventRecord(w.done, s));
+        w.used = true;
+    }
+};

@@ -167,7 +167,15 @@ class QueryService:
     def load_index(self, request):
         if not self.data_path:
             return "FAILED_PRECONDITION", "server has no data path", None
-        base = os.path.join(self.data_path, request.index, request.epoch)
+        # names are single path components: no separators, no '..', nothing that
+        # resolves outside --data-path (the reference concatenates them unchecked)
+        for part in (request.index, request.epoch):
+            if not part or part in (".", "..") or "/" in part or "\\" in part or "\0" in part:
+                return "INVALID_ARGUMENT", "index and epoch must be plain names", None
+        root = os.path.realpath(self.data_path)
+        base = os.path.join(root, request.index, request.epoch)
+        if os.path.commonpath([root, os.path.realpath(base + ".ivf")]) != root:
+            return "INVALID_ARGUMENT", "index path leaves the data path", None
         try:
             with open(base + ".json") as f:
                 meta = json.load(f)

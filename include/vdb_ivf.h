@@ -173,7 +173,11 @@ int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
  * first; the handle becomes read-only (add fails with VDB_ERR_STATE). */
 int vdb_ivf_open_lists(vdb_ivf* index, const char* path);
 
+/* get_gpu_memory_usage's definition: count * (dim * 4 + 8) bytes per GPU-resident list. */
 uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* index);
+/* HBM this handle really holds for lists and centroids (64-row blocks, dimension padding,
+ * the scan's slack block, the whole cache in the list-cache tier). */
+uint64_t vdb_ivf_gpu_bytes_allocated(const vdb_ivf* index);
 uint64_t vdb_ivf_ntotal(const vdb_ivf* index);
 uint32_t vdb_ivf_dimension(const vdb_ivf* index);
 uint32_t vdb_ivf_nlist(const vdb_ivf* index);

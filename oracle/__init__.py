@@ -53,6 +53,7 @@ def lib():
             "oracle_search": (None, [vp, _f32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _f32p, _u64p]),
             "oracle_search_mt": (None, [vp, _f32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _f32p, _u64p, ctypes.c_int]),
             "oracle_search_shard": (None, [vp, _f32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p, _f32p, _u64p]),
+            "oracle_search_shard_mt": (None, [vp, _f32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p, _f32p, _u64p, ctypes.c_int]),
             "oracle_merge_ranks": (None, [_f32p, _u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _f32p, _u64p]),
             "oracle_select_nprobe": (None, [vp, _f32p, ctypes.c_uint32, _u32p]),
             "oracle_assign": (None, [vp, _f32p, ctypes.c_uint64, _u32p]),
@@ -130,13 +131,17 @@ class OracleIndex:
             lib().oracle_search_mt(self._h, _p(q, _f32p), n, nprobe, k, _p(D, _f32p), _p(I, _u64p), threads)
         return D, I
 
-    def search_shard(self, queries: np.ndarray, nprobe: int, k: int, owned: np.ndarray):
+    def search_shard(self, queries: np.ndarray, nprobe: int, k: int, owned: np.ndarray, threads: int = 1):
         q = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, self.dim)
         o = np.ascontiguousarray(owned, dtype=np.uint8)
         n = q.shape[0]
         D = np.empty((n, k), dtype=np.float32)
         I = np.empty((n, k), dtype=np.uint64)
-        lib().oracle_search_shard(self._h, _p(q, _f32p), n, nprobe, k, _p(o, _u8p), _p(D, _f32p), _p(I, _u64p))
+        if threads == 1:
+            lib().oracle_search_shard(self._h, _p(q, _f32p), n, nprobe, k, _p(o, _u8p), _p(D, _f32p), _p(I, _u64p))
+        else:
+            lib().oracle_search_shard_mt(self._h, _p(q, _f32p), n, nprobe, k, _p(o, _u8p), _p(D, _f32p),
+                                         _p(I, _u64p), threads)
         return D, I
 
     def select_nprobe(self, query: np.ndarray, nprobe: int) -> np.ndarray:

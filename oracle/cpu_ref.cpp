@@ -328,6 +328,36 @@ void oracle_search_shard(oracle_ivf* h, const float* queries, uint32_t n, uint32
         });
 }
 
+// oracle_search_shard with the scans of the (query, probe) pairs in parallel and the
+// slot logic replayed serially afterwards (bit-identical to the serial version).
+void oracle_search_shard_mt(oracle_ivf* h, const float* queries, uint32_t n, uint32_t nprobe, uint32_t k,
+                            const uint8_t* owned, float* D, uint64_t* I, int threads) {
+    static const std::vector<Cand> kEmpty;
+    const uint32_t P = std::min(nprobe, h->nlist);
+    std::vector<std::vector<uint32_t>> probes(n);
+    for (uint32_t q = 0; q < n; ++q) probes[q] = h->select(queries + (size_t)q * h->dim, nprobe);
+    std::vector<std::vector<Cand>> res((size_t)n * P);
+#ifdef _OPENMP
+    int nt = threads > 0 ? threads : omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+#endif
+    for (int64_t e = 0; e < (int64_t)n * P; ++e) {
+        const uint32_t q = (uint32_t)(e / P), p = (uint32_t)(e % P);
+        const uint32_t l = probes[q][p];
+        if (!owned[l] || h->lists[l].count == 0) continue;
+        h->scan_list(l, queries + (size_t)q * h->dim, std::min<uint64_t>(k, h->lists[l].count), res[e]);
+    }
+    (void)threads;
+    run_search(
+        h, queries, n, nprobe,
+        [&](uint32_t q, uint32_t p, uint32_t, const float*, std::vector<Cand>& out) { out = res[(size_t)q * P + p]; },
+        [&](uint32_t q, const std::vector<Slot>& slots) {
+            std::vector<const std::vector<Cand>*> ptrs;
+            for (const Slot& s : slots) ptrs.push_back(s.source >= 0 && owned[s.source] ? &s.res : &kEmpty);
+            merge(ptrs, k, D + (size_t)q * k, I + (size_t)q * k);
+        });
+}
+
 void oracle_merge_ranks(const float* dist, const uint64_t* ids, uint32_t nranks, uint32_t n,
                         uint32_t k, float* out_dist, uint64_t* out_ids) {
     for (uint32_t q = 0; q < n; ++q) {

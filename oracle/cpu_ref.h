@@ -45,6 +45,8 @@ void oracle_search_mt(oracle_ivf* h, const float* queries, uint32_t n, uint32_t 
  * partials equals oracle_search. */
 void oracle_search_shard(oracle_ivf* h, const float* queries, uint32_t n, uint32_t nprobe,
                          uint32_t k, const uint8_t* owned, float* distances, uint64_t* indices);
+void oracle_search_shard_mt(oracle_ivf* h, const float* queries, uint32_t n, uint32_t nprobe, uint32_t k,
+                            const uint8_t* owned, float* D, uint64_t* I, int threads);
 void oracle_merge_ranks(const float* dist, const uint64_t* ids, uint32_t nranks, uint32_t n,
                         uint32_t k, float* out_dist, uint64_t* out_ids);
 

@@ -138,6 +138,9 @@ def test_shard_decomposition(world):
     parts = [o.search_shard(Q, 7, 10, (owner == r).astype(np.uint8)) for r in range(world)]
     Dm, Im = oracle.merge_ranks(np.stack([p[0] for p in parts]), np.stack([p[1] for p in parts]), 10)
     assert np.array_equal(Im, I) and np.array_equal(bits(Dm), bits(D))
+    for r in range(world):  # the parallel shard search (large-config GPU tests) is bit-identical
+        Dt, It = o.search_shard(Q, 7, 10, (owner == r).astype(np.uint8), threads=4)
+        assert np.array_equal(It, parts[r][1]) and np.array_equal(bits(Dt), bits(parts[r][0]))
 
 
 def test_count_only_lists_keep_shard_results():

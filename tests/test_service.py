@@ -130,3 +130,16 @@ def test_cli_accepts_both_flag_forms(monkeypatch):
         service.main(["--address=127.0.0.1:6000", "--data-path", "/tmp/x", "--workers=3", "--batch-size=64",
                       "--coalesce-window", "2"])
     assert seen == {"address": "127.0.0.1:6000", "workers": 3, "data": "/tmp/x"}
+
+
+def test_load_index_rejects_paths_outside_data_path(tmp_path):
+    # LoadIndex builds <data_path>/<index>/<epoch>; a network caller must not be able to
+    # name a file outside --data-path (query_service.cpp:218-265 concatenates unchecked)
+    (tmp_path / "outside.json").write_text('{"dimension": 4, "nlist": 1}')
+    svc = service.QueryService(str(tmp_path / "data"))
+    for index, epoch in (("..", "outside"), ("a/../..", "outside"), ("/etc", "passwd"), ("idx", "../../outside"),
+                         ("", "e"), ("idx", "")):
+        st, detail, _ = svc.load_index(M["LoadIndexRequest"](index=index, epoch=epoch))
+        assert st == "INVALID_ARGUMENT", (index, epoch, st, detail)
+    st, _, _ = svc.load_index(M["LoadIndexRequest"](index="idx", epoch="e1"))
+    assert st == "NOT_FOUND"

@@ -30,7 +30,7 @@ run() {  # run <name> <seconds> <cmd...>: stop the session on any failure
 nproc > "$O/nproc.txt"
 lscpu > "$O/lscpu.txt" 2>/dev/null
 if has tests; then
-    run pytest 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread
+    run pytest 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread
     tail -3 "$O/pytest.log"
 fi
 if has smoke; then
@@ -44,7 +44,9 @@ if has bench; then
 fi
 if has multi; then
     # one-GPU rehearsal of the N-rank path: 2 ranks on cuda:0, gloo exchange staged through host
-    run multi 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --same-device --dist-backend gloo --steps 20 --warmup 3 --no-cpu --prof-steps 4
+    # bench.py launches its own ranks (one process per GPU); with one GPU on the box the
+    # two ranks share it and exchange through host memory (a protocol rehearsal)
+    run multi 600 python -u bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu --prof-steps 4
     grep '^{' "$O/multi.log" > "$O/multi.json"
     cat "$O/multi.json"
 fi
@@ -54,7 +56,7 @@ if has grpc; then
     cat "$O/grpc.json"
 fi
 if has dump; then
-    run dump 600 python -u tests/debug_dump_index.py 10000000 4096
+    run dump 600 python -u tools/debug_dump_index.py 10000000 4096
 fi
 if has prof; then
     run prof 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight 1 $BARGS
