@@ -278,8 +278,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check-batches", type=int, default=4,
                     help="N>1: timed batches checked bit-for-bit against the unsharded index")
+    ap.add_argument("--exchange", default="engine", choices=["engine", "torch"],
+                    help="N ranks: engine = the engine's own RCCL all-gather + merge inside vdb_ivf_search_device "
+                         "(vdb_ivf_attach_comm); torch = the same packed records through torch.distributed")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo: rehearse the multi-rank path with host-staged exchange")
+                    help="--exchange torch: nccl (RCCL) or gloo (host-staged rehearsal)")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (one-GPU rehearsal)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight (streams) in the timed region; 0 = 2 on one GPU (3 measured no faster, "
@@ -322,12 +325,16 @@ def main():
         # fewer GPUs than ranks: a rehearsal of the N-rank protocol on the GPUs present,
         # with the exchange staged through host memory (RCCL wants one rank per GPU)
         args.same_device = True
-        args.dist_backend = "gloo"
+    if world > 1 and args.same_device:  # RCCL wants one rank per GPU
+        args.exchange, args.dist_backend = "torch", "gloo"
     args.rehearsal = world > 1 and args.same_device
+    # control traffic (barriers, the timing max, the comm id) goes over gloo unless the
+    # exchange itself is torch's nccl
+    args.ctrl_dev = "cuda" if (args.exchange == "torch" and args.dist_backend == "nccl") else "cpu"
     device = torch.device("cuda", local_rank % max(ndev, 1) if args.same_device else local_rank)
     torch.cuda.set_device(device)
     if world > 1:
-        if args.dist_backend == "nccl":
+        if args.ctrl_dev == "cuda":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group("gloo")
@@ -373,6 +380,13 @@ def run(vdb, args, device, rank, world):
         torch.cuda.synchronize()
         check = (q0, nchk, chk_d, chk_i)
         idx.set_shard(rank, world)
+    if world > 1 and args.exchange == "engine":
+        # the engine's own communicator: rank 0 draws the RCCL id, the others receive it
+        cid = torch.zeros(vdb.COMM_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            cid.copy_(torch.frombuffer(bytearray(vdb.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(cid, src=0)
+        idx.attach_comm(bytes(cid.numpy().tobytes()), rank, world)
     # Batches in flight: step s runs on streams[s % inflight]; the engine gives each
     # concurrent search its own workspace slot, so one batch's small kernels and scan
     # tail overlap the next batch's scan. Rank partials and gathers are per stream.
@@ -389,7 +403,7 @@ def run(vdb, args, device, rank, world):
         st = streams[slot]
         q = queries[s * B:(s + 1) * B]
         with torch.cuda.stream(st):
-            if world == 1:
+            if world == 1 or args.exchange == "engine":  # (engine exchange: final results on every rank)
                 idx.search_device(q.data_ptr(), B, args.nprobe, k, out_d[s * B:].data_ptr(), out_i[s * B:].data_ptr(),
                                   st.cuda_stream)
             else:
@@ -427,18 +441,13 @@ def run(vdb, args, device, rank, world):
         q0, nchk, chk_d, chk_i = check
         same = bool(torch.equal(out_i[q0:q0 + nchk], chk_i) and
                     torch.equal(out_d[q0:q0 + nchk].view(torch.int32), chk_d.view(torch.int32)))
-        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=device)
-        if args.dist_backend == "nccl":
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        else:
-            hf = flag.cpu()
-            dist.all_reduce(hf, op=dist.ReduceOp.MIN)
-            flag = hf
+        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=device if args.ctrl_dev == "cuda" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         parity_multi = bool(int(flag.item()) == 1)
     lat = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     p99 = percentile(lat, 0.99)
     if world > 1:
-        t = torch.tensor([elapsed, p99], dtype=torch.float64, device=device if args.dist_backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed, p99], dtype=torch.float64, device=device if args.ctrl_dev == "cuda" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, p99 = float(t[0]), float(t[1])
 
@@ -459,7 +468,7 @@ def run(vdb, args, device, rank, world):
     idx.profile_enable(False)
     p99_single = percentile([a.elapsed_time(b) for a, b in zip(s_ev, e_ev)], 0.99)
     if world > 1:
-        t = torch.tensor([p99_single], dtype=torch.float64, device=device if args.dist_backend == "nccl" else "cpu")
+        t = torch.tensor([p99_single], dtype=torch.float64, device=device if args.ctrl_dev == "cuda" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         p99_single = float(t[0])
 
@@ -502,7 +511,8 @@ def run(vdb, args, device, rank, world):
             "nvec": args.nvec, "dim": args.dim, "nlist": args.nlist, "nprobe": args.nprobe, "batch": B, "k": k,
             "train_vectors": min(args.train, args.nvec),
             "parallelism": (f"lists sharded over {world} rank(s) (LPT), one all-gather per batch of per-rank top-k "
-                            f"({'RCCL' if args.dist_backend == 'nccl' else 'gloo, host-staged rehearsal'})"
+                            + (" (engine RCCL communicator, vdb_ivf_attach_comm)" if args.exchange == "engine" else
+                               f" (torch.distributed {'RCCL' if args.dist_backend == 'nccl' else 'gloo, host-staged'})")
                             if world > 1 else "single GPU") + f"; {args.inflight} batches in flight",
         },
         "roofline": {

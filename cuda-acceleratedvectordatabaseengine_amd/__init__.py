@@ -131,6 +131,12 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_synchronize": (ctypes.c_int, [vp]),
         "vdb_ivf_stream": (vp, [vp]),
         "vdb_gen_normal_device": (ctypes.c_int, [vp, u64, u64, u64, vp]),
+        "vdb_comm_unique_id": (ctypes.c_int, [vp]),
+        "vdb_ivf_attach_comm": (ctypes.c_int, [vp, vp, u32, u32]),
+        "vdb_ivf_detach_comm": (ctypes.c_int, [vp]),
+        "vdb_ivf_create_group": (ctypes.c_int, [ctypes.POINTER(_Config), vp, u32, ctypes.POINTER(vp)]),
+        "vdb_ivf_group_size": (u32, [vp]),
+        "vdb_ivf_list_owners": (ctypes.c_int, [vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -175,6 +181,16 @@ def merge_ranks_device(dist_ptr: int, ids_ptr: int, nranks: int, n: int, k: int,
                                         ctypes.c_void_p(stream or 0)))
 
 
+COMM_ID_BYTES = 128  # VDB_COMM_ID_BYTES
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL communicator id (rank 0 draws it and shares it with the other ranks)."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    _check(lib().vdb_comm_unique_id(buf))
+    return buf.raw
+
+
 def rank_record_bytes(n: int, k: int) -> int:
     """Bytes of one rank's packed partial record (f32 dist [n][k], pad to 8, u64 ids [n][k])."""
     return int(lib().vdb_rank_record_bytes(n, k))
@@ -202,6 +218,7 @@ class IVFFlatIndex:
         use_gpu: bool = True
         max_gpu_memory: int = 8 << 30
         device: int = 0
+        devices: tuple = ()  # > 1 entries: one index sharded by list over these GPUs (group handle)
 
     @dataclass
     class SearchParams:
@@ -216,7 +233,11 @@ class IVFFlatIndex:
         c = _Config(config.dimension, config.nlist, int(config.metric), int(config.use_gpu),
                     config.max_gpu_memory, config.device)
         h = ctypes.c_void_p()
-        _check(lib().vdb_ivf_create(ctypes.byref(c), ctypes.byref(h)))
+        if config.devices:
+            devs = (ctypes.c_int * len(config.devices))(*config.devices)
+            _check(lib().vdb_ivf_create_group(ctypes.byref(c), devs, len(config.devices), ctypes.byref(h)))
+        else:
+            _check(lib().vdb_ivf_create(ctypes.byref(c), ctypes.byref(h)))
         self._h = h
 
     def close(self):
@@ -309,6 +330,26 @@ class IVFFlatIndex:
     # ---- sharding ----
     def set_shard(self, rank: int, world: int):
         _check(lib().vdb_ivf_set_shard(self._h, rank, world))
+
+    def attach_comm(self, comm_id: bytes, rank: int, world: int):
+        """Join the RCCL communicator `comm_id` as `rank` of `world` (after set_shard /
+        plan_shard with the same rank and world): searches then return final results."""
+        if len(comm_id) != COMM_ID_BYTES:
+            raise ValueError("comm_id must be COMM_ID_BYTES long")
+        _check(lib().vdb_ivf_attach_comm(self._h, ctypes.c_char_p(comm_id), rank, world))
+
+    def detach_comm(self):
+        _check(lib().vdb_ivf_detach_comm(self._h))
+
+    @property
+    def group_size(self) -> int:
+        return int(lib().vdb_ivf_group_size(self._h))
+
+    def list_owners(self) -> np.ndarray:
+        """Per list: the member (group) or rank (shard) storing it; 2**32 - 1 = none."""
+        out = np.empty(self.config.nlist, dtype=np.uint32)
+        _check(lib().vdb_ivf_list_owners(self._h, _ptr(out)))
+        return out
 
     def plan_shard(self, rank: int, world: int, final_sizes):
         """Sharded build: fix this rank's lists from the final list sizes before any add."""

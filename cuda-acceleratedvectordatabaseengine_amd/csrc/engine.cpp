@@ -4,6 +4,21 @@
 
 namespace vdbe {
 thread_local std::string g_last_error;
+
+namespace group {  // group.cpp: the same calls on a group handle (one member per device)
+void train_device(vdb_ivf* g, const float* d_v, uint64_t n);
+void set_centroids(vdb_ivf* g, const float* c);
+void add_host(vdb_ivf* g, const float* v, const uint64_t* ids, const uint32_t* lists, uint64_t n);
+void add_device(vdb_ivf* g, const float* d_v, const uint64_t* d_ids, const uint32_t* d_lists, uint64_t n);
+uint64_t gpu_bytes(const vdb_ivf* g, bool allocated);
+void set_option(vdb_ivf* g, const std::string& name, int64_t value);
+void synchronize(vdb_ivf* g);
+}  // namespace group
+
+// Calls that act on one device's shard have no group meaning.
+inline void no_group(const vdb_ivf* h, const char* what) {
+    require(!h->is_group(), std::string(what) + " is not available on a group handle", VDB_ERR_UNSUPPORTED);
+}
 }  // namespace vdbe
 
 extern "C" {
@@ -77,6 +92,11 @@ int vdb_ivf_train(vdb_ivf* h, const float* v, uint64_t n) {
         require(n > 0, "train needs at least one vector");
         DevBuf<float> dv;
         HIPCHECK(hipMemcpyAsync(dv.ensure(n * h->dim), v, n * h->dim * 4, hipMemcpyHostToDevice, h->stream));
+        if (h->is_group()) {
+            HIPCHECK(hipStreamSynchronize(h->stream));
+            group::train_device(h, dv.p, n);
+            return;
+        }
         h->train(dv.p, n);
     });
 }
@@ -86,6 +106,7 @@ int vdb_ivf_train_device(vdb_ivf* h, const float* d_v, uint64_t n) {
         require(h && (d_v || n == 0), "null argument");
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
+        if (h->is_group()) return group::train_device(h, d_v, n);
         h->train(d_v, n);
     });
 }
@@ -95,6 +116,7 @@ int vdb_ivf_set_centroids(vdb_ivf* h, const float* c) {
         require(h && c, "null argument");
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
+        if (h->is_group()) return group::set_centroids(h, c);
         h->set_centroids_host(c);
     });
 }
@@ -104,7 +126,9 @@ int vdb_ivf_get_centroids(vdb_ivf* h, float* c) {
         require(h && c, "null argument");
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
-        h->export_centroids(c);
+        h->head()->set_device();
+        h->head()->export_centroids(c);
+        h->set_device();
     });
 }
 
@@ -114,6 +138,7 @@ int vdb_ivf_add(vdb_ivf* h, const float* v, const uint64_t* ids, uint64_t n) {
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
         if (n == 0) return;
+        if (h->is_group()) return group::add_host(h, v, ids, nullptr, n);
         DevBuf<float> dv;
         DevBuf<uint64_t> di;
         HIPCHECK(hipMemcpyAsync(dv.ensure(n * h->dim), v, n * h->dim * 4, hipMemcpyHostToDevice, h->stream));
@@ -128,6 +153,7 @@ int vdb_ivf_add_device(vdb_ivf* h, const float* d_v, const uint64_t* d_ids, uint
         require(h && ((d_v && d_ids) || n == 0), "null argument");
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
+        if (h->is_group()) return group::add_device(h, d_v, d_ids, nullptr, n);
         h->add(d_v, d_ids, n);
         HIPCHECK(hipStreamSynchronize(h->stream));
     });
@@ -138,6 +164,7 @@ int vdb_ivf_add_to_lists(vdb_ivf* h, const float* v, const uint64_t* ids, const 
         require(h && ((v && ids && lists) || n == 0), "null argument");
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
+        if (h->is_group()) return group::add_host(h, v, ids, lists, n);
         h->add_to_lists_host(v, ids, lists, n);
     });
 }
@@ -148,9 +175,12 @@ int vdb_ivf_assign_device(vdb_ivf* h, const float* d_v, uint64_t n, uint32_t* d_
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
         if (n == 0) return;
+        vdb_ivf* a = h->head();  // a group assigns on its first member (device of d_v)
+        a->set_device();
         DevBuf<float> tmp;
-        h->assign(h->padded_rows(d_v, n, tmp), n, d_lists);
-        HIPCHECK(hipStreamSynchronize(h->stream));
+        a->assign(a->padded_rows(d_v, n, tmp), n, d_lists);
+        HIPCHECK(hipStreamSynchronize(a->stream));
+        h->set_device();
     });
 }
 
@@ -161,6 +191,7 @@ int vdb_ivf_add_to_lists_device(vdb_ivf* h, const float* d_v, const uint64_t* d_
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
         if (n == 0) return;
+        if (h->is_group()) return group::add_device(h, d_v, d_ids, d_lists, n);
         // The grouping kernels index per-list arrays by these ids: check them first.
         std::vector<uint32_t> hl(n);
         HIPCHECK(hipMemcpyAsync(hl.data(), d_lists, n * 4, hipMemcpyDeviceToHost, h->stream));
@@ -177,6 +208,7 @@ int vdb_ivf_plan_shard(vdb_ivf* h, uint32_t rank, uint32_t world, const uint64_t
         require(h && final_sizes && world > 0 && rank < world, "invalid shard");
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
+        no_group(h, "plan_shard");
         h->plan_shard(rank, world, final_sizes);
     });
 }
@@ -190,7 +222,8 @@ int vdb_ivf_save(vdb_ivf* h, const char* path) {
         // disagree with the rows written.
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
-        require(h->world == 1, "save a sharded handle from every rank's full copy instead", VDB_ERR_STATE);
+        require(h->is_group() || h->world == 1, "save a sharded handle from every rank's full copy instead",
+                VDB_ERR_STATE);
         if (h->file_home()) {  // fopen("wb") would truncate the file the lists are served from
             struct stat a, b;
             if (::stat(path, &a) == 0 && ::fstat(h->home_fd, &b) == 0)
@@ -210,7 +243,8 @@ int vdb_ivf_save(vdb_ivf* h, const char* path) {
             put("VDBIVF01", 8);
             put(hdr, sizeof(hdr));
             std::vector<float> c((size_t)h->nlist * h->dim);
-            h->export_centroids(c.data());
+            h->head()->set_device();
+            h->head()->export_centroids(c.data());
             put(c.data(), c.size() * 4);
             std::vector<float> v;
             std::vector<uint64_t> ids;
@@ -218,7 +252,9 @@ int vdb_ivf_save(vdb_ivf* h, const char* path) {
                 const uint64_t cnt = h->count[l];
                 v.resize(cnt * h->dim);
                 ids.resize(cnt);
-                h->export_list(l, v.data(), ids.data());
+                vdb_ivf* st = h->store_of(l);  // (a group: the member storing the list)
+                st->set_device();
+                st->export_list(l, v.data(), ids.data());
                 put(&cnt, 8);
                 put(ids.data(), cnt * 8);
                 put(v.data(), v.size() * 4);
@@ -283,12 +319,19 @@ int vdb_ivf_load(vdb_ivf* h, const char* path) {
         h->set_device();
         require(h->total == 0, "load() needs an empty index (this one holds vectors)", VDB_ERR_STATE);
         std::vector<float> old((size_t)h->nlist * h->dim);
-        h->export_centroids(old.data());
-        h->set_centroids_host(c.data());
+        h->head()->set_device();
+        h->head()->export_centroids(old.data());
+        h->set_device();
+        auto set_c = [&](const float* cc) {
+            if (h->is_group()) group::set_centroids(h, cc);
+            else h->set_centroids_host(cc);
+        };
+        set_c(c.data());
         try {
-            h->add_to_lists_host(vs.data(), is.data(), ls.data(), is.size());
+            if (h->is_group()) group::add_host(h, vs.data(), is.data(), ls.data(), is.size());
+            else h->add_to_lists_host(vs.data(), is.data(), ls.data(), is.size());
         } catch (...) {
-            h->set_centroids_host(old.data());  // all or nothing: the empty handle keeps its centroids
+            set_c(old.data());  // all or nothing: the empty handle keeps its centroids
             throw;
         }
     });
@@ -325,6 +368,7 @@ int vdb_ivf_set_shard(vdb_ivf* h, uint32_t rank, uint32_t world) {
         require(h && world > 0 && rank < world, "invalid shard");
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
+        no_group(h, "set_shard");
         h->set_shard(rank, world);
     });
 }
@@ -387,7 +431,7 @@ int vdb_ivf_warmup(vdb_ivf* h, const uint32_t* lists, uint32_t n) {
         // each list is loaded like load_list_to_gpu (ivf_flat_index.cpp:387-444): one
         // that cannot fit the cache is skipped (the reference returns false).
         std::lock_guard<std::mutex> g(h->mu);
-        if (!h->tiered()) return;
+        if (h->is_group() || !h->tiered()) return;  // (a group keeps every list HBM-resident)
         h->set_device();
         for (uint32_t i = 0; i < n; ++i) (void)h->make_resident(lists + i, 1, h->stream);
         HIPCHECK(hipStreamSynchronize(h->stream));
@@ -400,7 +444,7 @@ int vdb_ivf_evict(vdb_ivf* h, uint32_t list) {
         // Without the tier residency is permanent and eviction is a no-op; in the tier
         // the list leaves the cache (evict_list_from_gpu, ivf_flat_index.cpp:447-471).
         std::lock_guard<std::mutex> g(h->mu);
-        if (!h->tiered() || h->cache_off[list] == vdb_ivf::kAbsent) return;
+        if (h->is_group() || !h->tiered() || h->cache_off[list] == vdb_ivf::kAbsent) return;
         h->set_device();
         h->quiesce();
         h->cache_free(list);
@@ -413,6 +457,7 @@ int vdb_ivf_evict(vdb_ivf* h, uint32_t list) {
 uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* h) {
     if (!h) return 0;
     std::lock_guard<std::mutex> g(h->mu);
+    if (h->is_group()) return group::gpu_bytes(h, false);
     uint64_t b = 0;
     for (uint32_t l = 0; l < h->nlist; ++l) {
         const bool resident = h->tiered() ? h->cache_off[l] != vdb_ivf::kAbsent : (bool)h->owned[l];
@@ -424,6 +469,7 @@ uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* h) {
 uint64_t vdb_ivf_gpu_bytes_allocated(const vdb_ivf* h) {
     if (!h) return 0;
     std::lock_guard<std::mutex> g(h->mu);
+    if (h->is_group()) return group::gpu_bytes(h, true);
     const uint64_t cent = (uint64_t)h->nlist * h->dp * 8;  // row-major + interleaved copies
     if (h->tiered()) return (h->cache_blocks + 1) * vdb_ivf::block_bytes(h->dp) + cent;
     return (h->arena_blocks + (h->arena_blocks ? 1 : 0)) * vdb_ivf::block_bytes(h->dp) + cent;
@@ -444,8 +490,10 @@ int vdb_ivf_get_list(vdb_ivf* h, uint32_t list, float* vectors, uint64_t* ids) {
     return guarded([&] {
         require(h && list < h->nlist, "list id out of range");
         std::lock_guard<std::mutex> g(h->mu);
+        vdb_ivf* st = h->store_of(list);
+        st->set_device();
+        st->export_list(list, vectors, ids);
         h->set_device();
-        h->export_list(list, vectors, ids);
     });
 }
 
@@ -453,6 +501,7 @@ int vdb_ivf_set_batch(vdb_ivf* h, uint32_t batch) {
     return guarded([&] {
         require(h && batch > 0, "invalid batch");
         std::lock_guard<std::mutex> g(h->mu);
+        if (h->is_group()) return group::set_option(h, "batch", batch);
         h->batch = batch;
     });
 }
@@ -461,6 +510,7 @@ int vdb_ivf_set_stale_slots(vdb_ivf* h, int enable) {
     return guarded([&] {
         require(h, "null handle");
         std::lock_guard<std::mutex> g(h->mu);
+        if (h->is_group()) return group::set_option(h, "stale_slots", enable ? 1 : 0);
         h->stale = enable ? 1 : 0;
     });
 }
@@ -470,6 +520,7 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         require(h && name, "null argument");
         std::lock_guard<std::mutex> g(h->mu);
         const std::string n(name);
+        if (h->is_group()) return group::set_option(h, n, value);
         if (n == "coarse_mode") {
             require(value == 0 || value == 1, "coarse_mode is 0 or 1");
             h->coarse_mode = (int)value;
@@ -540,6 +591,7 @@ int vdb_ivf_open_lists(vdb_ivf* h, const char* path) {
     return guarded([&] {
         require(h && path, "null argument");
         std::lock_guard<std::mutex> g(h->mu);
+        no_group(h, "open_lists");
         h->set_device();
         h->open_lists(path);
     });
@@ -562,6 +614,7 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* h, int mode) {
     return guarded([&] {
         require(h && (mode == 0 || mode == 1), "coarse mode is 0 (exact VALU) or 1 (MFMA + exact re-rank)");
         std::lock_guard<std::mutex> g(h->mu);
+        if (h->is_group()) return group::set_option(h, "coarse_mode", mode);
         h->coarse_mode = mode;
     });
 }
@@ -570,7 +623,7 @@ int vdb_ivf_profile_enable(vdb_ivf* h, int enable) {
     return guarded([&] {
         require(h, "null handle");
         std::lock_guard<std::mutex> g(h->mu);
-        h->prof = enable != 0;
+        h->head()->prof = enable != 0;  // (a group: its first member, rank 0)
     });
 }
 
@@ -578,18 +631,24 @@ int vdb_ivf_profile_reset(vdb_ivf* h) {
     return guarded([&] {
         require(h, "null handle");
         std::lock_guard<std::mutex> g(h->mu);
-        h->set_device();
+        if (h->is_group()) group::synchronize(h);
+        vdb_ivf* p = h->head();
+        p->set_device();
         HIPCHECK(hipDeviceSynchronize());
-        h->events_used = 0;
-        HIPCHECK(hipMemsetAsync(h->stats.ensure(8), 0, 64, h->stream));
-        HIPCHECK(hipStreamSynchronize(h->stream));
+        p->events_used = 0;
+        HIPCHECK(hipMemsetAsync(p->stats.ensure(8), 0, 64, p->stream));
+        HIPCHECK(hipStreamSynchronize(p->stream));
+        h->set_device();
     });
 }
 
 int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
     return guarded([&] {
         require(h && out, "null argument");
-        std::lock_guard<std::mutex> g(h->mu);
+        std::lock_guard<std::mutex> gl(h->mu);
+        if (h->is_group()) group::synchronize(h);
+        vdb_ivf* const hh = h;
+        h = h->head();
         h->set_device();
         HIPCHECK(hipDeviceSynchronize());
         vdb_ivf_profile p{};
@@ -613,12 +672,14 @@ int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
         p.scan_bytes = st[1] * (uint64_t)h->dim * 4;
         p.pair_vectors = st[4];
         *out = p;
+        hh->set_device();
     });
 }
 
 int vdb_ivf_synchronize(vdb_ivf* h) {
     return guarded([&] {
         require(h, "null handle");
+        if (h->is_group()) return group::synchronize(h);
         h->set_device();
         HIPCHECK(hipStreamSynchronize(h->stream));
     });

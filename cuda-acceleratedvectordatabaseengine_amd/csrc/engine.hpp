@@ -249,6 +249,8 @@ struct vdb_ivf {
         DevBuf<uint64_t> l1_i;
         DevBuf<vdbk::ScanItem> items, items_w;
         DevBuf<uint8_t> xrec, xgat;  // multi-GPU: this rank's packed partials, the gathered records
+        DevBuf<float> gq;            // group member: the call's queries on this device
+        DevBuf<uint32_t> greq;       // group member: the call's request starts on this device
         hipStream_t side = nullptr;  // narrow-item scan, concurrent with the wide items
         hipStream_t gstream = nullptr;  // group member: the stream this slot's searches run on
         hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
@@ -275,6 +277,12 @@ struct vdb_ivf {
     bool group_rccl = false;      // members on distinct devices: RCCL; else device copies (rehearsal)
     std::vector<hipEvent_t> gev;  // group call fences, 2 per member
     bool is_group() const { return !members.empty(); }
+    vdb_ivf* head() { return is_group() ? members[0].get() : this; }
+    // the handle storing list l (a group member, or this handle)
+    vdb_ivf* store_of(uint32_t l) {
+        if (!is_group()) return this;
+        return owner[l] == kUnplaced ? members[0].get() : members[owner[l]].get();
+    }
     DevBuf<float> out_d, qin;  // host-API staging (synchronous calls)
     DevBuf<uint64_t> out_i;
     DevBuf<uint32_t> d_req;    // coalesced calls: request start per query
@@ -1007,6 +1015,17 @@ struct vdb_ivf {
         upload_directory();
     }
 
+    // Group member: store exactly the lists `new_owned` marks (placement by the group).
+    // A list may only move here while empty; lists leaving are dropped.
+    void set_owned(const std::vector<uint8_t>& new_owned) {
+        for (uint32_t l = 0; l < nlist; ++l)
+            require(!new_owned[l] || owned[l] || count[l] == 0, "a placed list cannot move between members",
+                    VDB_ERR_STATE);
+        if (new_owned == owned) return;
+        relayout(count, new_owned);
+        upload_directory();
+    }
+
     // Sharded build, for an index larger than one GPU (100M x 768 = 307 GB): the final
     // list sizes (from an assignment pass) fix this handle's lists before any add, so
     // appends store only the owned lists' rows and count the rest. The plan is the same
@@ -1154,8 +1173,69 @@ struct vdb_ivf {
         return true;
     }
 
+    uint32_t batch_cap(uint32_t P) const {
+        return std::max<uint32_t>(1, std::min<uint32_t>(batch, vdbk::kPlanMaxPairs / P));
+    }
+
+    // Grow a slot-owned buffer; a buffer still read by the slot's previous call is
+    // only freed once that call is done.
+    template <class T>
+    T* slot_buf(SearchSlot& w, DevBuf<T>& b, size_t n) {
+        if (b.cap < n && b.p && w.used) HIPCHECK(hipEventSynchronize(w.done));
+        return b.ensure(n);
+    }
+
+    // One reference search() call on this handle's device: take the next workspace slot,
+    // order stream s after the slot's previous call, start the call's probe slots
+    // (allocated once per call, cpp:210-211). `xworld` > 0 sizes the multi-GPU records.
+    SearchSlot& begin_call(uint32_t n, uint32_t P, uint32_t k, hipStream_t s, uint32_t xworld) {
+        if (!stats.p) {
+            stats.ensure(8);
+            HIPCHECK(hipMemsetAsync(stats.p, 0, 64, s));
+        }
+        SearchSlot& w = slots[next_slot];
+        next_slot = (next_slot + 1) % kSlots;
+        const uint32_t B = std::min(batch_cap(P), n);
+        ensure_workspace(w, B, P, k);
+        if (xworld) {
+            const uint64_t rb = vdb_rank_record_bytes(B, k);
+            slot_buf(w, w.xrec, rb);
+            slot_buf(w, w.xgat, rb * xworld);
+        }
+        if (w.used) HIPCHECK(hipStreamWaitEvent(s, w.done, 0));
+        HIPCHECK(hipMemsetAsync(w.carry_i.p, 0xFF, (size_t)P * k * 8, s));
+        return w;
+    }
+
+    void end_call(SearchSlot& w, hipStream_t s) {
+        HIPCHECK(hipEventRecord(w.done, s));
+        w.used = true;
+    }
+
+    // The slot's packed record for a batch of B queries (vdb_rank_record_bytes layout).
+    static float* rec_dist(SearchSlot& w) { return (float*)w.xrec.p; }
+    static uint64_t* rec_ids(SearchSlot& w, uint32_t B, uint32_t k) {
+        return (uint64_t*)(w.xrec.p + ((uint64_t)B * k * 4 + 7) / 8 * 8);
+    }
+    // Final results of a batch from `nranks` gathered records: unique-id top-k of the
+    // union (= merge_results over every rank's lists, cpp:474-518).
+    static void merge_gathered(SearchSlot& w, uint32_t nranks, uint32_t B, uint32_t k, float* od, uint64_t* oi,
+                               hipStream_t s) {
+        const uint64_t rec = vdb_rank_record_bytes(B, k);
+        const float* d = (const float*)w.xgat.p;
+        const uint64_t* ids = (const uint64_t*)(w.xgat.p + ((uint64_t)B * k * 4 + 7) / 8 * 8);
+        vdbk::launch_rank_merge(vdbk::topk_regs(k), d, ids, rec / 4, rec / 8, nranks, B, k, od, oi, s);
+        HIPCHECK(hipGetLastError());
+    }
+
+    // Group handle (group.cpp): the same call over every member's shard.
+    void group_search_device(const float* d_q, uint32_t n, uint32_t P, uint32_t k, float* d_dist, uint64_t* d_ids,
+                             hipStream_t s, const uint32_t* req_start);
+
     // req_start: null (one reference search() call) or, for a coalesced batch of calls,
     // per query the call-global index of its request's first query (device memory).
+    // With a communicator attached, every batch's partials are all-gathered over RCCL
+    // and merged, so d_dist / d_ids receive the final results on every rank.
     void search_device(const float* d_q, uint32_t n, uint32_t nprobe, uint32_t k, float* d_dist, uint64_t* d_ids,
                        hipStream_t s, const uint32_t* req_start = nullptr) {
         if (n == 0 || k == 0) return;
@@ -1167,26 +1247,31 @@ struct vdb_ivf {
             return;
         }
         require(P <= (uint32_t)vdbk::kMaxK, "nprobe above 1024 is not supported", VDB_ERR_UNSUPPORTED);
-        if (!stats.p) {
-            stats.ensure(8);
-            HIPCHECK(hipMemsetAsync(stats.p, 0, 64, s));
+        if (is_group()) {
+            group_search_device(d_q, n, P, k, d_dist, d_ids, s, req_start);
+            return;
         }
-        const uint32_t bmax = std::max<uint32_t>(1, std::min<uint32_t>(batch, vdbk::kPlanMaxPairs / P));
-        SearchSlot& w = slots[next_slot];
-        next_slot = (next_slot + 1) % kSlots;
-        ensure_workspace(w, std::min(bmax, n), P, k);
-        if (w.used) HIPCHECK(hipStreamWaitEvent(s, w.done, 0));
-        // Probe-slot contents live for one search call (cpp:210-211).
-        HIPCHECK(hipMemsetAsync(w.carry_i.p, 0xFF, (size_t)P * k * 8, s));
+        const bool xchg = comm != nullptr;
+        if (xchg)
+            require(comm_world == world && comm_rank == rank,
+                    "the attached communicator's (rank, world) differs from the handle's shard", VDB_ERR_STATE);
+        SearchSlot& w = begin_call(n, P, k, s, xchg ? comm_world : 0);
+        const uint32_t bmax = batch_cap(P);
         for (uint32_t b0 = 0, B = std::min(bmax, n); b0 < n; b0 += B, B = std::min(B, n - b0)) {
-            // (list-cache tier: a batch whose probed lists overflow the cache is halved)
-            while (!run_batch(w, d_q + (size_t)b0 * dim, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s,
-                              req_start, b0)) {
+            float* od = xchg ? rec_dist(w) : d_dist + (size_t)b0 * k;
+            uint64_t* oi = xchg ? rec_ids(w, B, k) : d_ids + (size_t)b0 * k;
+            // (list-cache tier: a batch whose probed lists overflow the cache is halved;
+            // never with a communicator, whose ranks must agree on every batch)
+            while (!run_batch(w, d_q + (size_t)b0 * dim, B, P, k, od, oi, s, req_start, b0)) {
                 require(B > 1, "list_cache_bytes cannot hold the lists one query probes", VDB_ERR_OUT_OF_MEMORY);
                 B = (B + 1) / 2;
+                if (xchg) oi = rec_ids(w, B, k);
+            }
+            if (xchg) {
+                NCCLCHECK(ncclAllGather(w.xrec.p, w.xgat.p, vdb_rank_record_bytes(B, k), ncclUint8, comm, s));
+                merge_gathered(w, comm_world, B, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s);
             }
         }
-        HIPCHECK(hipEventRecord(w.done, s));
-        w.used = true;
+        end_call(w, s);
     }
 };

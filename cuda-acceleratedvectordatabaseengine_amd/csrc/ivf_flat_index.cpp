@@ -29,7 +29,11 @@ IVFFlatIndex::IVFFlatIndex(const Config& config, TransferManager* tm) : config_(
     c.use_gpu = config_.use_gpu ? 1 : 0;
     c.max_gpu_memory = config_.max_gpu_memory;
     c.device = tm_ ? tm_->config().device : 0;
-    ok(vdb_ivf_create(&c, &h_), "vdb_ivf_create");
+    if (config_.devices.size() > 1)
+        ok(vdb_ivf_create_group(&c, config_.devices.data(), static_cast<uint32_t>(config_.devices.size()), &h_),
+           "vdb_ivf_create_group");
+    else
+        ok(vdb_ivf_create(&c, &h_), "vdb_ivf_create");
 }
 
 IVFFlatIndex::~IVFFlatIndex() {

@@ -29,6 +29,10 @@ public:
         kernels::Metric metric;
         bool use_gpu = true;
         size_t max_gpu_memory = 8ULL << 30;
+        // Not in the reference (its index runs on device 0 only): more than one entry
+        // shards the index by list over these GPUs (vdb_ivf_create_group); every call
+        // below is unchanged and results are identical to one GPU.
+        std::vector<int> devices = {};
     };
 
     struct SearchParams {

@@ -144,6 +144,35 @@ int vdb_merge_ranks_packed_device(const void* d_records, uint32_t nranks, uint32
 /* Host-only: the LPT owner of every list for `world` ranks (no GPU needed). */
 int vdb_shard_plan(const uint64_t* list_sizes, uint32_t nlist, uint32_t world, uint32_t* owner);
 
+/* ---- Multi-GPU inside the engine (RCCL over xGMI) ----
+ * One process per GPU: rank 0 draws a communicator id (vdb_comm_unique_id) and shares it
+ * with the other ranks (any channel); every rank, after set_shard / plan_shard with the
+ * same (rank, world), calls vdb_ivf_attach_comm. From then on vdb_ivf_search_device /
+ * vdb_ivf_search on that handle all-gather every batch's per-rank partials (ONE RCCL
+ * all-gather per batch of vdb_rank_record_bytes per rank) and merge them on the device,
+ * so every rank receives the FINAL results. Every rank must issue the same search calls
+ * (same n, nprobe, k and batch option) in the same order. Not combined with the
+ * list-cache tier. */
+#define VDB_COMM_ID_BYTES 128
+int vdb_comm_unique_id(void* id); /* VDB_COMM_ID_BYTES bytes (ncclGetUniqueId) */
+int vdb_ivf_attach_comm(vdb_ivf* index, const void* id, uint32_t rank, uint32_t world);
+int vdb_ivf_detach_comm(vdb_ivf* index);
+/* One process driving several GPUs: a group handle with one member index per device
+ * (devices[0] holds the host-API staging; device pointers passed to the group's calls
+ * live on devices[0]). The group is used through every call of this header like a
+ * single-device handle: train runs on devices[0] and its centroids are copied to every
+ * member; add places each list on a member when the list first receives vectors
+ * (largest first on the least-loaded member: the LPT plan of vdb_shard_plan for a bulk
+ * add) and every member stores its lists; a search broadcasts the queries (RCCL), runs
+ * each member's shard and all-gathers + merges per batch, with results bit-identical to
+ * one device. Members on distinct devices use ncclCommInitAll; members sharing a device
+ * (a one-GPU rehearsal) exchange through device copies. Not available on a group:
+ * set_shard, plan_shard, open_lists, the list-cache tier. */
+int vdb_ivf_create_group(const vdb_ivf_config* config, const int* devices, uint32_t ndevices, vdb_ivf** out);
+uint32_t vdb_ivf_group_size(const vdb_ivf* index); /* members; 1 for a single-device handle */
+/* Per list the member (group) or rank (sharded handle) storing it; UINT32_MAX: none. */
+int vdb_ivf_list_owners(vdb_ivf* index, uint32_t* owner);
+
 /* List residency. By default the whole index is HBM-resident (288 GB per GPU) and
  * these keep the API. With the list-cache tier (option "list_cache_bytes" > 0) the
  * lists live in page-locked host memory and HBM caches whole lists under that byte

@@ -8,6 +8,7 @@
 // Usage: gpu_vs_cpu_test [N Q D nlist] (ctest: 10000 100 64 32).
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <iomanip>
 #include <iostream>
@@ -78,6 +79,14 @@ int main(int argc, char** argv) {
         cfg.nlist = nlist;
         cfg.metric = kernels::Metric::L2;
         cfg.max_gpu_memory = 256 << 20;
+        if (const char* d = std::getenv("VDB_TEST_DEVICES")) {  // e.g. "0,1": the index sharded over GPUs
+            for (const char* p = d; *p;) {
+                cfg.devices.push_back(std::atoi(p));
+                while (*p && *p != ',') ++p;
+                if (*p == ',') ++p;
+            }
+            std::cout << "GPU index sharded over " << cfg.devices.size() << " device(s): " << d << std::endl;
+        }
         IVFFlatIndex index(cfg, &tm);
         auto t0 = clk::now();
         index.train(v.data(), train);

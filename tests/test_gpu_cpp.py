@@ -28,3 +28,14 @@ def test_gpu_vs_cpu_program_ctest_args(binaries):
                        text=True, timeout=600)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "results differing from the CPU path: 0" in p.stdout
+
+
+def test_gpu_vs_cpu_program_on_a_group_handle(binaries):
+    # the same program with Config::devices = {0, 0}: one index sharded over two members
+    # (here sharing the one GPU), results still bit-identical to the CPU path
+    env = dict(os.environ, VDB_TEST_DEVICES="0,0")
+    p = subprocess.run([os.path.join(binaries, "gpu_vs_cpu_test"), "10000", "100", "64", "32"], capture_output=True,
+                       text=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "sharded over 2 device(s)" in p.stdout
+    assert "results differing from the CPU path: 0" in p.stdout
