@@ -58,12 +58,22 @@ def percentile(values, p):
     return s[int(p * (len(s) - 1))] if s else 0.0
 
 
+def fill_rows(vdb, args, buf, row0, m, seed, stream):
+    """Rows row0 .. row0 + m of the synthetic stream `seed` into buf (device, m x dim):
+    iid N(0,1) draws, or Gaussian-mixture draws around args.centers (--data mixture)."""
+    if args.data == "mixture":
+        vdb.gen_mixture_device(buf.data_ptr(), m, args.dim, args.centers.data_ptr(), args.centers.shape[0],
+                               args.mix_sigma, seed, row0, stream)
+    else:
+        vdb.gen_normal_device(buf.data_ptr(), m * args.dim, seed=seed, offset=row0 * args.dim, stream=stream)
+
+
 def build_index(vdb, args, device, rank, world):
     dim, n = args.dim, args.nvec
     stream = torch.cuda.current_stream().cuda_stream
     assert stream != 0, "run under an explicit torch stream (handle 0 means the engine's own stream)"
     data = torch.empty((n, dim), dtype=torch.float32, device=device)
-    vdb.gen_normal_device(data.data_ptr(), n * dim, seed=12345, stream=stream)
+    fill_rows(vdb, args, data, 0, n, 12345, stream)
     ids = torch.arange(n, dtype=torch.int64, device=device)
     torch.cuda.synchronize()
     idx = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, args.nlist, vdb.Metric.L2, device=device.index))
@@ -95,13 +105,13 @@ def build_index_sharded(vdb, args, device, rank, world):
     idx = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, args.nlist, vdb.Metric.L2, device=device.index))
     t0 = time.perf_counter()
     ntrain = min(args.train, n)
-    vdb.gen_normal_device(data.data_ptr(), ntrain * dim, seed=12345, offset=0, stream=stream)
+    fill_rows(vdb, args, data, 0, ntrain, 12345, stream)
     torch.cuda.synchronize()
     idx.train_device(data.data_ptr(), ntrain)
     t1 = time.perf_counter()
     for a in range(0, n, chunk):
         m = min(chunk, n - a)
-        vdb.gen_normal_device(data.data_ptr(), m * dim, seed=12345, offset=a * dim, stream=stream)
+        fill_rows(vdb, args, data, a, m, 12345, stream)
         torch.cuda.synchronize()
         idx.assign_device(data.data_ptr(), m, asg[a:].data_ptr())
         log(rank, f"[bench] assigned {a + m} of {n} ({time.perf_counter() - t1:.1f}s)")
@@ -110,7 +120,7 @@ def build_index_sharded(vdb, args, device, rank, world):
     idx.plan_shard(rank, world, sizes)
     for a in range(0, n, chunk):
         m = min(chunk, n - a)
-        vdb.gen_normal_device(data.data_ptr(), m * dim, seed=12345, offset=a * dim, stream=stream)
+        fill_rows(vdb, args, data, a, m, 12345, stream)
         torch.arange(a, a + m, dtype=torch.int64, device=device, out=ids[:m])
         torch.cuda.synchronize()
         idx.add_to_lists_device(data.data_ptr(), ids.data_ptr(), asg[a:].data_ptr(), m)
@@ -216,6 +226,54 @@ def cpu_baseline(vdb, idx, args, queries_host, budget_s):
     }
 
 
+def host_api_leg(idx, args, queries, out_d, out_i):
+    """The drop-in path a server uses: vdb_ivf_search from `--host-threads` caller
+    threads, host buffers in and out (PCIe included), each call one batch of B queries
+    (the rows of the timed steps), coalesced into device batches of at most
+    `--host-coalesce` queries with up to three batches in flight. Checked bit for bit
+    against the device-resident results of the same rows (same call boundaries)."""
+    import threading
+    B, k = args.batch, args.k
+    q0 = args.warmup * B
+    calls = [queries[q0 + j * B:q0 + (j + 1) * B].cpu().numpy() for j in range(args.steps)]
+    ref_d = out_d[q0:q0 + args.steps * B].cpu().numpy()
+    ref_i = out_i[q0:q0 + args.steps * B].cpu().numpy().view(np.uint64)
+    idx.set_option("coalesce_max_queries", args.host_coalesce)
+    for j in range(min(4, len(calls))):  # warm-up (staging buffers, streams)
+        idx.search(calls[j], nprobe=args.nprobe, k=k)
+    b0, r0 = idx.coalesce_stats()
+    total = max(args.host_calls, len(calls))
+    lock, nxt, same = threading.Lock(), [0], [True]
+
+    def worker():
+        while True:
+            with lock:
+                j = nxt[0]
+                nxt[0] += 1
+            if j >= total:
+                return
+            c = j % len(calls)
+            D, I = idx.search(calls[c], nprobe=args.nprobe, k=k)
+            if j < len(calls):
+                ok = np.array_equal(I, ref_i[c * B:(c + 1) * B]) and \
+                    np.array_equal(D.view(np.uint32), ref_d[c * B:(c + 1) * B].view(np.uint32))
+                if not ok:
+                    same[0] = False
+
+    th = [threading.Thread(target=worker) for _ in range(args.host_threads)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    b1, r1 = idx.coalesce_stats()
+    return {"value": round(total * B / el, 1), "unit": "queries/s", "calls": total, "queries_per_call": B,
+            "caller_threads": args.host_threads, "device_batch_max_queries": args.host_coalesce,
+            "device_batches": b1 - b0, "calls_per_device_batch": round((r1 - r0) / max(b1 - b0, 1), 2),
+            "pcie_inclusive": True, "parity_with_device_path": same[0]}
+
+
 def shard_parity(vdb, idx, args, queries_host, rank, world):
     """Parity of one shard at full size: the oracle's shard search (oracle_search_shard:
     owned probed lists scanned, the others kept as counts for the empty-list rule,
@@ -303,6 +361,16 @@ def main():
     ap.add_argument("--shard-check", type=int, default=0, metavar="Q",
                     help="with --emulate-shard: check Q queries of this shard bit for bit against the oracle")
     ap.add_argument("--prewarm", action="store_true", help="warm every list up front (list-cache tier)")
+    ap.add_argument("--data", choices=["iid", "mixture"], default="iid",
+                    help="iid N(0,1) vectors (the reference generator's distribution; k-means makes hub lists), or a "
+                         "Gaussian mixture (balanced lists, ~1.3 queries per probed list: the regime of clustered data)")
+    ap.add_argument("--mix-components", type=int, default=0, help="mixture components (0 = nlist)")
+    ap.add_argument("--mix-sigma", type=float, default=0.5, help="mixture noise (centers are N(0,1))")
+    ap.add_argument("--host-api", action="store_true",
+                    help="also time the host API (vdb_ivf_search) from --host-threads caller threads")
+    ap.add_argument("--host-threads", type=int, default=8)
+    ap.add_argument("--host-calls", type=int, default=400, help="host-API calls of --batch queries each")
+    ap.add_argument("--host-coalesce", type=int, default=64, help="max queries per coalesced device batch")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning knob (vdb_ivf_set_option), e.g. wide_stride=1; results never change")
     args = ap.parse_args()
@@ -347,6 +415,10 @@ def main():
 
 
 def run(vdb, args, device, rank, world):
+    if args.data == "mixture":
+        args.centers = torch.empty((args.mix_components or args.nlist, args.dim), dtype=torch.float32, device=device)
+        vdb.gen_normal_device(args.centers.data_ptr(), args.centers.numel(), seed=777,
+                              stream=torch.cuda.current_stream().cuda_stream)
     if args.sharded_build:
         shards = world if world > 1 else max(args.emulate_shard, 1)
         idx, build_info = build_index_sharded(vdb, args, device, rank if world > 1 else 0, shards)
@@ -363,7 +435,7 @@ def run(vdb, args, device, rank, world):
     nq = (args.warmup + args.steps + args.prof_steps) * B
     main_stream = torch.cuda.current_stream()
     queries = torch.empty((nq, args.dim), dtype=torch.float32, device=device)
-    vdb.gen_normal_device(queries.data_ptr(), nq * args.dim, seed=12346, stream=main_stream.cuda_stream)
+    fill_rows(vdb, args, queries, 0, nq, 12346, main_stream.cuda_stream)
     out_d = torch.empty((nq, k), dtype=torch.float32, device=device)
     out_i = torch.empty((nq, k), dtype=torch.int64, device=device)
     check = None
@@ -481,6 +553,8 @@ def run(vdb, args, device, rank, world):
         with open(args.traffic_json) as f:
             tj = json.load(f)
         key = f"{args.nvec}x{args.dim}/{args.nlist}/{args.nprobe}/{B}/{k}/N{world}"
+        if args.data != "iid":
+            key += f"/{args.data}"
         if args.emulate_shard > 1:
             key += f"/shard0of{args.emulate_shard}"
         if args.opt:  # knobs can change the traffic (never the results)
@@ -504,7 +578,10 @@ def run(vdb, args, device, rank, world):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic: iid N(0,1) fp32 vectors generated on device (seed 12345), queries seed 12346",
+        "data": ("synthetic: iid N(0,1) fp32 vectors generated on device (seed 12345), queries seed 12346"
+                 if args.data == "iid" else
+                 f"synthetic: Gaussian mixture of {args.centers.shape[0]} components (centers N(0,1) seed 777, "
+                 f"sigma {args.mix_sigma}) generated on device (seed 12345), queries from the same mixture (seed 12346)"),
         "config": {
             "workload": f"{args.nvec // 1_000_000}M x {args.dim}D IVF-Flat L2, nlist {args.nlist}, nprobe {args.nprobe}, "
                         f"batch {B}, k {k}",
@@ -540,6 +617,8 @@ def run(vdb, args, device, rank, world):
     }
     if parity_multi is not None:
         result["parity_vs_single_gpu"] = {"batches": min(args.check_batches, args.steps), "bit_identical": parity_multi}
+    if args.host_api and world == 1:
+        result["host_api"] = host_api_leg(idx, args, queries, out_d, out_i)
     if world == 1 and rank == 0 and not args.no_cpu and args.emulate_shard <= 1:
         qh = queries[: args.cpu_queries].cpu().numpy()
         result["cpu_baseline"] = cpu_baseline(vdb, idx, args, qh, args.cpu_budget)

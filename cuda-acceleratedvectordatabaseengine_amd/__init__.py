@@ -131,6 +131,7 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_synchronize": (ctypes.c_int, [vp]),
         "vdb_ivf_stream": (vp, [vp]),
         "vdb_gen_normal_device": (ctypes.c_int, [vp, u64, u64, u64, vp]),
+        "vdb_gen_mixture_device": (ctypes.c_int, [vp, u64, u32, vp, u32, ctypes.c_float, u64, u64, vp]),
         "vdb_comm_unique_id": (ctypes.c_int, [vp]),
         "vdb_ivf_attach_comm": (ctypes.c_int, [vp, vp, u32, u32]),
         "vdb_ivf_detach_comm": (ctypes.c_int, [vp]),
@@ -172,6 +173,14 @@ def shard_plan(list_sizes, world: int) -> np.ndarray:
 def gen_normal_device(ptr: int, n: int, seed: int, offset: int = 0, stream: int | None = None):
     """Fill n fp32 at device address ``ptr`` with deterministic N(0,1) draws."""
     _check(lib().vdb_gen_normal_device(ctypes.c_void_p(ptr), n, seed, offset, ctypes.c_void_p(stream or 0)))
+
+
+def gen_mixture_device(ptr: int, rows: int, dim: int, centers_ptr: int, ncomp: int, sigma: float, seed: int,
+                       row0: int = 0, stream: int | None = None):
+    """Fill rows x dim fp32 at ``ptr`` with Gaussian-mixture draws around the ncomp x dim
+    device centers (synthetic clustered data; rows row0.. of one deterministic stream)."""
+    _check(lib().vdb_gen_mixture_device(ctypes.c_void_p(ptr), rows, dim, ctypes.c_void_p(centers_ptr), ncomp,
+                                        ctypes.c_float(sigma), seed, row0, ctypes.c_void_p(stream or 0)))
 
 
 def merge_ranks_device(dist_ptr: int, ids_ptr: int, nranks: int, n: int, k: int, out_dist_ptr: int,

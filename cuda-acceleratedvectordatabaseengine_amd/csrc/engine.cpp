@@ -687,6 +687,15 @@ int vdb_ivf_synchronize(vdb_ivf* h) {
 
 void* vdb_ivf_stream(vdb_ivf* h) { return h ? (void*)h->stream : nullptr; }
 
+int vdb_gen_mixture_device(float* d_out, uint64_t rows, uint32_t dim, const float* d_centers, uint32_t ncomp,
+                           float sigma, uint64_t seed, uint64_t row0, void* stream) {
+    return guarded([&] {
+        require((d_out && d_centers && ncomp > 0) || rows == 0, "invalid argument");
+        vdbk::launch_gen_mixture(d_out, rows, dim, d_centers, ncomp, sigma, seed, row0, (hipStream_t)stream);
+        HIPCHECK(hipGetLastError());
+    });
+}
+
 int vdb_gen_normal_device(float* d_out, uint64_t n, uint64_t seed, uint64_t offset, void* stream) {
     return guarded([&] {
         require(d_out || n == 0, "null argument");

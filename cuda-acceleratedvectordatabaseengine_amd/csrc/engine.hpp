@@ -146,16 +146,40 @@ struct PendingSearch {
 
 // Request coalescing (the reference's intent: QueryServiceImpl::Config max_batch_size /
 // coalesce_window_ms, query_service.h:25-31, never implemented there): concurrent
-// vdb_ivf_search callers enqueue; one worker thread takes every compatible waiting call
-// (same nprobe and k), up to max_queries, and runs them as ONE device search whose
-// per-call slot semantics are kept exact (request boundaries, kernels' req_start).
-// While the device works on one batch, the next one accumulates.
+// vdb_ivf_search callers enqueue; a dispatcher thread takes every compatible waiting call
+// (same nprobe and k), up to max_queries, stages the queries in page-locked memory and
+// enqueues ONE device search on a staging slot's own stream (H2D, search, D2H), then
+// goes straight on to the next batch: up to kHostSlots batches are in flight, so one
+// batch's copies and coarse step overlap the previous batch's scan (the pipelining the
+// reference's DoubleBuffer / StreamScheduler intended, transfer_manager.h:168-239). A
+// completion thread waits for each batch in issue order and hands the results back.
+// Per-call slot semantics stay exact (request boundaries, kernels' req_start).
+struct HostBatch {
+    std::vector<PendingSearch*> reqs;
+    uint32_t nq = 0, P = 0, K = 0;
+    DevBuf<float> hq, hd;     // page-locked staging
+    DevBuf<uint64_t> hi;
+    DevBuf<uint32_t> hreq;
+    DevBuf<float> dq, dd;     // device
+    DevBuf<uint64_t> di;
+    DevBuf<uint32_t> dreq;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    int rc = VDB_OK;
+    std::string err;
+    HostBatch() { hq.host = hd.host = hi.host = hreq.host = true; }
+};
+
 struct Coalescer {
+    static constexpr int kHostSlots = 3;
     std::mutex m;
-    std::condition_variable wake, done;
+    std::condition_variable wake, done, slot_free, issued;
     std::deque<PendingSearch*> queue;
-    std::thread worker;
-    bool stop = false;
+    std::deque<HostBatch*> inflight;  // issue order
+    std::vector<HostBatch*> free_slots;
+    HostBatch slots[kHostSlots];
+    std::thread dispatcher, completer;
+    bool stop = false, dispatch_done = false;
     uint64_t batches = 0, requests = 0;
 };
 
@@ -291,9 +315,6 @@ struct vdb_ivf {
     bool coalesce = true;
     uint32_t coalesce_max_queries = 1024;
     uint32_t coalesce_window_us = 0;
-    std::vector<float> hq_stage;
-    std::vector<float> hd_stage;
-    std::vector<uint64_t> hi_stage;
     DevBuf<unsigned long long> stats;
 
     bool prof = false;
@@ -354,7 +375,14 @@ struct vdb_ivf {
     void start_coalescer() {
         if (co) return;
         co.reset(new Coalescer());
-        co->worker = std::thread([this] { coalesce_loop(); });
+        set_device();
+        for (HostBatch& hb : co->slots) {
+            HIPCHECK(hipStreamCreateWithFlags(&hb.stream, hipStreamNonBlocking));
+            HIPCHECK(hipEventCreateWithFlags(&hb.done, hipEventDisableTiming));
+            co->free_slots.push_back(&hb);
+        }
+        co->dispatcher = std::thread([this] { dispatch_loop(); });
+        co->completer = std::thread([this] { complete_loop(); });
     }
 
     void stop_coalescer() {
@@ -364,89 +392,149 @@ struct vdb_ivf {
             co->stop = true;
         }
         co->wake.notify_all();
-        if (co->worker.joinable()) co->worker.join();
+        co->slot_free.notify_all();
+        if (co->dispatcher.joinable()) co->dispatcher.join();
+        if (co->completer.joinable()) co->completer.join();
+        (void)hipSetDevice(device);
+        for (HostBatch& hb : co->slots) {
+            if (hb.stream) (void)hipStreamDestroy(hb.stream);
+            if (hb.done) (void)hipEventDestroy(hb.done);
+        }
         co.reset();
     }
 
-    void coalesce_loop() {
+    void dispatch_loop() {
         Coalescer& c = *co;
+        (void)hipSetDevice(device);
         for (;;) {
-            std::vector<PendingSearch*> run;
-            uint32_t nq = 0;
+            HostBatch* hb = nullptr;
             {
                 std::unique_lock<std::mutex> lk(c.m);
                 c.wake.wait(lk, [&] { return c.stop || !c.queue.empty(); });
-                if (c.queue.empty()) return;  // stop requested and nothing left
+                if (c.queue.empty()) break;  // stop requested and nothing left
+                // a free staging slot: at most kHostSlots batches in flight (calls keep
+                // queueing meanwhile, so the next batch grows while the device is busy)
+                c.slot_free.wait(lk, [&] { return !c.free_slots.empty(); });
                 if (coalesce_window_us)
                     c.wake.wait_for(lk, std::chrono::microseconds(coalesce_window_us), [&] {
                         uint64_t t = 0;
                         for (auto* r : c.queue) t += r->n;
                         return c.stop || t >= coalesce_max_queries;
                     });
-                const uint32_t P = c.queue.front()->nprobe, K = c.queue.front()->k;
+                hb = c.free_slots.back();
+                c.free_slots.pop_back();
+                hb->reqs.clear();
+                hb->nq = 0;
+                hb->P = c.queue.front()->nprobe;
+                hb->K = c.queue.front()->k;
                 for (auto it = c.queue.begin(); it != c.queue.end();) {
                     PendingSearch* r = *it;
-                    if (r->nprobe == P && r->k == K && (run.empty() || nq + r->n <= coalesce_max_queries)) {
-                        run.push_back(r);
-                        nq += r->n;
+                    if (r->nprobe == hb->P && r->k == hb->K && (hb->reqs.empty() || hb->nq + r->n <= coalesce_max_queries)) {
+                        hb->reqs.push_back(r);
+                        hb->nq += r->n;
                         it = c.queue.erase(it);
                     } else {
                         ++it;
                     }
                 }
                 c.batches++;
-                c.requests += run.size();
+                c.requests += hb->reqs.size();
             }
-            int rc = VDB_OK;
-            std::string err;
+            hb->rc = VDB_OK;
+            hb->err.clear();
             try {
-                std::lock_guard<std::mutex> g(mu);
-                if (run.size() == 1) {
-                    PendingSearch* r = run[0];
-                    search_host(r->q, r->n, r->nprobe, r->k, r->dist, r->ids, nullptr);
-                } else {
-                    const uint32_t K = run[0]->k;
-                    hq_stage.resize((size_t)nq * dim);
-                    hd_stage.resize((size_t)nq * K);
-                    hi_stage.resize((size_t)nq * K);
-                    std::vector<uint32_t> rs(nq);
-                    uint32_t o = 0;
-                    for (PendingSearch* r : run) {
-                        std::memcpy(hq_stage.data() + (size_t)o * dim, r->q, (size_t)r->n * dim * 4);
-                        for (uint32_t i = 0; i < r->n; ++i) rs[o + i] = o;
-                        o += r->n;
-                    }
-                    search_host(hq_stage.data(), nq, run[0]->nprobe, K, hd_stage.data(), hi_stage.data(), rs.data());
-                    o = 0;
-                    for (PendingSearch* r : run) {
-                        std::memcpy(r->dist, hd_stage.data() + (size_t)o * K, (size_t)r->n * K * 4);
-                        std::memcpy(r->ids, hi_stage.data() + (size_t)o * K, (size_t)r->n * K * 8);
-                        o += r->n;
-                    }
+                const uint32_t nq = hb->nq, K = hb->K;
+                float* hq = hb->hq.ensure((size_t)nq * dim);
+                uint32_t* hr = hb->reqs.size() > 1 ? hb->hreq.ensure(nq) : nullptr;
+                uint32_t o = 0;
+                for (PendingSearch* r : hb->reqs) {
+                    std::memcpy(hq + (size_t)o * dim, r->q, (size_t)r->n * dim * 4);
+                    if (hr)
+                        for (uint32_t i = 0; i < r->n; ++i) hr[o + i] = o;
+                    o += r->n;
                 }
+                hb->hd.ensure((size_t)nq * K);
+                hb->hi.ensure((size_t)nq * K);
+                std::lock_guard<std::mutex> g(mu);  // held only while the batch is enqueued
+                set_device();
+                HIPCHECK(hipMemcpyAsync(hb->dq.ensure((size_t)nq * dim), hq, (size_t)nq * dim * 4, hipMemcpyHostToDevice,
+                                        hb->stream));
+                const uint32_t* dr = nullptr;
+                if (hr) {
+                    HIPCHECK(hipMemcpyAsync(hb->dreq.ensure(nq), hr, (size_t)nq * 4, hipMemcpyHostToDevice, hb->stream));
+                    dr = hb->dreq.p;
+                }
+                search_device(hb->dq.p, nq, hb->P, K, hb->dd.ensure((size_t)nq * K), hb->di.ensure((size_t)nq * K),
+                              hb->stream, dr);
+                HIPCHECK(hipMemcpyAsync(hb->hd.p, hb->dd.p, (size_t)nq * K * 4, hipMemcpyDeviceToHost, hb->stream));
+                HIPCHECK(hipMemcpyAsync(hb->hi.p, hb->di.p, (size_t)nq * K * 8, hipMemcpyDeviceToHost, hb->stream));
+                HIPCHECK(hipEventRecord(hb->done, hb->stream));
             } catch (const VdbError& e) {
-                rc = e.code;
-                err = e.what();
+                hb->rc = e.code;
+                hb->err = e.what();
             } catch (const std::exception& e) {
-                rc = VDB_ERR_DEVICE;
-                err = e.what();
+                hb->rc = VDB_ERR_DEVICE;
+                hb->err = e.what();
             }
             {
                 std::lock_guard<std::mutex> g(c.m);
-                for (PendingSearch* r : run) {
-                    r->err = err;
-                    r->rc = rc;
+                c.inflight.push_back(hb);
+            }
+            c.issued.notify_one();
+        }
+        {
+            std::lock_guard<std::mutex> g(c.m);
+            c.dispatch_done = true;
+        }
+        c.issued.notify_one();
+    }
+
+    void complete_loop() {
+        Coalescer& c = *co;
+        (void)hipSetDevice(device);
+        for (;;) {
+            HostBatch* hb = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(c.m);
+                c.issued.wait(lk, [&] { return !c.inflight.empty() || c.dispatch_done; });
+                if (c.inflight.empty()) return;
+                hb = c.inflight.front();
+                c.inflight.pop_front();
+            }
+            if (hb->rc == VDB_OK) {
+                const hipError_t e = hipEventSynchronize(hb->done);
+                if (e != hipSuccess) {
+                    hb->rc = VDB_ERR_DEVICE;
+                    hb->err = std::string("search batch: ") + hipGetErrorString(e);
                 }
             }
+            if (hb->rc == VDB_OK) {
+                uint32_t o = 0;
+                for (PendingSearch* r : hb->reqs) {
+                    std::memcpy(r->dist, hb->hd.p + (size_t)o * hb->K, (size_t)r->n * hb->K * 4);
+                    std::memcpy(r->ids, hb->hi.p + (size_t)o * hb->K, (size_t)r->n * hb->K * 8);
+                    o += r->n;
+                }
+            }
+            {
+                std::lock_guard<std::mutex> g(c.m);
+                for (PendingSearch* r : hb->reqs) {
+                    r->err = hb->err;
+                    r->rc = hb->rc;
+                }
+                hb->reqs.clear();
+                c.free_slots.push_back(hb);
+            }
             c.done.notify_all();
+            c.slot_free.notify_one();
         }
     }
 
     void search_coalesced(const float* q, uint32_t n, uint32_t nprobe, uint32_t k, float* dist, uint64_t* ids) {
         PendingSearch r{q, n, nprobe, k, dist, ids};
         {
-            // not `mu`: the worker holds that while the device runs a batch, and callers
-            // must be able to queue meanwhile
+            // not `mu`: the dispatcher takes that to enqueue a batch, and callers must be
+            // able to queue meanwhile
             std::lock_guard<std::mutex> g(co_init_mu);
             start_coalescer();
         }

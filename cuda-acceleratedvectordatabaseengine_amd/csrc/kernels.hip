@@ -1815,6 +1815,26 @@ __global__ void synth_gen_normal(float* __restrict__ out, uint64_t n, uint64_t s
     }
 }
 
+// Gaussian mixture (synthetic clustered data): row r belongs to component
+// splitmix(seed') ^ r mod ncomp, and x[r][d] = centers[comp][d] + sigma * N(0,1), the
+// noise being element r * dim + d of the same counter-based stream as above.
+__global__ void synth_gen_mixture(float* __restrict__ out, uint64_t rows, uint32_t dim,
+                                  const float* __restrict__ centers, uint32_t ncomp, float sigma, uint64_t seed,
+                                  uint64_t row0) {
+    const uint64_t sk = splitmix64(seed);
+    const uint64_t ck = splitmix64(seed ^ 0x6D69787475726531ull);
+    for (uint64_t e = gtid(); e < rows * dim; e += gstride()) {
+        const uint64_t r = e / dim;
+        const uint32_t d = (uint32_t)(e - r * dim);
+        const uint64_t gr = row0 + r;
+        const uint32_t comp = (uint32_t)(splitmix64(ck ^ gr) % ncomp);
+        const uint64_t h = splitmix64(sk ^ (gr * dim + d));
+        const float u1 = ((float)(h >> 40) + 1.0f) * (1.0f / 16777216.0f);
+        const float u2 = (float)(h & 0xFFFFFFull) * (1.0f / 16777216.0f);
+        out[e] = centers[(uint64_t)comp * dim + d] + sigma * (sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2));
+    }
+}
+
 // ============================================================================
 // Launchers
 // ============================================================================
@@ -2147,6 +2167,12 @@ void launch_slots_from_order(const uint32_t* sorted_keys, uint64_t n, const uint
 void launch_gen_normal(float* out, uint64_t n, uint64_t seed, uint64_t offset, hipStream_t s) {
     if (!n) return;
     synth_gen_normal<<<launch_grid(n), 256, 0, s>>>(out, n, seed, offset);
+}
+
+void launch_gen_mixture(float* out, uint64_t rows, uint32_t dim, const float* centers, uint32_t ncomp, float sigma,
+                        uint64_t seed, uint64_t row0, hipStream_t s) {
+    if (!rows || !dim) return;
+    synth_gen_mixture<<<launch_grid(rows * dim), 256, 0, s>>>(out, rows, dim, centers, ncomp, sigma, seed, row0);
 }
 
 hipError_t radix_sort_pairs(void* temp, size_t& temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,

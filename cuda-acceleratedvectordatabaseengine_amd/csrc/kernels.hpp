@@ -145,6 +145,8 @@ void launch_iota(uint32_t* out, uint64_t n, hipStream_t s);
 void launch_slots_from_order(const uint32_t* sorted_keys, uint64_t n, const uint64_t* group_start,
                              const uint64_t* list_base_slot, uint64_t* dest_slot, hipStream_t s);
 void launch_gen_normal(float* out, uint64_t n, uint64_t seed, uint64_t offset, hipStream_t s);
+void launch_gen_mixture(float* out, uint64_t rows, uint32_t dim, const float* centers, uint32_t ncomp, float sigma,
+                        uint64_t seed, uint64_t row0, hipStream_t s);
 
 // Stable key/value radix sort (hipCUB). temp == nullptr queries temp_bytes.
 hipError_t radix_sort_pairs(void* temp, size_t& temp_bytes, const uint32_t* keys_in, uint32_t* keys_out,

@@ -250,6 +250,11 @@ void* vdb_ivf_stream(vdb_ivf* index);
 /* Deterministic N(0,1) fp32 generator on the device (synthetic benchmark data):
  * element e of the stream (seed, offset + i) is written to d_out[i]. */
 int vdb_gen_normal_device(float* d_out, uint64_t n, uint64_t seed, uint64_t offset, void* stream);
+/* Gaussian-mixture rows (synthetic clustered data, balanced IVF lists): row row0 + r
+ * belongs to a component drawn from (seed, row), x = d_centers[comp] (ncomp x dim,
+ * device) + sigma * N(0,1). Independent of how the rows are split into calls. */
+int vdb_gen_mixture_device(float* d_out, uint64_t rows, uint32_t dim, const float* d_centers, uint32_t ncomp,
+                           float sigma, uint64_t seed, uint64_t row0, void* stream);
 
 #ifdef __cplusplus
 }

@@ -55,32 +55,48 @@ def test_cfg1_ivf_train_and_search_100k_x_128():
     assert np.array_equal(bits(D), bits(Dr))
 
 
-def test_cfg2_1m_x_768_nlist256_nprobe16_batch64():
+@pytest.mark.parametrize("data", ["iid", "mixture"])
+def test_cfg2_1m_x_768_nlist256_nprobe16_batch64(data):
+    """`mixture`: bench.py --data mixture's generator (256 Gaussian components, sigma 0.5),
+    balanced lists probed by ~1-2 queries each — the narrow-item regime of clustered data."""
     import torch
     n, dim, nlist, nprobe, B, k = 1_000_000, 768, 256, 16, 64, 10
     dev = torch.device("cuda", 0)
     with torch.cuda.stream(torch.cuda.Stream(dev)):
         s = torch.cuda.current_stream().cuda_stream
-        data = torch.empty((n, dim), dtype=torch.float32, device=dev)
-        vdb.gen_normal_device(data.data_ptr(), n * dim, seed=12345, stream=s)
-        ids = torch.arange(n, dtype=torch.int64, device=dev)
+        data_t = torch.empty((n, dim), dtype=torch.float32, device=dev)
         q = torch.empty((B, dim), dtype=torch.float32, device=dev)
-        vdb.gen_normal_device(q.data_ptr(), B * dim, seed=12346, stream=s)
+        if data == "mixture":
+            centers = torch.empty((nlist, dim), dtype=torch.float32, device=dev)
+            vdb.gen_normal_device(centers.data_ptr(), nlist * dim, seed=777, stream=s)
+            vdb.gen_mixture_device(data_t.data_ptr(), n, dim, centers.data_ptr(), nlist, 0.5, 12345, 0, s)
+            vdb.gen_mixture_device(q.data_ptr(), B, dim, centers.data_ptr(), nlist, 0.5, 12346, 0, s)
+        else:
+            vdb.gen_normal_device(data_t.data_ptr(), n * dim, seed=12345, stream=s)
+            vdb.gen_normal_device(q.data_ptr(), B * dim, seed=12346, stream=s)
+        ids = torch.arange(n, dtype=torch.int64, device=dev)
         torch.cuda.synchronize()
         g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist))
-        g.train_device(data.data_ptr(), 100_000)
-        g.add_device(data.data_ptr(), ids.data_ptr(), n)
+        g.train_device(data_t.data_ptr(), 100_000)
+        g.add_device(data_t.data_ptr(), ids.data_ptr(), n)
         od = torch.empty((B, k), dtype=torch.float32, device=dev)
         oi = torch.empty((B, k), dtype=torch.int64, device=dev)
         g.search_device(q.data_ptr(), B, nprobe, k, od.data_ptr(), oi.data_ptr(), s)
         torch.cuda.synchronize()
         Q = q.cpu().numpy()
         D, I = od.cpu().numpy(), oi.cpu().numpy().view(np.uint64)
-        del data, ids
+        if data == "mixture":  # the generator: chunked calls give the same rows
+            part = torch.empty((1000, dim), dtype=torch.float32, device=dev)
+            vdb.gen_mixture_device(part.data_ptr(), 1000, dim, centers.data_ptr(), nlist, 0.5, 12345, 5000, s)
+            torch.cuda.synchronize()
+            assert torch.equal(part, data_t[5000:6000])
+        del data_t, ids
     o = oracle.OracleIndex(dim, nlist, 0)
     o.centroids = g.centroids
     sizes = g.list_sizes()
     assert int(sizes.sum()) == n
+    if data == "mixture":  # mostly one component per list (k-means merges a few), no hub lists
+        assert np.median(sizes) > 0.75 * n / nlist and sizes.max() < 8 * n / nlist
     probed = sorted({int(l) for qv in Q for l in o.select_nprobe(qv, nprobe)})
     for l in probed:  # only the probed lists are ever read for these queries
         v, i = o.list_buffers(l, int(sizes[l]))

@@ -198,7 +198,9 @@ def test_torch_nccl_world1_exchange():
     dev = torch.device("cuda", 0)
     store = dist.HashStore()
     dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    st = torch.cuda.Stream(dev)
     try:
+        torch.cuda.set_stream(st)  # an explicit stream: handle 0 would mean the engine's own stream
         B, k = 100, 10
         rec = vdb.rank_record_bytes(B, k)
         part = torch.empty(rec, dtype=torch.uint8, device=dev)
@@ -213,4 +215,5 @@ def test_torch_nccl_world1_exchange():
         torch.cuda.synchronize()
         assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), *o.search(Q, 8, 10))
     finally:
+        torch.cuda.set_stream(torch.cuda.default_stream(dev))
         dist.destroy_process_group()
