@@ -58,6 +58,20 @@ def percentile(values, p):
     return s[int(p * (len(s) - 1))] if s else 0.0
 
 
+def mixture_centers(vdb, ncomp, group, dim, spread, device):
+    """Two-level mixture: ncomp / group super-cluster centers S ~ N(0,1) (seed 777), and
+    component j = S[j // group] + spread * N(0,1) (seed 778). Clustered data with locality:
+    the group sibling components of a point's super-cluster are its nearest ones."""
+    import torch
+    s = torch.cuda.current_stream().cuda_stream
+    nsup = (ncomp + group - 1) // group
+    sup = torch.empty((nsup, dim), dtype=torch.float32, device=device)
+    off = torch.empty((ncomp, dim), dtype=torch.float32, device=device)
+    vdb.gen_normal_device(sup.data_ptr(), sup.numel(), seed=777, stream=s)
+    vdb.gen_normal_device(off.data_ptr(), off.numel(), seed=778, stream=s)
+    return sup.repeat_interleave(group, dim=0)[:ncomp] + spread * off
+
+
 def fill_rows(vdb, args, buf, row0, m, seed, stream):
     """Rows row0 .. row0 + m of the synthetic stream `seed` into buf (device, m x dim):
     iid N(0,1) draws, or Gaussian-mixture draws around args.centers (--data mixture)."""
@@ -365,7 +379,10 @@ def main():
                     help="iid N(0,1) vectors (the reference generator's distribution; k-means makes hub lists), or a "
                          "Gaussian mixture (balanced lists, ~1.3 queries per probed list: the regime of clustered data)")
     ap.add_argument("--mix-components", type=int, default=0, help="mixture components (0 = nlist)")
-    ap.add_argument("--mix-sigma", type=float, default=0.5, help="mixture noise (centers are N(0,1))")
+    ap.add_argument("--mix-group", type=int, default=0,
+                    help="components per super-cluster (0 = nprobe): a query's nprobe nearest lists are its siblings")
+    ap.add_argument("--mix-spread", type=float, default=0.35, help="component centers around their super-cluster")
+    ap.add_argument("--mix-sigma", type=float, default=0.1, help="points around their component center")
     ap.add_argument("--host-api", action="store_true",
                     help="also time the host API (vdb_ivf_search) from --host-threads caller threads")
     ap.add_argument("--host-threads", type=int, default=8)
@@ -416,9 +433,8 @@ def main():
 
 def run(vdb, args, device, rank, world):
     if args.data == "mixture":
-        args.centers = torch.empty((args.mix_components or args.nlist, args.dim), dtype=torch.float32, device=device)
-        vdb.gen_normal_device(args.centers.data_ptr(), args.centers.numel(), seed=777,
-                              stream=torch.cuda.current_stream().cuda_stream)
+        args.centers = mixture_centers(vdb, args.mix_components or args.nlist, args.mix_group or args.nprobe,
+                                       args.dim, args.mix_spread, device)
     if args.sharded_build:
         shards = world if world > 1 else max(args.emulate_shard, 1)
         idx, build_info = build_index_sharded(vdb, args, device, rank if world > 1 else 0, shards)
@@ -580,8 +596,10 @@ def run(vdb, args, device, rank, world):
         "dtype": "fp32",
         "data": ("synthetic: iid N(0,1) fp32 vectors generated on device (seed 12345), queries seed 12346"
                  if args.data == "iid" else
-                 f"synthetic: Gaussian mixture of {args.centers.shape[0]} components (centers N(0,1) seed 777, "
-                 f"sigma {args.mix_sigma}) generated on device (seed 12345), queries from the same mixture (seed 12346)"),
+                 f"synthetic: two-level Gaussian mixture, {args.centers.shape[0]} components in super-clusters of "
+                 f"{args.mix_group or args.nprobe} (supers N(0,1) seed 777, components +{args.mix_spread} N(0,1) seed 778, "
+                 f"points +{args.mix_sigma} N(0,1)) generated on device (seed 12345), queries from the same mixture "
+                 f"(seed 12346)"),
         "config": {
             "workload": f"{args.nvec // 1_000_000}M x {args.dim}D IVF-Flat L2, nlist {args.nlist}, nprobe {args.nprobe}, "
                         f"batch {B}, k {k}",

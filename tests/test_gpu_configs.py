@@ -57,8 +57,8 @@ def test_cfg1_ivf_train_and_search_100k_x_128():
 
 @pytest.mark.parametrize("data", ["iid", "mixture"])
 def test_cfg2_1m_x_768_nlist256_nprobe16_batch64(data):
-    """`mixture`: bench.py --data mixture's generator (256 Gaussian components, sigma 0.5),
-    balanced lists probed by ~1-2 queries each — the narrow-item regime of clustered data."""
+    """`mixture`: bench.py --data mixture's generator (256 Gaussian components in super-clusters
+    of 16), balanced lists probed by few queries each — the narrow-item regime of clustered data."""
     import torch
     n, dim, nlist, nprobe, B, k = 1_000_000, 768, 256, 16, 64, 10
     dev = torch.device("cuda", 0)
@@ -66,11 +66,11 @@ def test_cfg2_1m_x_768_nlist256_nprobe16_batch64(data):
         s = torch.cuda.current_stream().cuda_stream
         data_t = torch.empty((n, dim), dtype=torch.float32, device=dev)
         q = torch.empty((B, dim), dtype=torch.float32, device=dev)
-        if data == "mixture":
-            centers = torch.empty((nlist, dim), dtype=torch.float32, device=dev)
-            vdb.gen_normal_device(centers.data_ptr(), nlist * dim, seed=777, stream=s)
-            vdb.gen_mixture_device(data_t.data_ptr(), n, dim, centers.data_ptr(), nlist, 0.5, 12345, 0, s)
-            vdb.gen_mixture_device(q.data_ptr(), B, dim, centers.data_ptr(), nlist, 0.5, 12346, 0, s)
+        if data == "mixture":  # bench.py's two-level mixture: super-clusters of nprobe components
+            import bench
+            centers = bench.mixture_centers(vdb, nlist, nprobe, dim, 0.35, dev)
+            vdb.gen_mixture_device(data_t.data_ptr(), n, dim, centers.data_ptr(), nlist, 0.1, 12345, 0, s)
+            vdb.gen_mixture_device(q.data_ptr(), B, dim, centers.data_ptr(), nlist, 0.1, 12346, 0, s)
         else:
             vdb.gen_normal_device(data_t.data_ptr(), n * dim, seed=12345, stream=s)
             vdb.gen_normal_device(q.data_ptr(), B * dim, seed=12346, stream=s)
@@ -87,7 +87,7 @@ def test_cfg2_1m_x_768_nlist256_nprobe16_batch64(data):
         D, I = od.cpu().numpy(), oi.cpu().numpy().view(np.uint64)
         if data == "mixture":  # the generator: chunked calls give the same rows
             part = torch.empty((1000, dim), dtype=torch.float32, device=dev)
-            vdb.gen_mixture_device(part.data_ptr(), 1000, dim, centers.data_ptr(), nlist, 0.5, 12345, 5000, s)
+            vdb.gen_mixture_device(part.data_ptr(), 1000, dim, centers.data_ptr(), nlist, 0.1, 12345, 5000, s)
             torch.cuda.synchronize()
             assert torch.equal(part, data_t[5000:6000])
         del data_t, ids
