@@ -575,8 +575,9 @@ def run(vdb, args, device, rank, world):
             key += f"/shard0of{args.emulate_shard}"
         if args.opt:  # knobs can change the traffic (never the results)
             key += "/" + ",".join(sorted(args.opt))
-        if tj.get("workload") == key:
-            traffic = tj.get("hbm_bytes_per_scan_launch")
+        entry = tj.get("workloads", {}).get(key) or (tj if tj.get("workload") == key else None)
+        if entry:
+            traffic = entry.get("hbm_bytes_per_scan_launch")
     except (OSError, ValueError):
         pass
 

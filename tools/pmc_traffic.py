@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 --pmc FETCH_SIZE pass over bench.py into HBM bytes per batch.
+"""Summarise rocprofv3 --pmc FETCH_SIZE passes over bench.py into HBM bytes per scan
+launch, one entry per workload, merged into one JSON file that bench.py reads
+(--traffic-json; the bench line's roofline.traffic).
 
 FETCH_SIZE counts the L2's memory-side read requests; on gfx950 it reports exactly half
 of the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, "HBM"), so the
-value is doubled. rocprofv3 reports FETCH_SIZE in KiB.
+value is doubled. rocprofv3 reports FETCH_SIZE in KiB. The scan phase of one batch is one
+ivf_scan_wide dispatch (plus ivf_scan_narrow when the fused scan is off): the bytes of
+all scan dispatches are summed and divided by the number of batches.
 
-usage: tools/pmc_traffic.py <pmc-output-dir> <batches> <workload-key> [out.json]
-The scan phase of one batch is one ivf_scan_wide dispatch (plus ivf_scan_narrow when the
-fused scan is off); the
-bytes of all scan dispatches are summed and divided by the number of batches.
+usage: tools/pmc_traffic.py <out.json> (<pmc-output-dir> <batches> <workload-key>)...
 """
 import csv
 import glob
@@ -18,9 +19,7 @@ import sys
 from collections import defaultdict
 
 
-def main():
-    d, batches, key = sys.argv[1], int(sys.argv[2]), sys.argv[3]
-    out = sys.argv[4] if len(sys.argv) > 4 else None
+def summarise(d, batches, key):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         sys.exit(f"no counter_collection.csv under {d}")
@@ -35,19 +34,33 @@ def main():
             dispatches[name].add(row.get("Dispatch_Id", ""))
     scan = {k: v for k, v in per_kernel.items() if "ivf_scan" in k}
     kib = sum(scan.values())
-    bytes_per_batch = kib * 1024.0 * 2.0 / batches
-    res = {
+    return {
         "workload": key,
-        "hbm_bytes_per_scan_launch": int(bytes_per_batch),
-        "source": "rocprofv3 --pmc FETCH_SIZE (KiB, x2 gfx950 correction) summed over ivf_scan_wide + "
-                  f"ivf_scan_narrow dispatches of {batches} batches",
+        "hbm_bytes_per_scan_launch": int(kib * 1024.0 * 2.0 / batches),
+        "source": "rocprofv3 --pmc FETCH_SIZE (KiB, x2 gfx950 correction) summed over the ivf_scan_* "
+                  f"dispatches of {batches} batches",
         "per_kernel_bytes_per_batch": {k: int(v * 2048 / batches) for k, v in scan.items()},
         "dispatches": {k: len(v) for k, v in dispatches.items() if "ivf_scan" in k},
     }
-    print(json.dumps(res, indent=1))
-    if out:
-        with open(out, "w") as fh:
-            json.dump(res, fh, indent=1)
+
+
+def main():
+    out, rest = sys.argv[1], sys.argv[2:]
+    if len(rest) % 3 or not rest:
+        sys.exit(__doc__)
+    merged = {"workloads": {}}
+    if os.path.exists(out):
+        with open(out) as fh:
+            old = json.load(fh)
+        merged["workloads"].update(old.get("workloads", {}))
+        if "workload" in old:  # the round-1 single-workload form
+            merged["workloads"][old["workload"]] = old
+    for i in range(0, len(rest), 3):
+        res = summarise(rest[i], int(rest[i + 1]), rest[i + 2])
+        merged["workloads"][res["workload"]] = res
+        print(json.dumps(res))
+    with open(out, "w") as fh:
+        json.dump(merged, fh, indent=1)
 
 
 if __name__ == "__main__":

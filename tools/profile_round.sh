@@ -1,17 +1,24 @@
 #!/bin/bash
-# The round's measured evidence, in dependency order (run via gpurun from the repo root):
-# PMC HBM bytes of the scan first (the bench line's roofline.traffic reads them), then the
-# headline bench line, the 1/8-shard emulation, a batch-512 line, and the kernel-trace
-# summary of the one-in-flight bench command. Every GPU step has its own time limit.
-#   usage: bash tools/profile_round.sh <tag>
+# The round's measured evidence (run via gpurun from the repo root), each GPU step under
+# its own time limit, stopping at the first failure:
+#   traffic  PMC FETCH_SIZE of the scan (x2 gfx950 correction) for the iid headline, the
+#            mixture workload and the cfg4 1/8 shard -> gpurun_out/<tag>/traffic.json
+#   mfma     SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CYCLES / GRBM_GUI_ACTIVE of the matrix-core
+#            kernels (coarse bounds, 2x2 assignment bounds) and the re-rank / assign kernels
+#   bench    the headline line and the mixture line, reading traffic.json
+#   trace    rocprofv3 --kernel-trace --stats of the headline bench at 1 and 2 batches in
+#            flight, and of the mixture bench
+#   shard    the cfg4 rank-0-of-8 shard line (sharded 100M build), with its kernel trace
+#   usage: bash tools/profile_round.sh <tag> [steps, comma-separated]
 set -o pipefail
 TAG=${1:-round}
+STEPS=${2:-traffic,mfma,bench,trace}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R" || exit 1
 export TMPDIR=/tmp
-KEY="10000000x768/4096/32/64/10/N1"
+has() { [[ ",$STEPS," == *",$1,"* ]]; }
 run() {  # run <name> <seconds> <cmd...>
     local name=$1 secs=$2
     shift 2
@@ -21,16 +28,49 @@ run() {  # run <name> <seconds> <cmd...>
     echo "[$(date +%T)] $name rc=$rc"
     if [ $rc -ne 0 ]; then tail -30 "$O/$name.log"; exit $rc; fi
 }
-run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ivf_scan_ -d "$O/pmc_f" -o f -f csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --prof-steps 2
-python3 tools/pmc_traffic.py "$O/pmc_f" 8 "$KEY" "$O/traffic.json" | head -4
-run pmc_sq 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES --kernel-include-regex ivf_scan_ -d "$O/pmc_s" -o s -f csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --prof-steps 2
-run bench 400 python3 -u bench.py --traffic-json "$O/traffic.json"
-grep '^{' "$O/bench.log" > "$O/bench.json" && cut -c 1-300 "$O/bench.json"
-run shard 300 python3 -u bench.py --no-cpu --emulate-shard 8 --inflight 3
-grep '^{' "$O/shard.log" > "$O/shard.json"
-run batch512 300 python3 -u bench.py --no-cpu --batch 512 --steps 30
-grep '^{' "$O/batch512.log" > "$O/batch512.json"
-run prof 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight 1
-find "$O/prof" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats.csv" \;
-head -8 "$O/kernel_stats.csv"
+SHORT="--steps 5 --warmup 1 --no-cpu --prof-steps 2"
+CFG4="--cfg cfg4 --emulate-shard 8 --no-cpu --inflight 3"
+if has traffic; then
+    run pmc_iid 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ivf_scan_ -d "$O/pmc_iid" -o f -f csv -- python3 bench.py $SHORT
+    run pmc_mix 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ivf_scan_ -d "$O/pmc_mix" -o f -f csv -- python3 bench.py $SHORT --data mixture
+    python3 tools/pmc_traffic.py "$O/traffic.json" "$O/pmc_iid" 8 "10000000x768/4096/32/64/10/N1" \
+        "$O/pmc_mix" 8 "10000000x768/4096/32/64/10/N1/mixture" | tail -3
+fi
+if has traffic4; then
+    run pmc_cfg4 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ivf_scan_ -d "$O/pmc_cfg4" -o f -f csv -- python3 bench.py $CFG4 --steps 5 --warmup 1 --prof-steps 2
+    python3 tools/pmc_traffic.py "$O/traffic.json" "$O/pmc_cfg4" 8 "100000000x768/16384/64/64/10/N1/shard0of8" | tail -3
+fi
+if has mfma; then
+    # the bench build's assignment (10M x 4096 bounds on the 2x2 kernel) and the search
+    # batches' coarse step; rocprofv3 -L first, for the record of the counters present
+    rocprofv3 -L > "$O/counters_available.txt" 2>&1 || true
+    run pmc_mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "ivf_coarse|ivf_assign|ivf_select_rerank" -d "$O/pmc_mfma" -o m -f csv -- python3 bench.py $SHORT
+    run trace_mfma 300 rocprofv3 --kernel-trace --stats --kernel-include-regex "ivf_coarse|ivf_assign|ivf_select_rerank" -d "$O/trace_mfma" -o t -f csv -- python3 bench.py $SHORT
+    python3 tools/mfma_report.py "$O/pmc_mfma" "$O/trace_mfma" "$O/mfma.json" | tail -30
+fi
+if has bench; then
+    run bench 400 python3 -u bench.py --traffic-json "$O/traffic.json" --host-api
+    grep '^{' "$O/bench.log" > "$O/bench.json" && cut -c 1-400 "$O/bench.json"
+    run bench_mix 400 python3 -u bench.py --traffic-json "$O/traffic.json" --data mixture --host-api
+    grep '^{' "$O/bench_mix.log" > "$O/bench_mix.json" && cut -c 1-400 "$O/bench_mix.json"
+fi
+if has trace; then
+    for inf in 1 2; do
+        run trace_inflight$inf 300 rocprofv3 --kernel-trace --stats -d "$O/trace_inflight$inf" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight $inf
+        find "$O/trace_inflight$inf" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_inflight$inf.csv" \;
+        head -6 "$O/kernel_stats_inflight$inf.csv"
+    done
+    run trace_mix 300 rocprofv3 --kernel-trace --stats -d "$O/trace_mix" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight 1 --data mixture
+    find "$O/trace_mix" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_mixture.csv" \;
+    head -6 "$O/kernel_stats_mixture.csv"
+fi
+if has shard; then
+    run shard 600 python3 -u bench.py $CFG4 --shard-check 4 --traffic-json "$O/traffic.json"
+    grep '^{' "$O/shard.log" > "$O/shard.json" && cut -c 1-400 "$O/shard.json"
+fi
+if has shardtrace; then
+    run trace_cfg4 600 rocprofv3 --kernel-trace --stats -d "$O/trace_cfg4" -o k -f csv -- python3 bench.py $CFG4 --steps 20 --warmup 2 --inflight 1
+    find "$O/trace_cfg4" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_cfg4_shard.csv" \;
+    head -6 "$O/kernel_stats_cfg4_shard.csv"
+fi
 echo "profile_round $TAG done"
