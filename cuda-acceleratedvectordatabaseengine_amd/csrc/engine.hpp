@@ -267,7 +267,7 @@ struct vdb_ivf {
     struct SearchSlot {
         DevBuf<float> qpad, cd, cdelta, part_d, slot_d, carry_d;
         DevBuf<uint64_t> part_i, slot_i, carry_i;
-        DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters, l1base, cand;
+        DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters, l1base, cand, thr;
         DevBuf<uint2> l1_items;
         DevBuf<float> l1_d;
         DevBuf<uint64_t> l1_i;
@@ -1153,7 +1153,7 @@ struct vdb_ivf {
         const size_t max_wide = max_items / 4 + BP + 1;
         const bool grow = w.items_w.cap < max_wide || w.qpad.cap < (size_t)B * dp || w.cd.cap < (size_t)B * nlist ||
                           w.cdelta.cap < (size_t)B * nlist || w.cand.cap < (size_t)B * nlist ||
-                          w.probes.cap < BP || w.items.cap < max_items || w.part_d.cap < max_items * k ||
+                          w.probes.cap < BP || w.thr.cap < BP || w.items.cap < max_items || w.part_d.cap < max_items * k ||
                           w.slot_d.cap < BP * k || w.carry_d.cap < (size_t)P * k || w.l1_items.cap < max_l1 ||
                           w.l1_d.cap < max_l1 * k;
         if (!grow) return;
@@ -1169,6 +1169,7 @@ struct vdb_ivf {
         w.pbs.ensure(BP);
         w.counters.ensure(8);
         w.l1base.ensure(BP);
+        w.thr.ensure(BP);
         w.l1_items.ensure(max_l1);
         w.l1_d.ensure(max_l1 * k);
         w.l1_i.ensure(max_l1 * k);
@@ -1223,11 +1224,11 @@ struct vdb_ivf {
         // segments per item: one per wave (more adds tail latency, no throughput)
         const uint32_t segs_item = segs_item_opt ? segs_item_opt : (uint32_t)waves;
         vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? (int)wide_group : 0, segs_item, w.items.p, w.items_w.p,
-                          w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, s);
+                          w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, w.thr.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
         vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
-                                wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item, 0};
+                                wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item, 0, w.thr.p};
         if (wide && fused_scan) {
             // one persistent grid takes both queues (no side stream, no fork/join)
             // (narrow_blocks counts 4-wave workgroups: as many waves start on the narrow queue)

@@ -111,6 +111,18 @@ __global__ __launch_bounds__(256) void ivf_coarse_distances(const float4* __rest
 // unordered); keeps every selected list id valid.
 __device__ __forceinline__ float nan_last(float d) { return d == d ? d : __builtin_inff(); }
 
+// Order-preserving float <-> uint32 map (a < b as floats <=> enc(a) < enc(b) as
+// unsigned), so shared thresholds can be lowered with integer atomic minimum.
+__device__ __forceinline__ uint32_t ord_enc(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float ord_dec(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+constexpr uint32_t kThrInf = 0xFF800000u;  // ord_enc(+inf)
+
+
 // ============================================================================
 // Coarse quantiser, selection part: the first min(nprobe, nlist) lists by
 // (dist, list_id) — partial_sort on std::pair (cpp:324-333). One wave per query.
@@ -693,7 +705,8 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
                                                         uint32_t* __restrict__ nseg_qp,
                                                         uint32_t* __restrict__ l1base_qp,
                                                         uint2* __restrict__ l1_items,
-                                                        unsigned long long* __restrict__ stats) {
+                                                        unsigned long long* __restrict__ stats,
+                                                        uint32_t* __restrict__ thr) {
     __shared__ uint32_t keys[kPlanMaxPairs];
     __shared__ uint32_t starts[kPlanMaxPairs + 1];
     __shared__ uint32_t base_n[kPlanMaxPairs];
@@ -705,6 +718,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     const uint32_t wide = wide_on;  // wide group size (0: no wide items)
 
     if (tid == 0) s_nvalid = 0;
+    for (uint32_t i = tid; i < BP; i += blockDim.x) thr[i] = kThrInf;  // the scan's shared thresholds
     for (uint32_t i = tid; i < NP; i += blockDim.x) {
         uint32_t key = kInvalidKey;
         if (i < BP) {
@@ -1022,23 +1036,33 @@ __device__ __forceinline__ f2 dist_term2(f2 acc, f2 q, f2 x) {
     }
 }
 
-// One wave of a wide item: segment it.seg * 4 + wave of list it.list against GP
-// query pairs read from LDS as interleaved pairs (q[2p][d], q[2p+1][d]). Two queries
-// run per packed instruction (v_pk_add_f32 / v_pk_mul_f32 round each half exactly
-// like the scalar ops); every query's sum still runs in d order. Per query only the
-// k-th distance lives in registers; the top-k lists live in LDS (tk_d / tk_i), and
-// the insertion code exists once, looping over the queries that have candidates.
+// One wave of a wide item: segment `seg` of list it.list against GP query pairs read
+// from LDS as interleaved pairs (q[2p][d], q[2p+1][d]): the item's pairs are staged
+// tile-major with `pstride` pairs per tile, and this wave takes the GP pairs starting at
+// qlds (its queries are the item's q0 .. q0 + np - 1). Two queries run per packed
+// instruction (v_pk_add_f32 / v_pk_mul_f32 round each half exactly like the scalar
+// ops); every query's sum still runs in d order. Per query only the k-th distance
+// lives in registers; the top-k lists live in LDS (tk_d / tk_i), and the insertion
+// code exists once, looping over the queries that have candidates.
 #ifndef VDB_BIG_GROUP_PREFETCH
 #define VDB_BIG_GROUP_PREFETCH 0  // 1 spills ~100 VGPRs in the 16-pair instantiation (measured with -Rpass-analysis)
 #endif
 constexpr bool kBigGroupPrefetch = VDB_BIG_GROUP_PREFETCH != 0;
 
-template <int GP, int M>
-__device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds, float* tk_d,
-                                               uint64_t* tk_i, const uint32_t seg) {
+// Shared thresholds (exact): a candidate strictly worse than a k-th distance that some
+// wave has already reached on the same (query, list) cannot be in that list's top-k —
+// those k candidates are in that wave's segment partial and beat it — so it is never
+// inserted. Partials may then hold fewer than k entries; the merges take the top-min(k,
+// n_l) of the union, which is unchanged. Ties (equal distance) are always kept.
+template <int GP, int M, bool SPLIT>
+__device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds,
+                                               const uint32_t pstride_rt, const int q0, const int np, float* tk_d,
+                                               uint64_t* tk_i, uint32_t* s_thr, const uint32_t seg) {
     constexpr int G = 2 * GP;
+    // pairs per staged tile row: the wave's own pair count unless the item's queries are
+    // split between two halves of the workgroup (a wave-uniform scalar either way)
+    const uint32_t pstride = SPLIT ? pstride_rt : (uint32_t)GP;
     const uint32_t d4 = a.d4;
-    const int np = (int)it.npairs;
     const int lane = lane_id();
     const uint32_t count = a.count[it.list];
     const uint32_t seg_vectors = a.seg_blocks * 64;
@@ -1077,7 +1101,7 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
     auto compute = [&](const float4 x, uint32_t t, auto) {
         const f2 xlo = {x.x, x.y}, xhi = {x.z, x.w};
         if constexpr (kDirect) {
-            const float4* cur = qlds + (size_t)t * GP * 2;
+            const float4* cur = qlds + (size_t)t * pstride * 2;
 #pragma unroll
             for (int p = 0; p < GP; ++p) {
                 const float4 lo = cur[2 * p], hi = cur[2 * p + 1];
@@ -1087,7 +1111,7 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
                 acc[p] = dist_term2<M, 1>(acc[p], f2{hi.z, hi.w}, xhi);
             }
         } else {
-            const float4* nxt = qlds + (size_t)(t + 1 == d4 ? 0 : t + 1) * GP * 2;
+            const float4* nxt = qlds + (size_t)(t + 1 == d4 ? 0 : t + 1) * pstride * 2;
 #pragma unroll
             for (int p = 0; p < GP; ++p) {
                 const float4 lo = qb[p][0], hi = qb[p][1];
@@ -1102,11 +1126,15 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
     };
     auto finish = [&](uint32_t j, uint64_t id) {
         const bool valid = j * 64 + lane < nv;
+        // the item's shared thresholds (the other waves' progress on the same list)
+        float th[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) th[g] = g < np ? fminf(kd[g], ord_dec(s_thr[g])) : kd[g];
         uint32_t pend = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const float dist = dist_finish<M>((g & 1) ? acc[g >> 1].y : acc[g >> 1].x);
-            if (g < np && __ballot(valid && dist <= kd[g])) pend |= 1u << g;
+            if (g < np && __ballot(valid && dist <= th[g])) pend |= 1u << g;
         }
         if (a.diag & 1) pend = 0;  // DIAGNOSTIC: no top-k maintenance (results invalid)
         if (pend) {
@@ -1119,7 +1147,7 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
                 for (int g = 0; g < G; ++g)
                     if (g == gs) {
                         dist = dist_finish<M>((g & 1) ? acc[g >> 1].y : acc[g >> 1].x);
-                        kdg = kd[g];
+                        kdg = th[g];
                     }
                 float* sd = tk_d + gs * k;
                 uint64_t* si = tk_i + gs * k;
@@ -1137,6 +1165,8 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
 #pragma unroll
                 for (int g = 0; g < G; ++g)
                     if (g == gs) kd[g] = nkd;
+                // a full list's k-th below the shared threshold lowers it for the item's waves
+                if (nkd < kdg && lane == 0) atomicMin(&s_thr[gs], ord_enc(nkd));
             } while (pend);
         }
 #pragma unroll
@@ -1145,8 +1175,13 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
     // more than 8 pairs: fewer tiles in flight (the pairs' query registers take the rest)
     constexpr int T = GP <= 8 ? kTilePipe : (kBigGroupPrefetch ? kTilePipe / 4 : kTilePipe / 2);
     stream_blocks<T>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
+    // the segment's k-th distances lower the list-wide thresholds for later items
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+        if (g < np && lane == 0 && kd[g] < __builtin_inff())
+            atomicMin(&a.thr[it.pair_start + q0 + g], ord_enc(kd[g]));
     for (int g = 0; g < np; ++g) {
-        const uint32_t part = a.part_base_sorted[it.pair_start + g] + seg;
+        const uint32_t part = a.part_base_sorted[it.pair_start + q0 + g] + seg;
         if (lane < k) {
             a.part_d[(size_t)part * k + lane] = tk_d[g * k + lane];
             a.part_i[(size_t)part * k + lane] = tk_i[g * k + lane];
@@ -1198,20 +1233,28 @@ __device__ __forceinline__ void drain_narrow(const ScanArgs& a) {
     }
 }
 
-// ivf_scan_wide: the large lists. W = 4: two 4-wave workgroups per CU, items of up to
-// 16 queries; W = 8: one 8-wave workgroup per CU, items of up to 32 queries (half the
-// re-reads of lists probed by many queries, twice the VALU work per byte). A workgroup
-// takes one wide item at a time: its segments x its queries, staged once in LDS.
+// ivf_scan_wide: the large lists. A workgroup takes one wide item at a time: a range of
+// a list's segments x up to 4W of the list's queries, staged once in LDS as pairs.
+//  * W = 4: two 4-wave workgroups per CU, items of up to 16 queries; the 4 waves take the
+//    item's segments dynamically, each against all of the item's queries.
+//  * W = 8: one 8-wave workgroup per CU, items of up to 32 queries, so a list probed by
+//    17-32 queries of the batch is streamed from HBM once instead of twice. Up to 16
+//    queries the 8 waves share the segments as above. Beyond 16 the waves split into
+//    two halves of 4, each half taking the item's segments in the same order against
+//    its half of the queries: the two waves streaming one segment run side by side on
+//    the CU, so the second read is served on-chip, and every wave keeps at most 8 query
+//    pairs in registers (the code path that does not spill).
 template <int M, int W>
-__global__ __launch_bounds__(64 * W, W == 4 ? 2 : 1) void ivf_scan_wide(ScanArgs a) {
+__global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
     constexpr int GW = 4 * W;  // queries per item at most
     // Dynamic LDS: [d4][gpv][2] float4 of staged query pairs (tile-major), then per wave
-    // GW x k top-k ids (u64), then the same for distances (f32).
+    // kWaveQueries x k top-k ids (u64), then the same for distances (f32).
     extern __shared__ __attribute__((aligned(16))) float4 qlds[];
     const uint32_t d4 = a.d4;
-    uint64_t* tk_i = (uint64_t*)(qlds + (size_t)(GW / 2) * d4 * 2) + (size_t)wave_index() * GW * a.k;
-    float* tk_d = (float*)((uint64_t*)(qlds + (size_t)(GW / 2) * d4 * 2) + (size_t)W * GW * a.k) +
-                  (size_t)wave_index() * GW * a.k;
+    const uint32_t wv = wave_index();
+    uint64_t* tk_i = (uint64_t*)(qlds + (size_t)(GW / 2) * d4 * 2) + (size_t)wv * kWaveQueries * a.k;
+    float* tk_d = (float*)((uint64_t*)(qlds + (size_t)(GW / 2) * d4 * 2) + (size_t)W * kWaveQueries * a.k) +
+                  (size_t)wv * kWaveQueries * a.k;
     const uint32_t n_wide = a.counters[3];
     // Items of one list are adjacent in the plan; dispatching them in a strided order
     // mixes lists of many queries (VALU-heavy) with lists of few (HBM-heavy) on the
@@ -1224,7 +1267,8 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 2 : 1) void ivf_scan_wide(ScanArgs
     // start on the narrow queue, and every wave drains it once the wide queue is empty.
     if (a.fused && blockIdx.x + a.fused >= gridDim.x) drain_narrow<M>(a);
     __shared__ uint32_t s_next;
-    __shared__ uint32_t s_seg;  // next segment of the current item
+    __shared__ uint32_t s_seg[2];   // next segment of the current item (per query half)
+    __shared__ uint32_t s_thr[GW];  // per query of the item: the best k-th distance reached
     for (;;) {
         // persistent workgroups pull items from a queue (one atomic per item)
         if (threadIdx.x == 0) s_next = atomicAdd(&a.work[1], 1u);
@@ -1232,12 +1276,16 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 2 : 1) void ivf_scan_wide(ScanArgs
         const uint32_t b = s_next;
         if (b >= n_wide) break;
         const uint32_t item = stride > 1 ? (uint32_t)(((uint64_t)b * stride) % n_wide) : b;
-        const ScanItem it = a.items_w[item];
+        ScanItem it = a.items_w[item];
+        it.list = __builtin_amdgcn_readfirstlane(it.list);  // (wave-uniform: scalar address math)
+        it.seg = __builtin_amdgcn_readfirstlane(it.seg);
+        it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
+        it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
         const int np = (int)it.npairs;
         const int gp = (np + 1) / 2;
-        if (threadIdx.x == 0) s_seg = 0;  // visible after the staging barrier below
-        const int gpv = (a.diag & 2) ? 1 : gp;  // every pair count 1..GW/2 has its own instantiation
-                                                // (DIAGNOSTIC diag&2: one pair only, results invalid)
+        if (threadIdx.x < 2) s_seg[threadIdx.x] = 0;  // visible after the staging barrier below
+        if (threadIdx.x < (uint32_t)np) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
+        const int gpv = (a.diag & 2) ? 1 : gp;  // (DIAGNOSTIC diag&2: one pair only, results invalid)
         for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
             const uint32_t t = e / gpv, p = e - t * gpv;
             const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
@@ -1247,40 +1295,39 @@ __global__ __launch_bounds__(64 * W, W == 4 ? 2 : 1) void ivf_scan_wide(ScanArgs
             qlds[(t * gpv + p) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
         }
         __syncthreads();
-        // the item's segments [seg0, seg1) go to the waves dynamically: a wave that
-        // finishes early takes the next one, so waves idle only at the item's end
+        // This wave's queries: all of the item's (one group), or its half's (W = 8, more
+        // than 8 pairs). Pairs [p0, p0 + gw) are queries 2 p0 .. 2 p0 + nq - 1.
+        const bool split = W == 8 && gpv > 8;
+        const uint32_t half = split ? wv >> 2 : 0u;
+        const int gh = (gpv + 1) / 2;
+        const int p0 = split ? (int)half * gh : 0;
+        const int gw = split ? (half ? gpv - gh : gh) : gpv;
+        const int q0 = 2 * p0;
+        const int nq = split ? (half ? np - q0 : min(np, 2 * gh)) : ((a.diag & 2) ? min(np, 2) : np);
+        const float4* qw = qlds + (size_t)p0 * 2;
+        // the item's segments [seg0, seg1) go to the waves (of each half) dynamically: a
+        // wave that finishes early takes the next one, so waves idle only at the item's end
         const uint32_t seg_vectors = a.seg_blocks * 64;
         const uint32_t nseg = (a.count[it.list] + seg_vectors - 1) / seg_vectors;
         const uint32_t seg0 = it.seg * a.segs_item, seg1 = min(nseg, seg0 + a.segs_item);
         for (;;) {
             uint32_t sg = 0;
-            if (lane_id() == 0) sg = atomicAdd(&s_seg, 1u);
+            if (lane_id() == 0) sg = atomicAdd(&s_seg[half], 1u);
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
-            switch (gpv) {
-                case 1: scan_wide_wave<1, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                case 2: scan_wide_wave<2, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                case 3: scan_wide_wave<3, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                case 4: scan_wide_wave<4, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                case 5: scan_wide_wave<5, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                case 6: scan_wide_wave<6, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                case 7: scan_wide_wave<7, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                case 8: scan_wide_wave<8, M>(a, it, qlds, tk_d, tk_i, sg); break;
+#define VDB_WW(GPN)                                                                       \
+    case GPN:                                                                             \
+        if (W == 8 && split) scan_wide_wave<GPN, M, true>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg); \
+        else scan_wide_wave<GPN, M, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);           \
+        break;
+            switch (gw) {
+                VDB_WW(1) VDB_WW(2) VDB_WW(3) VDB_WW(4) VDB_WW(5) VDB_WW(6) VDB_WW(7)
                 default:
-                    if constexpr (W == 8) {
-                        switch (gpv) {
-                            case 9: scan_wide_wave<9, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                            case 10: scan_wide_wave<10, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                            case 11: scan_wide_wave<11, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                            case 12: scan_wide_wave<12, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                            case 13: scan_wide_wave<13, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                            case 14: scan_wide_wave<14, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                            case 15: scan_wide_wave<15, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                            default: scan_wide_wave<16, M>(a, it, qlds, tk_d, tk_i, sg); break;
-                        }
-                    }
+                    if (W == 8 && split) scan_wide_wave<8, M, true>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
+                    else scan_wide_wave<8, M, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
                     break;
             }
+#undef VDB_WW
         }
         __syncthreads();  // qlds is restaged by the next wide item
     }
@@ -1947,12 +1994,12 @@ void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint3
                  uint32_t P, uint32_t group, int wide, uint32_t segs_item, ScanItem* items, ScanItem* items_w,
                  uint32_t* counters,
                  uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp, uint32_t* nseg_qp,
-                 uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats, hipStream_t s) {
+                 uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats, uint32_t* thr, hipStream_t s) {
     uint32_t np = 1;
     while (np < B * P) np <<= 1;
     ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, (uint32_t)wide, segs_item, items,
                                        items_w, counters, sorted_pair, part_base_sorted, part_base_qp, nseg_qp,
-                                       l1base_qp, l1_items, stats);
+                                       l1base_qp, l1_items, stats, thr);
 }
 
 void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes, const uint32_t* count_global,
@@ -1978,7 +2025,7 @@ static constexpr size_t kWideStaticLds = 64;  // ivf_scan_wide's static LDS (the
 
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves) {
     const size_t gw = 4 * (size_t)waves;
-    return (gw / 2) * d4 * 2 * sizeof(float4) + (size_t)waves * gw * k * (sizeof(float) + sizeof(uint64_t));
+    return (gw / 2) * d4 * 2 * sizeof(float4) + (size_t)waves * kWaveQueries * k * (sizeof(float) + sizeof(uint64_t));
 }
 
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves) {

@@ -22,7 +22,8 @@ constexpr uint32_t kMergeBlocks = 256;  // level-1 partial merge: workgroups (gr
 constexpr int kTilePipeNarrow = 4;         // the same for narrow items (queries held in SGPRs)
 constexpr int kTileAlign = kTilePipe;      // D4 is padded to whole pipeline rounds
 constexpr int kMergeFan = 32;              // segment partials folded per level-1 merge wave
-constexpr int kWideGroup = 16;             // max pairs per wide scan item (large lists)
+constexpr int kWideGroup = 16;             // max queries per wide scan item (4-wave items)
+constexpr int kWaveQueries = 16;           // max queries one wave of a wide item computes (8 pairs)
 constexpr int kWideMinSeg = 4;             // lists with >= 4 segments are scanned by wide items
 constexpr int kNarrowMax = 4;              // pairs per narrow scan item
 constexpr int kPlanMaxPairs = 8192;        // batch * nprobe per plan launch
@@ -70,7 +71,7 @@ void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint3
                  uint32_t B, uint32_t P, uint32_t group, int wide, uint32_t segs_item, ScanItem* items, ScanItem* items_w,
                  uint32_t* counters, uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp,
                  uint32_t* nseg_qp, uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats,
-                 hipStream_t s);
+                 uint32_t* thr, hipStream_t s);
 void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes, const uint32_t* count_global,
                            const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                            const uint2* l1_items, const uint32_t* counters, const float* part_d,
@@ -99,6 +100,9 @@ struct ScanArgs {
     uint32_t segs_item;    // segments per wide item (>= 4; the 4 waves take them dynamically)
     uint32_t fused;        // ivf_scan_wide also drains the narrow queue (R = 1); the last `fused`
                            // workgroups start on narrow items (0: narrow items on their own kernel)
+    uint32_t* thr;         // per sorted (query, probe) pair: the best k-th distance any wave has
+                           // reached on that list so far (order-preserving uint encoding, reset
+                           // by the plan kernel); candidates strictly worse are never inserted
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Knob sweep (one build, many timings) on a bench workload.
+
+Builds the workload's index once (bench.build_index / build_index_sharded), then times
+the scan for each engine option set (HIP events of the engine's profile, one batch in
+flight) and the wall time per batch. Options never change results except diag (timing
+experiments only).
+usage: tools/knob_sweep.py cfg3|cfg4|mix "wide_group=32" "seg_vectors=1024,segs_per_item=8" ...
+  cfg4 = rank 0 of the 8-way sharded 100M x 768 index (the per-GPU work of 8 GPUs)
+"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+DEFAULTS = {"seg_vectors": 0, "segs_per_item": 0, "wide_stride": 1, "diag": 0, "fused_scan": 1, "narrow_blocks": 64,
+            "wide_group": 16}
+
+
+def main():
+    wl, sets = sys.argv[1], sys.argv[2:] or [""]
+    big = wl == "cfg4"
+    args = bench.argparse.Namespace(dim=768, nvec=100_000_000 if big else 10_000_000, nlist=16384 if big else 4096,
+                                    nprobe=64 if big else 32, batch=64, k=10, train=100_000, build_chunk=10_000_000,
+                                    data="mixture" if wl == "mix" else "iid", mix_components=0, mix_group=0,
+                                    mix_spread=0.35, mix_sigma=0.1)
+    vdb = bench.load_vdb()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    with torch.cuda.stream(torch.cuda.Stream(dev)):
+        if args.data == "mixture":
+            args.centers = bench.mixture_centers(vdb, args.nlist, args.nprobe, args.dim, args.mix_spread, dev)
+        if big:
+            idx, _ = bench.build_index_sharded(vdb, args, dev, 0, 8)
+        else:
+            idx, _ = bench.build_index(vdb, args, dev, 0, 1)
+        st = torch.cuda.current_stream()
+        B, steps = 64, 12
+        q = torch.empty((steps * B, 768), dtype=torch.float32, device=dev)
+        bench.fill_rows(vdb, args, q, 0, steps * B, 12346, st.cuda_stream)
+        od = torch.empty((B, 10), dtype=torch.float32, device=dev)
+        oi = torch.empty((B, 10), dtype=torch.int64, device=dev)
+        for s in sets:
+            opts = [o.split("=") for o in s.split(",") if o]
+            for n, v in opts:
+                idx.set_option(n, int(v))
+            for j in range(2):
+                idx.search_device(q[j * B:].data_ptr(), B, args.nprobe, 10, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
+            torch.cuda.synchronize()
+            idx.profile_enable(True)
+            idx.profile_reset()
+            t0 = time.perf_counter()
+            for j in range(steps):
+                idx.search_device(q[j * B:].data_ptr(), B, args.nprobe, 10, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
+            torch.cuda.synchronize()
+            wall = (time.perf_counter() - t0) / steps * 1e3
+            p = idx.profile_read()
+            idx.profile_enable(False)
+            n = max(p["scan_launches"], 1)
+            alg = p["scan_bytes"] / max(p["batches"], 1)
+            print(json.dumps({"workload": wl, "opts": s, "scan_ms": round(p["scan_ms"] / n, 3),
+                              "search_ms": round(p["total_ms"] / n, 3), "wall_ms": round(wall, 3),
+                              "alg_GB": round(alg / 1e9, 2), "frac": round(alg / (p["scan_ms"] / n * 1e-3) / 8e12, 4)}),
+                  flush=True)
+            for n_, _ in opts:  # back to defaults
+                idx.set_option(n_, DEFAULTS[n_])
+
+
+if __name__ == "__main__":
+    main()
