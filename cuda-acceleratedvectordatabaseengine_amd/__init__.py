@@ -50,7 +50,9 @@ class _Config(ctypes.Structure):
 class CacheStats(ctypes.Structure):
     _fields_ = [("capacity_bytes", ctypes.c_uint64), ("resident_bytes", ctypes.c_uint64),
                 ("resident_lists", ctypes.c_uint64), ("loads", ctypes.c_uint64), ("evictions", ctypes.c_uint64),
-                ("bytes_loaded", ctypes.c_uint64), ("file_bytes_read", ctypes.c_uint64)]
+                ("bytes_loaded", ctypes.c_uint64), ("file_bytes_read", ctypes.c_uint64),
+                ("subbatches", ctypes.c_uint64), ("prefetches", ctypes.c_uint64), ("sync_loads", ctypes.c_uint64),
+                ("io_uring", ctypes.c_int32), ("o_direct", ctypes.c_int32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -584,6 +584,11 @@ int vdb_ivf_cache_stats(vdb_ivf* h, vdb_ivf_cache_stats_t* out) {
         for (uint32_t l = 0; l < h->nlist && h->tiered(); ++l) n += h->cache_off[l] != vdb_ivf::kAbsent;
         out->resident_lists = n;
         out->file_bytes_read = h->file_bytes_read;
+        out->subbatches = h->tier_subbatches;
+        out->prefetches = h->tier_prefetches;
+        out->sync_loads = h->tier_sync_loads;
+        out->io_uring = h->uring && h->uring->uring() ? 1 : 0;
+        out->o_direct = h->home_fd_direct >= 0 ? 1 : 0;
     });
 }
 

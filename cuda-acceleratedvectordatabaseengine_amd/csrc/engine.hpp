@@ -38,6 +38,7 @@
 
 #include "../../include/vdb_ivf.h"
 #include "kernels.hpp"
+#include "uring.hpp"
 
 namespace vdbe {
 
@@ -250,15 +251,31 @@ struct vdb_ivf {
     bool tier_ev_used = false;
 
     // File home for the tier (vdb_ivf_open_lists): the lists stay in an index file written
-    // by vdb_ivf_save and are read into the cache on demand (pread -> pinned staging ->
-    // HBM -> pad + interleave kernels), instead of living in host memory.
+    // by vdb_ivf_save and are read into the cache on demand: io_uring reads (O_DIRECT when
+    // the file system allows it) into a ring of page-locked staging buffers, H2D copies,
+    // then pad + interleave kernels into the cache's block layout.
     int home_fd = -1;
+    int home_fd_direct = -1;         // O_DIRECT descriptor of the same file (or -1: buffered)
     std::vector<uint64_t> file_off;  // per list: file offset of its ids (vectors follow)
-    DevBuf<float> fstage[2];         // pinned: row-major vectors of a chunk
-    DevBuf<uint64_t> istage[2];      // pinned: ids of a chunk
-    hipEvent_t fstage_done[2] = {nullptr, nullptr};
-    DevBuf<float> drows, dpad;       // device: a chunk's rows, then zero-padded to dp
+    struct Stage {                   // one page-locked staging buffer of the read ring
+        DevBuf<char> buf;
+        hipEvent_t copied = nullptr;  // its H2D copies are done: the buffer may be refilled
+        bool copying = false;
+        int reads = 0;                // reads in flight
+        uint64_t m = 0, dst_block = 0;
+        size_t ids_delta = 0, vec_delta = 0;
+    };
+    static constexpr int kStages = 8;
+    Stage stages[kStages];
+    std::unique_ptr<UringReader> uring;
+    DevBuf<float> drows, dpad;       // device: a chunk's rows, then zero-padded to dp (search stream)
+    DevBuf<float> drows_cs, dpad_cs; // the same for loads on copy_stream (they may run concurrently)
     uint64_t file_bytes_read = 0;
+    // tier pipeline: loads for the next sub-batch run on copy_stream beside the scan
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t sb_done[2] = {nullptr, nullptr}, load_ev = nullptr, tier_call_ev = nullptr;
+    bool tier_call_used = false;
+    uint64_t tier_prefetches = 0, tier_sync_loads = 0, tier_subbatches = 0;
 
     // Search workspaces: a ring of slots so that searches issued on different streams
     // run concurrently (one batch's small kernels and scan tail overlap the next
@@ -334,9 +351,13 @@ struct vdb_ivf {
         }
         for (auto& e : gev) (void)hipEventDestroy(e);
         if (home_fd >= 0) ::close(home_fd);
-        for (auto& e : fstage_done)
+        if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+        for (auto& st : stages)
+            if (st.copied) (void)hipEventDestroy(st.copied);
+        for (hipEvent_t e : {sb_done[0], sb_done[1], load_ev, tier_call_ev, tier_ev})
             if (e) (void)hipEventDestroy(e);
-        if (tier_ev) (void)hipEventDestroy(tier_ev);
+        if (copy_stream) (void)hipStreamDestroy(copy_stream);
+        if (home_fd_direct >= 0) ::close(home_fd_direct);
         for (auto& e : events) {
             (void)hipEventDestroy(e.begin);
             (void)hipEventDestroy(e.coarse_end);
@@ -687,6 +708,9 @@ struct vdb_ivf {
     void upload_scan_directory(hipStream_t s) {
         const uint64_t* src = block_off.data();
         if (tiered()) {
+            // the previous upload's source must have been read before it is rewritten
+            if (tier_ev_used) HIPCHECK(hipEventSynchronize(tier_ev));
+            dir_stage.host = true;
             uint64_t* st = dir_stage.ensure(nlist);
             for (uint32_t l = 0; l < nlist; ++l) st[l] = cache_off[l] == kAbsent ? 0 : cache_off[l];
             src = st;
@@ -701,63 +725,107 @@ struct vdb_ivf {
         tier_ev_used = true;
     }
 
-    // Make `lists` resident (ids may repeat; lists not stored here or empty are
-    // skipped). False if together they exceed the cache. Copies are ordered on s.
-    bool make_resident(const uint32_t* lists, size_t n, hipStream_t s) {
-        ++use_tick;
-        std::vector<uint8_t> in_set(nlist, 0);
-        std::vector<uint32_t> want, miss;
+    // Cache residency planning. Lists that are empty or not stored here are never
+    // cached. `want` (unique lists) must all be resident afterwards; lists marked in
+    // `protect` are never evicted; a victim is the cached list whose next use (rank()
+    // : larger = later, UINT64_MAX = never) is furthest away, then the least recently
+    // used. Returns false, changing nothing, when `want` cannot be placed (over capacity,
+    // or fragmentation with `repack` off); with `repack` every cached list outside `want`
+    // is dropped and `want` is re-laid from offset 0 when fragmentation blocks a load.
+    // The cache map changes at once; the data moves with load_lists, in stream order.
+    template <class Rank>
+    bool plan_loads(const std::vector<uint32_t>& want, const std::vector<uint8_t>& protect, Rank&& rank, bool repack,
+                    std::vector<std::pair<uint32_t, uint64_t>>& loads) {
+        loads.clear();
         uint64_t need = 0;
-        for (size_t i = 0; i < n; ++i) {
-            const uint32_t l = lists[i];
-            if (l >= nlist || in_set[l] || !owned[l] || count[l] == 0) continue;
-            in_set[l] = 1;
-            want.push_back(l);
+        std::vector<uint32_t> miss;
+        for (uint32_t l : want) {
             need += list_blocks(l);
-            last_use[l] = use_tick;
             if (cache_off[l] == kAbsent) miss.push_back(l);
         }
         if (need > cache_blocks) return false;
         if (miss.empty()) return true;
-        quiesce();  // searches on other streams may still read the lists evicted below
         auto by_size = [&](uint32_t a, uint32_t b) { return count[a] != count[b] ? count[a] > count[b] : a < b; };
         std::vector<uint32_t> victims;
         for (uint32_t l = 0; l < nlist; ++l)
-            if (cache_off[l] != kAbsent && !in_set[l]) victims.push_back(l);
-        std::sort(victims.begin(), victims.end(),
-                  [&](uint32_t a, uint32_t b) { return last_use[a] != last_use[b] ? last_use[a] < last_use[b] : a < b; });
+            if (cache_off[l] != kAbsent && !protect[l]) victims.push_back(l);
+        std::vector<uint64_t> rk(nlist, 0);
+        for (uint32_t v : victims) rk[v] = rank(v);
+        std::sort(victims.begin(), victims.end(), [&](uint32_t a, uint32_t b) {
+            if (rk[a] != rk[b]) return rk[a] > rk[b];
+            return last_use[a] != last_use[b] ? last_use[a] < last_use[b] : a < b;
+        });
+        // dry run on a copy of the extent map, so a failed plan changes nothing
+        const std::map<uint64_t, uint64_t> free_save = free_ext;
+        const std::vector<uint64_t> off_save = cache_off;
+        const uint64_t used_save = cache_used, res_save = resident_n;
         std::sort(miss.begin(), miss.end(), by_size);
         size_t vi = 0;
+        uint64_t evicted = 0;
         for (size_t m = 0; m < miss.size(); ++m) {
             const uint32_t l = miss[m];
             uint64_t off;
             while ((off = cache_alloc(list_blocks(l))) == kAbsent && vi < victims.size()) {
                 cache_free(victims[vi++]);
-                ++cache_evictions;
+                ++evicted;
             }
             if (off == kAbsent) {
-                // fragmented: keep only this batch's lists, packed from offset 0 (they fit)
+                if (!repack) {  // undo: the caller falls back to a later, synchronous load
+                    free_ext = free_save;
+                    cache_off = off_save;
+                    cache_used = used_save;
+                    resident_n = res_save;
+                    loads.clear();
+                    return false;
+                }
+                // fragmented: keep only `want`, packed from offset 0 (they fit)
                 for (uint32_t v = 0; v < nlist; ++v)
                     if (cache_off[v] != kAbsent) cache_free(v);
                 miss = want;
                 std::sort(miss.begin(), miss.end(), by_size);
+                loads.clear();
                 m = (size_t)-1;
                 continue;
             }
             cache_off[l] = off;
             ++resident_n;
-            const uint64_t nb = list_blocks(l);
-            ++cache_loads;
-            cache_bytes_in += nb * block_bytes(dp);
-            if (file_home()) {
-                load_list_from_file(l, off, s);
-                continue;
-            }
-            HIPCHECK(hipMemcpyAsync(cache.p + off * d4 * 64, arena.p + block_off[l] * d4 * 64, nb * d4 * 64 * sizeof(float4),
-                                    hipMemcpyHostToDevice, s));
-            HIPCHECK(hipMemcpyAsync(cache_ids.p + off * 64, arena_ids.p + block_off[l] * 64, nb * 64 * 8,
-                                    hipMemcpyHostToDevice, s));
+            loads.push_back({l, off});
         }
+        cache_evictions += evicted;
+        cache_loads += loads.size();
+        for (auto& ld : loads) cache_bytes_in += list_blocks(ld.first) * block_bytes(dp);
+        return true;
+    }
+
+    // Unique cacheable lists of a probe array.
+    std::vector<uint32_t> cacheable(const uint32_t* lists, size_t n, std::vector<uint8_t>& mark) {
+        std::vector<uint32_t> out;
+        for (size_t i = 0; i < n; ++i) {
+            const uint32_t l = lists[i];
+            if (l >= nlist || mark[l] || !owned[l] || count[l] == 0) continue;
+            mark[l] = 1;
+            out.push_back(l);
+        }
+        for (uint32_t l : out) mark[l] = 0;
+        return out;
+    }
+
+    // Make `lists` resident on stream s (warmup and single lists): LRU eviction.
+    // False if together they exceed the cache.
+    bool make_resident(const uint32_t* lists, size_t n, hipStream_t s) {
+        ++use_tick;
+        std::vector<uint8_t> mark(nlist, 0);
+        const std::vector<uint32_t> want = cacheable(lists, n, mark);
+        for (uint32_t l : want) last_use[l] = use_tick;
+        std::vector<uint8_t> protect(nlist, 0);
+        for (uint32_t l : want) protect[l] = 1;
+        bool miss = false;
+        for (uint32_t l : want) miss |= cache_off[l] == kAbsent;
+        if (miss) quiesce();  // searches on other streams may still read the lists evicted below
+        std::vector<std::pair<uint32_t, uint64_t>> loads;
+        if (!plan_loads(want, protect, [](uint32_t) { return uint64_t(0); }, true, loads)) return false;
+        if (loads.empty()) return true;
+        load_lists(loads, s);
         upload_scan_directory(s);
         return true;
     }
@@ -776,34 +844,107 @@ struct vdb_ivf {
         }
     }
 
-    // One list from the file into cache blocks [off, off + blocks): chunks of whole
-    // 64-row blocks, each read into one of two pinned buffers (the other one's copy
-    // is in flight), copied to HBM, padded to dp and interleaved into the block layout.
-    void load_list_from_file(uint32_t l, uint64_t off, hipStream_t s) {
-        const uint64_t n = count[l];
-        const uint64_t rows = std::max<uint64_t>(64, ((32ull << 20) / ((uint64_t)dim * 4)) / 64 * 64);
-        for (int i = 0; i < 2; ++i) {
-            if (!fstage_done[i]) HIPCHECK(hipEventCreateWithFlags(&fstage_done[i], hipEventDisableTiming));
-            fstage[i].host = istage[i].host = true;
-            fstage[i].ensure(rows * dim);
-            istage[i].ensure(rows);
+    // Copy planned lists into their cache blocks, ordered on stream s. Host-memory home:
+    // one DMA per list. File home: every list is cut into chunks of whole 64-row blocks;
+    // each chunk's ids and rows are read (io_uring, up to kStages chunks in flight) into
+    // a page-locked staging buffer, copied to HBM, padded to dp and interleaved into the
+    // cache's block layout; a buffer is refilled once its copies have landed.
+    void load_lists(const std::vector<std::pair<uint32_t, uint64_t>>& loads, hipStream_t s) {
+        if (!file_home()) {
+            for (auto& ld : loads) {
+                const uint32_t l = ld.first;
+                const uint64_t off = ld.second, nb = list_blocks(l);
+                HIPCHECK(hipMemcpyAsync(cache.p + off * d4 * 64, arena.p + block_off[l] * d4 * 64,
+                                        nb * d4 * 64 * sizeof(float4), hipMemcpyHostToDevice, s));
+                HIPCHECK(hipMemcpyAsync(cache_ids.p + off * 64, arena_ids.p + block_off[l] * 64, nb * 64 * 8,
+                                        hipMemcpyHostToDevice, s));
+            }
+            return;
         }
-        drows.ensure(rows * dim);
-        dpad.ensure(rows * dp);
-        const uint64_t ids_at = file_off[l], vec_at = file_off[l] + n * 8;
-        for (uint64_t r0 = 0, c = 0; r0 < n; r0 += rows, ++c) {
-            const int i = (int)(c & 1);
-            const uint64_t m = std::min(rows, n - r0);
-            HIPCHECK(hipEventSynchronize(fstage_done[i]));  // this buffer's previous copy has landed
-            pread_all(istage[i].p, m * 8, ids_at + r0 * 8);
-            pread_all(fstage[i].p, m * dim * 4, vec_at + r0 * dim * 4);
-            const uint64_t b = off + r0 / 64;
-            HIPCHECK(hipMemcpyAsync(cache_ids.p + b * 64, istage[i].p, m * 8, hipMemcpyHostToDevice, s));
-            HIPCHECK(hipMemcpyAsync(drows.p, fstage[i].p, m * dim * 4, hipMemcpyHostToDevice, s));
-            HIPCHECK(hipEventRecord(fstage_done[i], s));
-            vdbk::launch_pad_rows(drows.p, m, dim, dp, dpad.p, s);
-            vdbk::launch_interleave(dpad.p, m, dp, cache.p + b * d4 * 64, s);
-            HIPCHECK(hipGetLastError());
+        const uint64_t rows = std::max<uint64_t>(64, ((32ull << 20) / ((uint64_t)dim * 4)) / 64 * 64);
+        const size_t ids_cap = (rows * 8 + 8192 + 4095) / 4096 * 4096;
+        const size_t vec_cap = (rows * dim * 4 + 8192 + 4095) / 4096 * 4096;
+        if (!uring) uring.reset(new UringReader(64));
+        for (Stage& st : stages) {
+            if (!st.copied) HIPCHECK(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming));
+            st.buf.host = true;
+            st.buf.ensure(ids_cap + vec_cap);
+        }
+        // loads on the copy stream may overlap loads on a search stream: separate device staging
+        DevBuf<float>& rows_d = s == copy_stream ? drows_cs : drows;
+        DevBuf<float>& pad_d = s == copy_stream ? dpad_cs : dpad;
+        rows_d.ensure(rows * dim);
+        pad_d.ensure(rows * dp);
+        struct Chunk {
+            uint32_t l;
+            uint64_t r0, m, dst_block;
+        };
+        std::vector<Chunk> chunks;
+        for (auto& ld : loads)
+            for (uint64_t r0 = 0; r0 < count[ld.first]; r0 += rows)
+                chunks.push_back({ld.first, r0, std::min(rows, count[ld.first] - r0), ld.second + r0 / 64});
+        const bool direct = home_fd_direct >= 0;
+        // one read; with O_DIRECT the aligned superset of [off, off + len)
+        auto read_into = [&](int si, char* dst, uint64_t off, uint64_t len, int part) -> size_t {
+            const uint64_t tag = ((uint64_t)si << 1) | (uint64_t)part;
+            if (!direct) {
+                uring->read(home_fd, dst, (uint32_t)len, off, tag);
+                return 0;
+            }
+            const uint64_t a0 = off & ~4095ull, a1 = (off + len + 4095) & ~4095ull;
+            uring->read(home_fd_direct, dst, (uint32_t)(a1 - a0), a0, tag);
+            return (size_t)(off - a0);
+        };
+        size_t next = 0;
+        int reading = 0;
+        while (next < chunks.size() || reading > 0) {
+            for (int si = 0; si < kStages && next < chunks.size(); ++si) {
+                Stage& st = stages[si];
+                if (st.reads) continue;
+                if (st.copying) {
+                    const hipError_t q = hipEventQuery(st.copied);
+                    if (q == hipErrorNotReady) continue;
+                    HIPCHECK(q);
+                    st.copying = false;
+                }
+                const Chunk& c = chunks[next++];
+                const uint64_t base = file_off[c.l];
+                st.m = c.m;
+                st.dst_block = c.dst_block;
+                st.ids_delta = read_into(si, st.buf.p, base + c.r0 * 8, c.m * 8, 0);
+                st.vec_delta = read_into(si, st.buf.p + ids_cap, base + count[c.l] * 8 + c.r0 * dim * 4, c.m * dim * 4, 1);
+                st.reads = 2;
+                ++reading;
+                file_bytes_read += c.m * 8 + c.m * dim * 4;
+            }
+            if (reading == 0) {  // every buffer waits for its copies: wait for one
+                for (Stage& st : stages)
+                    if (st.copying) {
+                        HIPCHECK(hipEventSynchronize(st.copied));
+                        st.copying = false;
+                        break;
+                    }
+                continue;
+            }
+            for (const UringReader::Done& d : uring->wait(1)) {
+                Stage& st = stages[d.tag >> 1];
+                const bool vec = d.tag & 1;
+                const int64_t want = (int64_t)((vec ? st.vec_delta : st.ids_delta) + st.m * (vec ? (uint64_t)dim * 4 : 8));
+                require(d.result >= want, "short read from the list file" +
+                                              (d.result < 0 ? std::string(": ") + std::strerror((int)-d.result) : ""),
+                        VDB_ERR_STATE);
+                if (--st.reads) continue;
+                --reading;
+                HIPCHECK(hipMemcpyAsync(cache_ids.p + st.dst_block * 64, st.buf.p + st.ids_delta, st.m * 8,
+                                        hipMemcpyHostToDevice, s));
+                HIPCHECK(hipMemcpyAsync(rows_d.p, st.buf.p + ids_cap + st.vec_delta, st.m * dim * 4,
+                                        hipMemcpyHostToDevice, s));
+                HIPCHECK(hipEventRecord(st.copied, s));
+                st.copying = true;
+                vdbk::launch_pad_rows(rows_d.p, st.m, dim, dp, pad_d.p, s);
+                vdbk::launch_interleave(pad_d.p, st.m, dp, cache.p + st.dst_block * d4 * 64, s);
+                HIPCHECK(hipGetLastError());
+            }
         }
     }
 
@@ -814,7 +955,10 @@ struct vdb_ivf {
         const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
         require(fd >= 0, std::string("cannot open ") + path, VDB_ERR_STATE);
         if (home_fd >= 0) ::close(home_fd);
+        if (home_fd_direct >= 0) ::close(home_fd_direct);
         home_fd = fd;
+        // lists are read with O_DIRECT where the file system allows it (no page-cache copy)
+        home_fd_direct = ::open(path, O_RDONLY | O_CLOEXEC | O_DIRECT);
         char magic[8];
         uint32_t hdr[4];
         pread_all(magic, 8, 0);
@@ -822,6 +966,8 @@ struct vdb_ivf {
         if (std::memcmp(magic, "VDBIVF01", 8) != 0 || hdr[0] != dim || hdr[1] != nlist || (int)hdr[2] != metric) {
             ::close(home_fd);
             home_fd = -1;
+            if (home_fd_direct >= 0) ::close(home_fd_direct);
+            home_fd_direct = -1;
             throw VdbError(VDB_ERR_INVALID_ARGUMENT, "index file does not match this index's configuration");
         }
         std::vector<float> c((size_t)nlist * dim);
@@ -853,6 +999,7 @@ struct vdb_ivf {
     // Turn the tier on (bytes > 0: HBM cache of that many bytes, arena moved to host
     // memory) or off (arena back in HBM).
     void set_list_cache(uint64_t bytes) {
+        require(bytes == 0 || !comm, "the list-cache tier cannot be combined with a communicator", VDB_ERR_STATE);
         quiesce();
         const uint64_t nb = bytes / block_bytes(dp);
         require(bytes == 0 || nb > 0, "list_cache_bytes is below one block of 64 vectors");
@@ -1184,19 +1331,10 @@ struct vdb_ivf {
     }
 
     // ---- search: ivf_flat_index.cpp:205-256, one batch of B queries ----
-    // Returns false (nothing merged, caller retries with fewer queries) when the tier's
-    // cache cannot hold every list the batch probes.
-    bool run_batch(SearchSlot& w, const float* d_q, uint32_t B, uint32_t P, uint32_t k, float* out_d_,
-                   uint64_t* out_i_, hipStream_t s, const uint32_t* req_start, uint32_t b0) {
-        const int regs_k = vdbk::topk_regs(k);
+    // Coarse step (select_nprobe_lists, cpp:298-336): padded queries into w.qpad, the
+    // first min(nprobe, nlist) lists by (dist, list) into w.probes.
+    void coarse_batch(SearchSlot& w, const float* d_q, uint32_t B, uint32_t P, hipStream_t s) {
         const int regs_p = vdbk::topk_regs(P);
-        const uint32_t group = (uint32_t)vdbk::scan_group(regs_k);
-        const uint32_t BP = B * P;
-        const uint64_t max_items = (uint64_t)B * nseg_prefix[P];
-        require(max_items < (1ull << 32), "batch too large", VDB_ERR_UNSUPPORTED);
-        EventSet* ev = prof ? &next_events() : nullptr;
-        if (ev) HIPCHECK(hipEventRecord(ev->begin, s));
-
         vdbk::launch_pad_rows(d_q, B, dim, dp, w.qpad.p, s);
         if (coarse_mode == 1 && metric != 2 && vdbk::rerank_rows(dp, regs_p) > 0) {
             vdbk::launch_coarse_mfma(metric, cent_rm.p, nlist, dp, w.qpad.p, B, w.cd.p, w.cdelta.p, s);
@@ -1206,15 +1344,18 @@ struct vdb_ivf {
             vdbk::launch_coarse(metric, cent_il.p, nlist, d4, w.qpad.p, B, w.cd.p, s);
             vdbk::launch_select(regs_p, w.cd.p, nlist, B, P, w.probes.p, s);
         }
-        if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
-        if (tiered() && resident_n < storable_n) {  // (everything cached: no host round trip)
-            HIPCHECK(hipMemcpyAsync(probe_stage.ensure(BP), w.probes.p, (size_t)BP * 4, hipMemcpyDeviceToHost, s));
-            HIPCHECK(hipStreamSynchronize(s));
-            if (!make_resident(probe_stage.p, BP, s)) {
-                if (ev) --events_used;
-                return false;
-            }
-        }
+    }
+
+    // Probe inversion, fine scan (search_list_cpu, cpp:339-384) and merges
+    // (merge_results, cpp:474-518) of a batch whose padded queries are in w.qpad and
+    // probes in w.probes.
+    void scan_batch(SearchSlot& w, uint32_t B, uint32_t P, uint32_t k, float* out_d_, uint64_t* out_i_, hipStream_t s,
+                    const uint32_t* req_start, uint32_t b0, EventSet* ev) {
+        const int regs_k = vdbk::topk_regs(k);
+        const uint32_t group = (uint32_t)vdbk::scan_group(regs_k);
+        const uint32_t BP = B * P;
+        const uint64_t max_items = (uint64_t)B * nseg_prefix[P];
+        require(max_items < (1ull << 32), "batch too large", VDB_ERR_UNSUPPORTED);
         // (tier: lists and directory entries another stream loaded must have landed)
         if (tiered() && tier_ev_used) HIPCHECK(hipStreamWaitEvent(s, tier_ev, 0));
         const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
@@ -1259,7 +1400,148 @@ struct vdb_ivf {
                                w.carry_i.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->end, s));
         HIPCHECK(hipGetLastError());
+    }
+
+    // One batch, every list HBM-resident (or the tier with every stored list cached).
+    bool run_batch(SearchSlot& w, const float* d_q, uint32_t B, uint32_t P, uint32_t k, float* out_d_,
+                   uint64_t* out_i_, hipStream_t s, const uint32_t* req_start, uint32_t b0) {
+        EventSet* ev = prof ? &next_events() : nullptr;
+        if (ev) HIPCHECK(hipEventRecord(ev->begin, s));
+        coarse_batch(w, d_q, B, P, s);
+        if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
+        scan_batch(w, B, P, k, out_d_, out_i_, s, req_start, b0, ev);
         return true;
+    }
+
+    // ---- list-cache tier search (cache smaller than the index) ----
+    // The probes of the whole call are computed first (coarse steps only), so loads and
+    // evictions are planned against the call's known future:
+    //  * the call is cut into sub-batches of at most `batch` queries whose probed lists
+    //    fill at most half the cache (so the next sub-batch's lists load beside them; a
+    //    query needing more gets a sub-batch of its own); results never depend on batch
+    //    boundaries;
+    //  * while sub-batch i scans, the lists of sub-batch i+1 are read from the home
+    //    (file: io_uring into page-locked staging; host memory: DMA) and copied into free
+    //    cache space on copy_stream; sub-batch i+1 waits for them by event;
+    //  * a victim is the cached list whose next use in the call is furthest away (not
+    //    used again: first), then the least recently used; sub-batch i's lists (and i+1's)
+    //    are never evicted while i runs.
+    void search_tiered(SearchSlot& w, const float* d_q, uint32_t n, uint32_t P, uint32_t k, float* d_dist,
+                       uint64_t* d_ids, hipStream_t s, const uint32_t* req_start) {
+        if (tier_call_used) HIPCHECK(hipEventSynchronize(tier_call_ev));  // probe_stage is reused
+        const uint32_t bmax = batch_cap(P);
+        // 1. probes of the whole call
+        probe_stage.host = true;
+        uint32_t* hp = probe_stage.ensure((size_t)n * P);
+        for (uint32_t b0 = 0; b0 < n; b0 += bmax) {
+            const uint32_t B = std::min(bmax, n - b0);
+            coarse_batch(w, d_q + (size_t)b0 * dim, B, P, s);
+            HIPCHECK(hipMemcpyAsync(hp + (size_t)b0 * P, w.probes.p, (size_t)B * P * 4, hipMemcpyDeviceToHost, s));
+        }
+        HIPCHECK(hipStreamSynchronize(s));
+        // 2. sub-batches whose lists fit the cache
+        std::vector<uint8_t> qmark(nlist, 0), umark(nlist, 0);  // (a query's lists, the sub-batch's lists)
+        std::vector<uint32_t> sb_begin;
+        std::vector<std::vector<uint32_t>> U;
+        uint64_t blocks = 0;
+        for (uint32_t q = 0; q < n; ++q) {
+            const std::vector<uint32_t> ql = cacheable(hp + (size_t)q * P, P, qmark);
+            uint64_t qb = 0, add = 0;
+            for (uint32_t l : ql) {
+                qb += list_blocks(l);
+                if (!umark[l]) add += list_blocks(l);
+            }
+            require(qb <= cache_blocks, "list_cache_bytes cannot hold the lists one query probes", VDB_ERR_OUT_OF_MEMORY);
+            // half the cache per sub-batch: the next one's lists can load beside it
+            if (U.empty() || q - sb_begin.back() >= bmax || blocks + add > cache_blocks / 2) {
+                if (!U.empty())
+                    for (uint32_t l : U.back()) umark[l] = 0;
+                sb_begin.push_back(q);
+                U.emplace_back();
+                blocks = 0;
+            }
+            for (uint32_t l : ql)
+                if (!umark[l]) {
+                    umark[l] = 1;
+                    U.back().push_back(l);
+                    blocks += list_blocks(l);
+                }
+        }
+        const size_t nsb = U.size();
+        sb_begin.push_back(n);
+        // next-use ranks: for each list the sub-batches that use it, in order
+        std::vector<std::vector<uint32_t>> uses(nlist);
+        bool miss = false;
+        for (size_t b = 0; b < nsb; ++b)
+            for (uint32_t l : U[b]) {
+                uses[l].push_back((uint32_t)b);
+                miss |= cache_off[l] == kAbsent;
+            }
+        auto rank_after = [&](size_t cur) {
+            return [&, cur](uint32_t l) -> uint64_t {
+                const auto& u = uses[l];
+                auto it = std::upper_bound(u.begin(), u.end(), (uint32_t)cur);
+                return it == u.end() ? ~0ull : (uint64_t)*it;
+            };
+        };
+        if (miss) quiesce();  // searches on other streams may still read lists evicted below
+        if (!copy_stream) {
+            HIPCHECK(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+            for (auto& e : sb_done) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIPCHECK(hipEventCreateWithFlags(&load_ev, hipEventDisableTiming));
+            HIPCHECK(hipEventCreateWithFlags(&tier_call_ev, hipEventDisableTiming));
+        }
+        // 3. sub-batches in order, each next one's lists loaded while the current one scans
+        std::vector<uint8_t> protect(nlist, 0);
+        std::vector<std::pair<uint32_t, uint64_t>> loads;
+        bool prefetched = false;
+        for (size_t b = 0; b < nsb; ++b) {
+            const uint32_t b0 = sb_begin[b], B = sb_begin[b + 1] - b0;
+            if (prefetched) {
+                HIPCHECK(hipStreamWaitEvent(s, load_ev, 0));
+            } else {  // load on s itself, after the previous sub-batch in stream order
+                for (uint32_t l : U[b]) protect[l] = 1;
+                const bool ok = plan_loads(U[b], protect, rank_after(b), true, loads);
+                for (uint32_t l : U[b]) protect[l] = 0;
+                require(ok, "list_cache_bytes cannot hold the lists one sub-batch probes", VDB_ERR_OUT_OF_MEMORY);
+                if (!loads.empty()) {
+                    load_lists(loads, s);
+                    upload_scan_directory(s);
+                    ++tier_sync_loads;
+                }
+            }
+            ++use_tick;
+            for (uint32_t l : U[b]) last_use[l] = use_tick;
+            EventSet* ev = prof ? &next_events() : nullptr;
+            if (ev) HIPCHECK(hipEventRecord(ev->begin, s));
+            vdbk::launch_pad_rows(d_q + (size_t)b0 * dim, B, dim, dp, w.qpad.p, s);
+            HIPCHECK(hipMemcpyAsync(w.probes.p, hp + (size_t)b0 * P, (size_t)B * P * 4, hipMemcpyHostToDevice, s));
+            if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
+            scan_batch(w, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s, req_start, b0, ev);
+            HIPCHECK(hipEventRecord(sb_done[b & 1], s));
+            ++tier_subbatches;
+            prefetched = false;
+            if (b + 1 < nsb) {
+                for (uint32_t l : U[b]) protect[l] = 1;
+                for (uint32_t l : U[b + 1]) protect[l] = 1;
+                const bool ok = plan_loads(U[b + 1], protect, rank_after(b + 1), false, loads);
+                for (uint32_t l : U[b]) protect[l] = 0;
+                for (uint32_t l : U[b + 1]) protect[l] = 0;
+                if (ok) {
+                    // victims may still be read by sub-batch b - 1 (not by b: protected)
+                    if (b >= 1) HIPCHECK(hipStreamWaitEvent(copy_stream, sb_done[(b - 1) & 1], 0));
+                    if (!loads.empty()) {
+                        load_lists(loads, copy_stream);  // the host reads the file while b scans
+                        upload_scan_directory(copy_stream);
+                        ++tier_prefetches;
+                    }
+                    HIPCHECK(hipEventRecord(load_ev, copy_stream));
+                    prefetched = true;
+                }
+            }
+        }
+        HIPCHECK(hipEventRecord(tier_call_ev, s));
+        tier_call_used = true;
     }
 
     uint32_t batch_cap(uint32_t P) const {
@@ -1345,17 +1627,17 @@ struct vdb_ivf {
             require(comm_world == world && comm_rank == rank,
                     "the attached communicator's (rank, world) differs from the handle's shard", VDB_ERR_STATE);
         SearchSlot& w = begin_call(n, P, k, s, xchg ? comm_world : 0);
+        if (tiered() && resident_n < storable_n) {  // (every stored list cached: the plain path)
+            require(!xchg, "the list-cache tier cannot be combined with a communicator", VDB_ERR_STATE);
+            search_tiered(w, d_q, n, P, k, d_dist, d_ids, s, req_start);
+            end_call(w, s);
+            return;
+        }
         const uint32_t bmax = batch_cap(P);
         for (uint32_t b0 = 0, B = std::min(bmax, n); b0 < n; b0 += B, B = std::min(B, n - b0)) {
             float* od = xchg ? rec_dist(w) : d_dist + (size_t)b0 * k;
             uint64_t* oi = xchg ? rec_ids(w, B, k) : d_ids + (size_t)b0 * k;
-            // (list-cache tier: a batch whose probed lists overflow the cache is halved;
-            // never with a communicator, whose ranks must agree on every batch)
-            while (!run_batch(w, d_q + (size_t)b0 * dim, B, P, k, od, oi, s, req_start, b0)) {
-                require(B > 1, "list_cache_bytes cannot hold the lists one query probes", VDB_ERR_OUT_OF_MEMORY);
-                B = (B + 1) / 2;
-                if (xchg) oi = rec_ids(w, B, k);
-            }
+            run_batch(w, d_q + (size_t)b0 * dim, B, P, k, od, oi, s, req_start, b0);
             if (xchg) {
                 NCCLCHECK(ncclAllGather(w.xrec.p, w.xgat.p, vdb_rank_record_bytes(B, k), ncclUint8, comm, s));
                 merge_gathered(w, comm_world, B, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s);

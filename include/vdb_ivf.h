@@ -191,6 +191,11 @@ typedef struct vdb_ivf_cache_stats_t {
     uint64_t evictions;       /* lists evicted to make room (not counting vdb_ivf_evict) */
     uint64_t bytes_loaded;
     uint64_t file_bytes_read; /* lists served from a file: bytes read from it */
+    uint64_t subbatches;      /* sub-batches searched through the tier (cut to fit the cache) */
+    uint64_t prefetches;      /* sub-batches whose lists were loaded while the previous one scanned */
+    uint64_t sync_loads;      /* sub-batches whose lists were loaded before their own scan */
+    int32_t io_uring;         /* 1: the file home is read through io_uring (0: pread fallback) */
+    int32_t o_direct;         /* 1: the file home is read with O_DIRECT */
 } vdb_ivf_cache_stats_t;
 int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
 /* The tier's home on disk (ListPrefetcher::register_list_file / prefetch_lists,

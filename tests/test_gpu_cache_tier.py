@@ -159,3 +159,58 @@ def test_lists_served_from_file(tmp_path, dim):
         h.add(X[:10], ids[:10])
     h.warmup_lists(list(range(NLIST)))       # LRU keeps what fits; results unchanged
     assert_same(*h.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
+
+
+def test_tier_pipeline_file_home_next_use_and_prefetch(tmp_path):
+    """A call of many queries against a file home with a cache that holds a few queries'
+    lists: the call is cut into sub-batches that fit, each next sub-batch's lists are read
+    (io_uring, O_DIRECT where allowed) while the current one scans, and evictions follow
+    the call's known next uses. Results bit-identical to the oracle, stale slots included."""
+    X, Q, ids, o, blocks, need = fixture()
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST))
+    g.centroids = o.centroids
+    g.add(X, ids)
+    path = str(tmp_path / "tier.vdb")
+    g.save(path)
+    del g
+    h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST))
+    h.set_option("list_cache_bytes", (3 * need + 8) * BLOCK_BYTES)   # room for ~3 queries' lists at once
+    h.open_lists(path)
+    Dr, Ir = o.search(Q, NPROBE, K)
+    for batch in (64, 5):
+        h.set_batch(batch)
+        assert_same(*h.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
+    st = h.cache_stats()
+    assert st["subbatches"] > 2 * len(Q) // 64 and st["prefetches"] > 0, st
+    assert st["file_bytes_read"] > 0 and st["loads"] > 0
+    assert st["io_uring"] in (0, 1) and st["o_direct"] in (0, 1)
+    # a second pass over the same calls: next-use eviction never needs more reads than
+    # one full load of every list per sub-batch
+    before = st["file_bytes_read"]
+    h.set_batch(64)
+    assert_same(*h.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
+    assert h.cache_stats()["file_bytes_read"] - before <= int(blocks.sum()) * 64 * (D * 4 + 8) * len(Q)
+
+
+def test_tier_concurrent_streams_under_eviction():
+    """Three searches in flight on three streams while the cache evicts and reloads
+    (host-memory home): every stream's results equal the oracle's (a search on
+    another stream must wait for lists and directory entries still being copied)."""
+    import torch
+    X, Q, ids, o, blocks, need = fixture()
+    g = make(o, X, ids, (2 * need + 8) * BLOCK_BYTES, False)
+    dev = torch.device("cuda", 0)
+    q = torch.from_numpy(Q).to(dev)
+    n = len(Q) // 3
+    od = torch.empty((3 * n, K), dtype=torch.float32, device=dev)
+    oi = torch.empty((3 * n, K), dtype=torch.int64, device=dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    for rep in range(3):
+        for j, s in enumerate(streams):
+            g.search_device(q[j * n:].data_ptr(), n, NPROBE, K, od[j * n:].data_ptr(), oi[j * n:].data_ptr(),
+                            s.cuda_stream)
+        torch.cuda.synchronize()
+        for j in range(3):
+            assert_same(od[j * n:(j + 1) * n].cpu().numpy(), oi[j * n:(j + 1) * n].cpu().numpy().view(np.uint64),
+                        *o.search(Q[j * n:(j + 1) * n], NPROBE, K))
+    assert g.cache_stats()["evictions"] > 0
