@@ -288,6 +288,63 @@ def host_api_leg(idx, args, queries, out_d, out_i):
             "pcie_inclusive": True, "parity_with_device_path": same[0]}
 
 
+def tier_leg(vdb, idx, args, device, queries):
+    """configs[4]'s mechanism on one GPU: the index is written to a file larger than the
+    HBM list cache (vdb_ivf_save), a fresh handle serves it from that file through the
+    list-cache tier (vdb_ivf_open_lists: io_uring reads, sub-batches cut to the cache,
+    next sub-batch's lists loaded while the current one scans, next-use eviction), and
+    calls of --tier-call queries are timed. Bytes read per batch of --batch queries are
+    reported against the batch's algorithmic list bytes (the floor without a cache)."""
+    import tempfile
+    d = args.tier_dir or tempfile.gettempdir()
+    path = os.path.join(d, f"vdb_tier_{os.getpid()}.ivf")
+    t0 = time.perf_counter()
+    idx.save(path)
+    t_save = time.perf_counter() - t0
+    file_bytes = os.path.getsize(path)
+    cfg = vdb.IVFFlatIndex.Config(args.dim, args.nlist, vdb.Metric.L2, device=device.index)
+    idx.close()  # the HBM-resident index is gone: only the tier's cache holds lists now
+    torch.cuda.empty_cache()
+    try:
+        h = vdb.IVFFlatIndex(cfg)
+        h.set_option("list_cache_bytes", int(args.tier_cache_gib * (1 << 30)))
+        h.set_option("batch", args.batch)
+        h.open_lists(path)
+        call = args.tier_call
+        st = torch.cuda.current_stream()
+        od = torch.empty((call, args.k), dtype=torch.float32, device=device)
+        oi = torch.empty((call, args.k), dtype=torch.int64, device=device)
+        calls = min(args.tier_calls, len(queries) // call)
+        h.search_device(queries.data_ptr(), call, args.nprobe, args.k, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()  # (warm-up call: code objects, staging, the cache's first contents)
+        s0 = h.cache_stats()
+        h.profile_enable(True)
+        h.profile_reset()
+        t0 = time.perf_counter()
+        for j in range(1, calls):
+            h.search_device(queries[j * call:].data_ptr(), call, args.nprobe, args.k, od.data_ptr(), oi.data_ptr(),
+                            st.cuda_stream)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        prof = h.profile_read()
+        s1 = h.cache_stats()
+        nq = (calls - 1) * call
+        batches = nq / args.batch
+        alg = prof["scan_bytes"] / batches  # the lists each batch of --batch queries probes, read once
+        read = (s1["file_bytes_read"] - s0["file_bytes_read"]) / batches
+        return {"value": round(nq / el, 1), "unit": "queries/s", "calls": calls - 1, "queries_per_call": call,
+                "file": path, "file_gb": round(file_bytes / 1e9, 2), "save_s": round(t_save, 1),
+                "cache_gib": args.tier_cache_gib, "cache_fraction_of_file": round(args.tier_cache_gib * (1 << 30) / file_bytes, 3),
+                "file_bytes_read_per_batch": int(read), "algorithmic_bytes_per_batch": int(alg),
+                "read_over_algorithmic": round(read / alg, 3) if alg else None,
+                "file_read_gbps": round((s1["file_bytes_read"] - s0["file_bytes_read"]) / el / 1e9, 2),
+                "subbatches": s1["subbatches"] - s0["subbatches"], "prefetches": s1["prefetches"] - s0["prefetches"],
+                "sync_loads": s1["sync_loads"] - s0["sync_loads"], "io_uring": s1["io_uring"], "o_direct": s1["o_direct"],
+                "batch": args.batch}
+    finally:
+        os.unlink(path)
+
+
 def shard_parity(vdb, idx, args, queries_host, rank, world):
     """Parity of one shard at full size: the oracle's shard search (oracle_search_shard:
     owned probed lists scanned, the others kept as counts for the empty-list rule,
@@ -383,6 +440,11 @@ def main():
                     help="components per super-cluster (0 = nprobe): a query's nprobe nearest lists are its siblings")
     ap.add_argument("--mix-spread", type=float, default=0.35, help="component centers around their super-cluster")
     ap.add_argument("--mix-sigma", type=float, default=0.1, help="points around their component center")
+    ap.add_argument("--tier-cache-gib", type=float, default=0.0,
+                    help="> 0: also serve the index from a file through the list-cache tier with this HBM cache")
+    ap.add_argument("--tier-call", type=int, default=512, help="queries per search call in the tier leg")
+    ap.add_argument("--tier-calls", type=int, default=8)
+    ap.add_argument("--tier-dir", default="", help="directory for the tier leg's index file (default: TMPDIR)")
     ap.add_argument("--host-api", action="store_true",
                     help="also time the host API (vdb_ivf_search) from --host-threads caller threads")
     ap.add_argument("--host-threads", type=int, default=8)
@@ -644,6 +706,11 @@ def run(vdb, args, device, rank, world):
     if world == 1 and args.emulate_shard > 1 and args.shard_check > 0:
         qh = queries[: args.shard_check].cpu().numpy()
         result["shard_parity"] = shard_parity(vdb, idx, args, qh, 0, args.emulate_shard)
+    if args.tier_cache_gib > 0 and world == 1:  # (last: it releases the HBM-resident index)
+        tq = torch.empty((args.tier_call * args.tier_calls, args.dim), dtype=torch.float32, device=device)
+        fill_rows(vdb, args, tq, 1 << 40, tq.shape[0], 12346, torch.cuda.current_stream().cuda_stream)
+        result["tier"] = tier_leg(vdb, idx, args, device, tq)
+        idx = None
     if rank == 0:
         print(json.dumps(result), flush=True)
 
