@@ -1137,6 +1137,8 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
             if (g < np && __ballot(valid && dist <= th[g])) pend |= 1u << g;
         }
         if (a.diag & 1) pend = 0;  // DIAGNOSTIC: no top-k maintenance (results invalid)
+        if ((a.diag & 4) && j == 0) pend = 0;  // DIAGNOSTIC: no insertion on a segment's first block
+        if ((a.diag & 8) && j != 0) pend = 0;  // DIAGNOSTIC: insertions on the first block only
         if (pend) {
             const uint64_t vid = valid ? id : kNoId;
             do {

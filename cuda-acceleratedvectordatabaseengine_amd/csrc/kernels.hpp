@@ -96,7 +96,8 @@ struct ScanArgs {
     uint32_t wide_stride;  // wide-item dispatch stride (prime; 0/1 = plan order)
     uint32_t* work;        // [2] item queues (narrow, wide), reset by the plan kernel
     uint32_t seg_blocks;   // 64-vector blocks per list segment (one wave's unit of a scan item)
-    uint32_t diag;         // diagnostics only (0 in production): 1 skip top-k upkeep, 2 one query pair
+    uint32_t diag;         // diagnostics only (0 in production): 1 skip top-k upkeep, 2 one query pair,
+                           // 4 no insertion on a segment's first block, 8 on its later blocks
     uint32_t segs_item;    // segments per wide item (>= 4; the 4 waves take them dynamically)
     uint32_t fused;        // ivf_scan_wide also drains the narrow queue (R = 1); the last `fused`
                            // workgroups start on narrow items (0: narrow items on their own kernel)
