@@ -84,18 +84,56 @@ int guarded(F&& f) {
     }
 }
 
+// Stream-ordered device memory for the engine's long-lived buffers (list arena, HBM list
+// cache, search workspaces): one hipMemPool per device whose release threshold keeps freed
+// memory reserved for the process (288 GB of HBM3E: an add's relayout and a workspace's
+// growth reuse it without driver calls), allocated and freed on a per-device allocation
+// stream. hipFreeAsync never synchronises the device the way hipFree does; the engine only
+// releases a pooled buffer once no queued work can read it (stream synchronised, searches
+// quiesced, or the workspace slot's previous call done).
+struct DevicePool {
+    hipMemPool_t pool = nullptr;
+    hipStream_t stream = nullptr;
+};
+inline DevicePool& device_pool(int dev) {
+    static std::mutex mu;
+    static DevicePool pools[64];
+    std::lock_guard<std::mutex> g(mu);
+    require(dev >= 0 && dev < 64, "device ordinal out of range", VDB_ERR_INVALID_ARGUMENT);
+    DevicePool& dp = pools[dev];
+    if (!dp.pool) {
+        hipMemPoolProps props = {};
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        HIPCHECK(hipMemPoolCreate(&dp.pool, &props));
+        uint64_t keep = ~0ull;
+        HIPCHECK(hipMemPoolSetAttribute(dp.pool, hipMemPoolAttrReleaseThreshold, &keep));
+        HIPCHECK(hipStreamCreateWithFlags(&dp.stream, hipStreamNonBlocking));
+    }
+    return dp;
+}
+
 // Growable device buffer (capacity in elements).
 template <class T>
 struct DevBuf {
     T* p = nullptr;
     size_t cap = 0;
     bool host = false;  // page-locked host memory the device reads and writes directly
+    bool pooled = false;  // device memory from the device's stream-ordered pool
+    int dev = 0;          // (pooled) the device the memory belongs to
     DevBuf() = default;
+    explicit DevBuf(bool pool) : pooled(pool) {}
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() { release(); }
     void release() {
-        if (p) (void)(host ? hipHostFree(p) : hipFree(p));
+        if (p) {
+            if (host) (void)hipHostFree(p);
+            else if (pooled) (void)hipFreeAsync(p, device_pool(dev).stream);
+            else (void)hipFree(p);
+        }
         p = nullptr;
         cap = 0;
     }
@@ -103,10 +141,16 @@ struct DevBuf {
         if (n <= cap && p) return p;
         release();
         size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-        if (host)
+        if (host) {
             HIPCHECK(hipHostMalloc((void**)&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
-        else
+        } else if (pooled) {
+            HIPCHECK(hipGetDevice(&dev));
+            DevicePool& dp = device_pool(dev);
+            HIPCHECK(hipMallocFromPoolAsync((void**)&p, bytes, dp.pool, dp.stream));
+            HIPCHECK(hipStreamSynchronize(dp.stream));  // usable from any stream right away
+        } else {
             HIPCHECK(hipMalloc(&p, bytes));
+        }
         cap = std::max<size_t>(n, 1);
         return p;
     }
@@ -114,6 +158,8 @@ struct DevBuf {
         std::swap(p, o.p);
         std::swap(cap, o.cap);
         std::swap(host, o.host);
+        std::swap(pooled, o.pooled);
+        std::swap(dev, o.dev);
     }
 };
 
@@ -203,8 +249,8 @@ struct vdb_ivf {
     std::vector<uint8_t> owned;       // lists this handle scans
     std::vector<uint64_t> block_off;  // arena block offset per owned list
     uint64_t arena_blocks = 0;
-    DevBuf<float4> arena;
-    DevBuf<uint64_t> arena_ids;
+    DevBuf<float4> arena{true};
+    DevBuf<uint64_t> arena_ids{true};
     DevBuf<uint64_t> d_block_off;
     DevBuf<uint32_t> d_count_local, d_count_global, d_nseg;
     std::vector<uint64_t> nseg_prefix;  // sum of the j largest local segment counts
@@ -232,8 +278,8 @@ struct vdb_ivf {
     // through the same directory (d_block_off), so the kernels are unchanged.
     static constexpr uint64_t kAbsent = ~0ull;
     uint64_t cache_blocks = 0;  // capacity in 64-vector blocks (0: tier off, the arena is in HBM)
-    DevBuf<float4> cache;
-    DevBuf<uint64_t> cache_ids;
+    DevBuf<float4> cache{true};
+    DevBuf<uint64_t> cache_ids{true};
     std::vector<uint64_t> cache_off;        // per list: cache block offset or kAbsent
     std::vector<uint64_t> last_use;         // per list: batch tick of the last probe
     std::map<uint64_t, uint64_t> free_ext;  // free cache extents: block offset -> blocks
@@ -282,16 +328,17 @@ struct vdb_ivf {
     // batch's scan). A call takes the next slot; its stream first waits for the
     // slot's previous batch (slot.done), wherever that ran.
     struct SearchSlot {
-        DevBuf<float> qpad, cd, cdelta, part_d, slot_d, carry_d;
-        DevBuf<uint64_t> part_i, slot_i, carry_i;
-        DevBuf<uint32_t> probes, nseg_qp, pbqp, sorted_pair, pbs, counters, l1base, cand, thr;
-        DevBuf<uint2> l1_items;
-        DevBuf<float> l1_d;
-        DevBuf<uint64_t> l1_i;
-        DevBuf<vdbk::ScanItem> items, items_w;
-        DevBuf<uint8_t> xrec, xgat;  // multi-GPU: this rank's packed partials, the gathered records
-        DevBuf<float> gq;            // group member: the call's queries on this device
-        DevBuf<uint32_t> greq;       // group member: the call's request starts on this device
+        DevBuf<float> qpad{true}, cd{true}, cdelta{true}, part_d{true}, slot_d{true}, carry_d{true};
+        DevBuf<uint64_t> part_i{true}, slot_i{true}, carry_i{true};
+        DevBuf<uint32_t> probes{true}, nseg_qp{true}, pbqp{true}, sorted_pair{true}, pbs{true}, counters{true},
+            l1base{true}, cand{true}, thr{true};
+        DevBuf<uint2> l1_items{true};
+        DevBuf<float> l1_d{true};
+        DevBuf<uint64_t> l1_i{true};
+        DevBuf<vdbk::ScanItem> items{true}, items_w{true};
+        DevBuf<uint8_t> xrec{true}, xgat{true};  // multi-GPU: this rank's packed partials, the gathered records
+        DevBuf<float> gq{true};            // group member: the call's queries on this device
+        DevBuf<uint32_t> greq{true};       // group member: the call's request starts on this device
         hipStream_t side = nullptr;  // narrow-item scan, concurrent with the wide items
         hipStream_t gstream = nullptr;  // group member: the stream this slot's searches run on
         hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
@@ -342,6 +389,10 @@ struct vdb_ivf {
         stop_coalescer();
         members.clear();  // each member waits for and frees its own device work
         (void)hipSetDevice(device);
+        try {
+            quiesce();  // pooled buffers are freed stream-ordered: no search may still read them
+        } catch (...) {
+        }
         if (stream) (void)hipStreamSynchronize(stream);
         for (auto& sl : slots)
             if (sl.gstream) (void)hipStreamSynchronize(sl.gstream);
@@ -626,8 +677,8 @@ struct vdb_ivf {
                 old_off[l] = block_off[l];
             }
         }
-        DevBuf<float4> na;
-        DevBuf<uint64_t> ni;
+        DevBuf<float4> na{!host_arena};
+        DevBuf<uint64_t> ni{!host_arena};
         na.host = ni.host = host_arena;
         // one slack block past the last list: the scan prefetches one chunk and one
         // block of ids beyond the segment it streams
