@@ -341,6 +341,7 @@ struct vdb_ivf {
         DevBuf<uint32_t> greq{true};       // group member: the call's request starts on this device
         hipStream_t side = nullptr;  // narrow-item scan, concurrent with the wide items
         hipStream_t gstream = nullptr;  // group member: the stream this slot's searches run on
+        hipEvent_t x_ready = nullptr, x_done = nullptr;  // fences around this slot's collectives
         hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
         bool used = false;
     };
@@ -357,6 +358,30 @@ struct vdb_ivf {
     ncclComm_t comm = nullptr;
     bool comm_owned = false;
     uint32_t comm_rank = 0, comm_world = 1;
+    // Every collective of the communicator runs on this one stream, fenced by events
+    // against the search stream that produced / consumes its buffers: with several
+    // batches in flight on several streams, every rank then executes its collectives in
+    // the same (issue) order whatever the library does across streams.
+    hipStream_t comm_stream = nullptr;
+
+    // Order a collective on comm_stream after the work queued on s (returns comm_stream).
+    void make_comm_stream() {  // with the communicator (the device must be current)
+        if (!comm_stream) HIPCHECK(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
+    }
+    hipStream_t comm_enter(SearchSlot& w, hipStream_t s) {
+        if (!w.x_ready) {
+            HIPCHECK(hipEventCreateWithFlags(&w.x_ready, hipEventDisableTiming));
+            HIPCHECK(hipEventCreateWithFlags(&w.x_done, hipEventDisableTiming));
+        }
+        HIPCHECK(hipEventRecord(w.x_ready, s));
+        HIPCHECK(hipStreamWaitEvent(comm_stream, w.x_ready, 0));
+        return comm_stream;
+    }
+    // ... and the work queued on s next after it.
+    void comm_leave(SearchSlot& w, hipStream_t s) {
+        HIPCHECK(hipEventRecord(w.x_done, comm_stream));
+        HIPCHECK(hipStreamWaitEvent(s, w.x_done, 0));
+    }
     // Group handle: members[m] holds the lists owner[l] == m places on its device; the
     // group itself holds only the host-API staging on members[0]'s device.
     std::vector<std::unique_ptr<vdb_ivf>> members;
@@ -422,7 +447,10 @@ struct vdb_ivf {
             if (sl.done) (void)hipEventDestroy(sl.done);
             if (sl.side) (void)hipStreamDestroy(sl.side);
             if (sl.gstream) (void)hipStreamDestroy(sl.gstream);
+            if (sl.x_ready) (void)hipEventDestroy(sl.x_ready);
+            if (sl.x_done) (void)hipEventDestroy(sl.x_done);
         }
+        if (comm_stream) (void)hipStreamDestroy(comm_stream);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -1690,7 +1718,9 @@ struct vdb_ivf {
             uint64_t* oi = xchg ? rec_ids(w, B, k) : d_ids + (size_t)b0 * k;
             run_batch(w, d_q + (size_t)b0 * dim, B, P, k, od, oi, s, req_start, b0);
             if (xchg) {
-                NCCLCHECK(ncclAllGather(w.xrec.p, w.xgat.p, vdb_rank_record_bytes(B, k), ncclUint8, comm, s));
+                const hipStream_t cs = comm_enter(w, s);
+                NCCLCHECK(ncclAllGather(w.xrec.p, w.xgat.p, vdb_rank_record_bytes(B, k), ncclUint8, comm, cs));
+                comm_leave(w, s);
                 merge_gathered(w, comm_world, B, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s);
             }
         }

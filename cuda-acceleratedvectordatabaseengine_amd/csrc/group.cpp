@@ -288,13 +288,22 @@ void vdb_ivf::group_search_device(const float* d_q, uint32_t n, uint32_t P, uint
     // the queries (and request starts) onto every member
     if (M > 1) {
         if (group_rccl) {
+            std::vector<hipStream_t> cs(M);
+            for (uint32_t m = 0; m < M; ++m) {
+                members[m]->set_device();
+                cs[m] = members[m]->comm_enter(*w[m], ms[m]);
+            }
             NCCLCHECK(ncclGroupStart());
             for (uint32_t m = 0; m < M; ++m) {
-                NCCLCHECK(ncclBroadcast(d_q, (void*)qm[m], (size_t)n * dim, ncclFloat32, 0, members[m]->comm, ms[m]));
+                NCCLCHECK(ncclBroadcast(d_q, (void*)qm[m], (size_t)n * dim, ncclFloat32, 0, members[m]->comm, cs[m]));
                 if (req_start)
-                    NCCLCHECK(ncclBroadcast(req_start, (void*)rm[m], n, ncclUint32, 0, members[m]->comm, ms[m]));
+                    NCCLCHECK(ncclBroadcast(req_start, (void*)rm[m], n, ncclUint32, 0, members[m]->comm, cs[m]));
             }
             NCCLCHECK(ncclGroupEnd());
+            for (uint32_t m = 0; m < M; ++m) {
+                members[m]->set_device();
+                members[m]->comm_leave(*w[m], ms[m]);
+            }
         } else {  // members sharing one device (a rehearsal): plain device copies
             for (uint32_t m = 1; m < M; ++m) {
                 members[m]->set_device();
@@ -316,10 +325,19 @@ void vdb_ivf::group_search_device(const float* d_q, uint32_t n, uint32_t P, uint
         }
         const uint64_t rb = vdb_rank_record_bytes(B, k);
         if (group_rccl) {
+            std::vector<hipStream_t> cs(M);
+            for (uint32_t m = 0; m < M; ++m) {
+                members[m]->set_device();
+                cs[m] = members[m]->comm_enter(*w[m], ms[m]);
+            }
             NCCLCHECK(ncclGroupStart());
             for (uint32_t m = 0; m < M; ++m)
-                NCCLCHECK(ncclAllGather(w[m]->xrec.p, w[m]->xgat.p, rb, ncclUint8, members[m]->comm, ms[m]));
+                NCCLCHECK(ncclAllGather(w[m]->xrec.p, w[m]->xgat.p, rb, ncclUint8, members[m]->comm, cs[m]));
             NCCLCHECK(ncclGroupEnd());
+            for (uint32_t m = 0; m < M; ++m) {
+                members[m]->set_device();
+                members[m]->comm_leave(*w[m], ms[m]);
+            }
         } else {
             for (uint32_t m = 1; m < M; ++m) {
                 members[m]->set_device();
@@ -390,6 +408,8 @@ int vdb_ivf_create_group(const vdb_ivf_config* cfg, const int* devices, uint32_t
                 g->members[m]->comm_owned = true;
                 g->members[m]->comm_rank = m;
                 g->members[m]->comm_world = ndev;
+                g->members[m]->set_device();
+                g->members[m]->make_comm_stream();
             }
         }
         *out = g.release();
@@ -436,6 +456,7 @@ int vdb_ivf_attach_comm(vdb_ivf* h, const void* id, uint32_t rank, uint32_t worl
         h->comm_owned = true;
         h->comm_rank = rank;
         h->comm_world = world;
+        h->make_comm_stream();
     });
 }
 
