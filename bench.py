@@ -687,6 +687,9 @@ def run(vdb, args, device, rank, world):
             "search_ms_per_batch": round(prof["total_ms"] / launches, 4),
             "distinct_lists_per_batch": round(prof["distinct_lists"] / max(prof["batches"], 1), 1),
             "distances_per_batch": int(prof["pair_vectors"] / max(prof["batches"], 1)),
+            **({"exact_reranks_per_batch": int(prof["exact_reranks"] / max(prof["batches"], 1)),
+                "bounded_blocks_per_batch": int(prof["bounded_blocks"] / max(prof["batches"], 1))}
+               if prof.get("bounded_blocks") else {}),
         },
         "build": build_info,
         **({"list_cache": idx.cache_stats()} if any(o.startswith("list_cache_bytes=") for o in args.opt) else {}),

@@ -549,6 +549,9 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "wide_group") {
             require(value == 16 || value == 32, "wide_group is 16 or 32");
             h->wide_group = (uint32_t)value;
+        } else if (n == "scan_mfma_min") {
+            require(value >= 0 && value <= 16, "scan_mfma_min is 0 (never) .. 16");
+            h->scan_mfma_min = (uint32_t)value;
         } else if (n == "fused_scan") {
             h->fused_scan = value != 0;
         } else if (n == "narrow_blocks") {
@@ -676,6 +679,8 @@ int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
         p.batches = st[3];
         p.scan_bytes = st[1] * (uint64_t)h->dim * 4;
         p.pair_vectors = st[4];
+        p.exact_reranks = st[5];
+        p.bounded_blocks = st[6];
         *out = p;
         hh->set_device();
     });

@@ -263,7 +263,13 @@ struct vdb_ivf {
     uint32_t wide_stride = 1;  // wide-item dispatch permutation (1 = plan order; measured best)
     uint32_t seg_blocks = 8;  // current segment size (blocks of 64 vectors; upload_directory sets it)
     uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)
-    uint32_t diag = 0;                          // scan diagnostics (results invalid when set)
+    uint32_t diag = 0;                          // scan diagnostics (results invalid when set, but 16)
+    // wide items of at least this many queries are bounded on the matrix cores and
+    // re-ranked exactly (ivf_scan_bounded); 0 = never. Off by default: on the bench
+    // workloads the exact re-ranks (per-list top-k insertions, ~5% of pairs, each a
+    // gathered re-read of an evicted vector) cost more than the VALU it saves
+    // (DESIGN.md "Bounded scan: measured and rejected as default").
+    uint32_t scan_mfma_min = 0;
     uint32_t segs_item_opt = 0;   // segments per wide item (0: one per wave, taken dynamically)
     uint32_t wide_group = 16;     // queries per wide item at most: 16 (4-wave workgroups) or 32 (8-wave)
     bool fused_scan = true;       // narrow items inside the wide scan's grid (option fused_scan; +2-3 %)
@@ -1443,12 +1449,19 @@ struct vdb_ivf {
         const bool wide = regs_k == 1 && wide_scan && vdbk::scan_wide_fits(d4, k, waves);
         // segments per item: one per wave (more adds tail latency, no throughput)
         const uint32_t segs_item = segs_item_opt ? segs_item_opt : (uint32_t)waves;
+        // wide items of many queries: bounded on the matrix cores (L2 / IP, 16-query items)
+        const uint32_t mfma_min = wide && waves == 4 && metric != 2 && !(diag & 2) && vdbk::scan_bounded_fits(d4, k)
+                                      ? scan_mfma_min : 0u;
         vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? (int)wide_group : 0, segs_item, w.items.p, w.items_w.p,
-                          w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, w.thr.p, s);
+                          w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, w.thr.p,
+                          mfma_min, s);
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
         vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
-                                wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item, 0, w.thr.p};
+                                wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item, 0, w.thr.p,
+                                mfma_min, (diag & 16) ? stats.p + 5 : nullptr};
+        // the bounded items first (the batch's most-probed lists), on the same stream
+        if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
         if (wide && fused_scan) {
             // one persistent grid takes both queues (no side stream, no fork/join)
             // (narrow_blocks counts 4-wave workgroups: as many waves start on the narrow queue)

@@ -696,7 +696,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
                                                         const uint32_t* __restrict__ nseg_local,
                                                         const uint32_t* __restrict__ count_local, uint32_t B,
                                                         uint32_t P, uint32_t NP, uint32_t gn, uint32_t wide_on,
-                                                        uint32_t segs_item,
+                                                        uint32_t segs_item, uint32_t mfma_min,
                                                         ScanItem* __restrict__ items_n, ScanItem* __restrict__ items_w,
                                                         uint32_t* __restrict__ counters,
                                                         uint32_t* __restrict__ sorted_pair,
@@ -844,7 +844,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         it.npairs = min(gn, m - gi * gn);
         items_n[x] = it;
     }
-    for (uint32_t x = tid; x < n_wide; x += blockDim.x) {
+    auto wide_item = [&](uint32_t x) {
         const uint32_t dl = find_owner(base_w, nd, x);
         const uint32_t off = x - base_w[dl];
         const uint32_t st = starts[dl], m = starts[dl + 1] - st;
@@ -857,15 +857,36 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         it.seg = quad;
         it.pair_start = st + p0;
         it.npairs = p1 - p0;
-        items_w[x] = it;
+        return it;
+    };
+    // Wide items of >= mfma_min queries go to the bounded scan kernel: items_w holds the
+    // exact ones first, then the bounded ones, each in list order (a stable partition
+    // over contiguous per-thread ranges).
+    const uint32_t wper = (n_wide + blockDim.x - 1) / blockDim.x;
+    const uint32_t w0 = min(n_wide, tid * wper), w1 = min(n_wide, w0 + wper);
+    uint32_t nb_local = 0;
+    if (mfma_min)
+        for (uint32_t x = w0; x < w1; ++x) nb_local += wide_item(x).npairs >= mfma_min ? 1u : 0u;
+    uint32_t n_bounded;
+    const uint32_t bb_base = plan_excl_scan(nb_local, sh, n_bounded);
+    const uint32_t n_exact = n_wide - n_bounded;
+    {
+        uint32_t xb = n_exact + bb_base, xe = w0 - bb_base;
+        for (uint32_t x = w0; x < w1; ++x) {
+            const ScanItem it = wide_item(x);
+            if (mfma_min && it.npairs >= mfma_min) items_w[xb++] = it;
+            else items_w[xe++] = it;
+        }
     }
     if (tid == 0) {
         counters[0] = n_narrow;
         counters[1] = nparts;
         counters[2] = nl1;
-        counters[3] = n_wide;
-        counters[4] = 0;  // work queues of the persistent scan kernels (narrow waves, wide workgroups)
-        counters[5] = 0;
+        counters[3] = n_exact;
+        counters[4] = 0;  // work queues of the persistent scan kernels (narrow waves, wide and
+        counters[5] = 0;  // bounded workgroups)
+        counters[6] = 0;
+        counters[7] = n_bounded;  // bounded items: items_w[n_exact, n_exact + n_bounded)
         atomicAdd(&stats[0], (unsigned long long)nd);
         atomicAdd(&stats[2], (unsigned long long)(n_narrow + n_wide));
         atomicAdd(&stats[3], 1ull);
@@ -1191,6 +1212,204 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
     }
 }
 
+// ============================================================================
+// Bounded wide wave (L2 / IP, items of >= a.mfma_min queries): the item semantics of
+// scan_wide_wave for up to 16 queries, with every (query, vector) distance first
+// BOUNDED on the matrix cores and computed exactly only where it can reach the top-k.
+//  * Stream: the segment's rows go through v_mfma_f32_16x16x1_4b_f32 (4 blocks of
+//    16 x 16 x 1): A = this lane's list vector (lane = vector, the arena's float4 in
+//    place), B = query (lane & 15) from the item's row-major staging [d4][16] float4.
+//    D lane l, reg r holds <q_(l&15), x_v> for v = 16 (r >> 2) + 4 (l >> 4) + (r & 3)
+//    (measured: tools/mfma_probe.hip). Vector and query norms ride along (VALU).
+//  * Bounds: approx = |q|^2 + |x|^2 - 2 <q, x> (L2) or -<q, x> (IP) is within
+//    delta = 4 (n + 4) u (|q| + |x|)^2 (L2; |q||x| for IP) of the reference's
+//    sequential fp32 distance — the coarse step's bound (ivf_coarse_mfma above).
+//  * Threshold per query: min(own k-th exact, the item's shared k-th, T_seg), where
+//    T_seg is the smallest block bound so far: per block, each of a query's 4 lanes
+//    takes the ceil(k/4)-th smallest upper bound of its 16 vectors and the block bound
+//    is the largest of the 4 — at least k vectors of the segment have exact distances
+//    <= it, so anything strictly above it is not in the segment's multiset top-k.
+//  * Candidates (lower bound not above the threshold; non-finite bounds always) are
+//    compacted into an LDS list and recomputed exactly in rounds of 64 (one lane per
+//    candidate, the reference's sequential sum over the re-read vector), then offered
+//    to the query's top-k exactly as scan_wide_wave does. Results are bit-identical:
+//    only candidates strictly worse than k vectors of the same list are skipped.
+// ============================================================================
+typedef float v16f __attribute__((ext_vector_type(16)));
+constexpr int kBoundPipe = 8;  // list rows in flight per lane (x 2 waves per SIMD: 16 KiB per SIMD)
+constexpr int kExactPipe = 4;  // rows in flight per lane of an exact re-rank round
+
+// (A real call: inlined into ivf_scan_wide, its registers would add to the exact
+// waves' and spill both; one call per segment costs nothing measurable.)
+template <int M>
+__device__ __forceinline__ void scan_wide_wave_mfma(const ScanArgs& a, const ScanItem it, const float4* qrow,
+                                                    const int np, float* tk_d, uint64_t* tk_i, uint32_t* s_thr,
+                                                    uint16_t* cand, const uint32_t seg) {
+    const uint32_t d4 = a.d4;
+    const int lane = lane_id();
+    const int qj = lane & 15;  // this lane's query: the B column of every D register
+    const bool qok = qj < np;
+    const uint32_t count = a.count[it.list];
+    const uint32_t seg_vectors = a.seg_blocks * 64;
+    const uint64_t b0 = a.block_off[it.list] + (uint64_t)seg * a.seg_blocks;
+    const uint32_t v0 = seg * seg_vectors;
+    const uint32_t nv = min(count - v0, seg_vectors);
+    const uint32_t nb = (nv + 63) >> 6;
+    const int k = (int)a.k;
+    const int cth = (k + 3) >> 2;  // lane rank of the block bound (k <= 16; larger k: no block bound)
+
+    for (int e = lane; e < kWaveQueries * k; e += 64) {
+        tk_d[e] = __builtin_inff();
+        tk_i[e] = kNoId;
+    }
+    float kdl = __builtin_inff();   // query qj's k-th exact distance (its top-k lives in LDS)
+    float tseg = __builtin_inff();  // query qj's smallest block bound in this segment
+    const float K = 4.0f * (float)(d4 * 4 + 4) * 5.9604645e-8f;  // 4 (n + 4) u
+    v16f acc = {};
+    float xn = 0.0f, qn = 0.0f;
+    float4 qb = qrow[qj];
+    const float4* seg_base = a.arena + b0 * d4 * 64;
+    auto compute = [&](const float4 x, uint32_t t, auto) {
+        const float4 q = qb;
+        qb = qrow[(size_t)(t + 1 == d4 ? 0 : t + 1) * 16 + qj];
+        acc = __builtin_amdgcn_mfma_f32_16x16x1f32(x.x, q.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x1f32(x.y, q.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x1f32(x.z, q.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x1f32(x.w, q.w, acc, 0, 0, 0);
+        xn = __builtin_fmaf(x.x, x.x, xn);
+        xn = __builtin_fmaf(x.y, x.y, xn);
+        xn = __builtin_fmaf(x.z, x.z, xn);
+        xn = __builtin_fmaf(x.w, x.w, xn);
+        qn = __builtin_fmaf(q.x, q.x, qn);
+        qn = __builtin_fmaf(q.y, q.y, qn);
+        qn = __builtin_fmaf(q.z, q.z, qn);
+        qn = __builtin_fmaf(q.w, q.w, qn);
+    };
+    auto finish = [&](uint32_t j, uint64_t id) {
+        const float xnl = xn, qnv = qn;
+        xn = 0.0f;
+        qn = 0.0f;
+        const float qa = sqrtf(qnv);
+        const float th = fminf(kdl, qok ? ord_dec(s_thr[qj]) : __builtin_inff());
+        const uint32_t vb = j * 64;
+        float lb[16];
+        uint32_t vmask = 0;
+        float m0 = __builtin_inff(), m1 = m0, m2 = m0, m3 = m0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int v = 16 * (r >> 2) + 4 * (lane >> 4) + (r & 3);
+            const float xv = __shfl(xnl, v);
+            const bool valid = vb + v < nv;
+            vmask |= valid ? 1u << r : 0u;
+            float ap, dl;
+            if constexpr (M == kL2) {
+                const float xa = sqrtf(xv);
+                ap = (qnv + xv) - 2.0f * acc[r];
+                dl = K * ((qa + xa) * (qa + xa)) + 1e-30f;
+            } else {
+                ap = -acc[r];
+                dl = K * (qa * sqrtf(xv)) + 1e-30f;
+            }
+            lb[r] = ap - dl;
+            float ub = ap + dl;
+            ub = valid && ub == ub ? ub : __builtin_inff();
+            m3 = fminf(m3, fmaxf(m2, ub));
+            m2 = fminf(m2, fmaxf(m1, ub));
+            m1 = fminf(m1, fmaxf(m0, ub));
+            m0 = fminf(m0, ub);
+        }
+        float tb = cth == 1 ? m0 : cth == 2 ? m1 : cth == 3 ? m2 : cth == 4 ? m3 : __builtin_inff();
+        tb = fmaxf(tb, xor_f<16>(tb));
+        tb = fmaxf(tb, xor_f<32>(tb));
+        tseg = fminf(tseg, tb);
+        const float T = fminf(th, tseg);
+        uint32_t bits = 0;
+        if (qok) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bits |= !(lb[r] > T) ? 1u << r : 0u;
+            bits &= vmask;
+        }
+        if (a.diag & 1) bits = 0;  // DIAGNOSTIC: no exact pass / top-k (results invalid)
+        // compact the candidates: (vector << 4 | query) per entry, lanes in order
+        const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, o);
+            inc += lane >= o ? y : 0u;
+        }
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        acc = v16f{};
+        if (total == 0) return;
+        uint32_t off = inc - cnt;
+        while (bits) {
+            const int r = __builtin_ctz(bits);
+            bits &= bits - 1;
+            const int v = 16 * (r >> 2) + 4 * (lane >> 4) + (r & 3);
+            cand[off++] = (uint16_t)((v << 4) | qj);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (a.mstats && lane == 0) atomicAdd(&a.mstats[0], (unsigned long long)total);
+        const float4* blk = seg_base + (size_t)j * d4 * 64;
+        for (uint32_t base = 0; base < total; base += 64) {
+            const bool act = base + lane < total;
+            const uint32_t ent = act ? cand[base + lane] : 0u;
+            const int cv = (int)(ent >> 4), cq = (int)(ent & 15);
+            // the reference's sequential sum for (query cq, vector cv), 8 rows in flight
+            const float4* xp = blk + cv;
+            const float4* qp = qrow + cq;
+            float sum = 0.0f;
+            for (uint32_t t0 = 0; t0 < d4; t0 += kExactPipe) {
+                float4 xv[kExactPipe], qv[kExactPipe];
+#pragma unroll
+                for (int u = 0; u < kExactPipe; ++u) {
+                    xv[u] = xp[(size_t)(t0 + u) * 64];
+                    qv[u] = qp[(size_t)(t0 + u) * 16];
+                }
+#pragma unroll
+                for (int u = 0; u < kExactPipe; ++u) sum = acc4<M>(sum, qv[u], xv[u]);
+            }
+            const float dist = dist_finish<M>(sum);
+            const uint64_t cid = shfl_u64(id, cv);
+            uint32_t qm = act ? 1u << cq : 0u;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) qm |= (uint32_t)__shfl_xor((int)qm, o);
+            qm = __builtin_amdgcn_readfirstlane(qm);
+            while (qm) {
+                const int gs = __builtin_ctz(qm);
+                qm &= qm - 1;
+                const float kdg = fminf(rd_lane(kdl, gs), ord_dec(s_thr[gs]));
+                float* sd = tk_d + gs * k;
+                uint64_t* si = tk_i + gs * k;
+                WaveTopK<1> tk;
+                tk.d[0] = lane < k ? sd[lane] : __builtin_inff();
+                tk.id[0] = lane < k ? si[lane] : kNoId;
+                float nkd;
+                uint64_t nki;
+                tk.at(k - 1, nkd, nki);
+                offer_lanes<1>(tk, act && cq == gs && dist <= kdg, dist, cid, k, nkd, nki);
+                if (lane < k) {
+                    sd[lane] = tk.d[0];
+                    si[lane] = tk.id[0];
+                }
+                if (qj == gs) kdl = nkd;
+                if (nkd < kdg && lane == 0) atomicMin(&s_thr[gs], ord_enc(nkd));
+            }
+        }
+    };
+    stream_blocks<kBoundPipe>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
+    if (a.mstats && lane == 0) atomicAdd(&a.mstats[1], (unsigned long long)nb);
+    // the segment's k-th distances lower the list-wide thresholds for later items
+    if (lane < np && kdl < __builtin_inff()) atomicMin(&a.thr[it.pair_start + lane], ord_enc(kdl));
+    for (int g = 0; g < np; ++g) {
+        const uint32_t part = a.part_base_sorted[it.pair_start + g] + seg;
+        if (lane < k) {
+            a.part_d[(size_t)part * k + lane] = tk_d[g * k + lane];
+            a.part_i[(size_t)part * k + lane] = tk_i[g * k + lane];
+        }
+    }
+}
+
 // One wave-item of a narrow list (<= 4 pairs of one segment).
 template <int R, int M>
 __device__ __forceinline__ void scan_narrow(const ScanArgs& a, const ScanItem it) {
@@ -1334,6 +1553,59 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
         __syncthreads();  // qlds is restaged by the next wide item
     }
     if (a.fused) drain_narrow<M>(a);
+}
+
+// ivf_scan_bounded: the wide items of >= a.mfma_min queries (items_w[counters[3] ..
+// counters[3] + counters[7])), one 4-wave workgroup per item at a time as in
+// ivf_scan_wide, every wave a bounded wave (scan_wide_wave_mfma). Its own kernel: the
+// bounded waves' registers inlined beside the exact waves' would spill both.
+// Dynamic LDS: [d4][16] float4 of staged queries (row-major), then per wave
+// kWaveQueries x k top-k ids (u64), then distances (f32).
+template <int M>
+__global__ __launch_bounds__(256, 2) void ivf_scan_bounded(ScanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float4 qlds[];
+    const uint32_t d4 = a.d4;
+    const uint32_t wv = wave_index();
+    uint64_t* tk_i = (uint64_t*)(qlds + (size_t)16 * d4) + (size_t)wv * kWaveQueries * a.k;
+    float* tk_d = (float*)((uint64_t*)(qlds + (size_t)16 * d4) + (size_t)4 * kWaveQueries * a.k) +
+                  (size_t)wv * kWaveQueries * a.k;
+    const uint32_t first = a.counters[3], n_bounded = a.counters[7];
+    __shared__ uint32_t s_next;
+    __shared__ uint32_t s_seg;
+    __shared__ uint32_t s_thr[16];
+    __shared__ uint16_t s_cand[4][1024];  // per wave: (vector << 4 | query) of one block's candidates
+    for (;;) {
+        if (threadIdx.x == 0) s_next = atomicAdd(&a.work[2], 1u);
+        __syncthreads();
+        const uint32_t b = s_next;
+        if (b >= n_bounded) break;
+        ScanItem it = a.items_w[first + b];
+        it.list = __builtin_amdgcn_readfirstlane(it.list);
+        it.seg = __builtin_amdgcn_readfirstlane(it.seg);
+        it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
+        it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
+        const int np = (int)it.npairs;  // <= 16 (wide group 16)
+        if (threadIdx.x == 0) s_seg = 0;
+        if (threadIdx.x < (uint32_t)np) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
+        for (uint32_t e = threadIdx.x; e < 16 * d4; e += blockDim.x) {
+            const uint32_t t = e >> 4, jq = e & 15;
+            qlds[e] = jq < (uint32_t)np
+                          ? ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + jq] >> 16) * d4 * 4))[t]
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        __syncthreads();
+        const uint32_t seg_vectors = a.seg_blocks * 64;
+        const uint32_t nseg = (a.count[it.list] + seg_vectors - 1) / seg_vectors;
+        const uint32_t seg0 = it.seg * a.segs_item, seg1 = min(nseg, seg0 + a.segs_item);
+        for (;;) {
+            uint32_t sg = 0;
+            if (lane_id() == 0) sg = atomicAdd(&s_seg, 1u);
+            sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
+            if (sg >= seg1) break;
+            scan_wide_wave_mfma<M>(a, it, qlds, np, tk_d, tk_i, s_thr, s_cand[wv], sg);
+        }
+        __syncthreads();  // qlds is restaged by the next item
+    }
 }
 
 // Offer n contiguous (dist, id) entries to a wave top-k: 64 x kPre entries per round,
@@ -1996,10 +2268,12 @@ void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint3
                  uint32_t P, uint32_t group, int wide, uint32_t segs_item, ScanItem* items, ScanItem* items_w,
                  uint32_t* counters,
                  uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp, uint32_t* nseg_qp,
-                 uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats, uint32_t* thr, hipStream_t s) {
+                 uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats, uint32_t* thr, uint32_t mfma_min,
+                 hipStream_t s) {
     uint32_t np = 1;
     while (np < B * P) np <<= 1;
-    ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, (uint32_t)wide, segs_item, items,
+    ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, (uint32_t)wide, segs_item,
+                                       wide == 16 ? mfma_min : 0u, items,
                                        items_w, counters, sorted_pair, part_base_sorted, part_base_qp, nseg_qp,
                                        l1base_qp, l1_items, stats, thr);
 }
@@ -2023,7 +2297,10 @@ void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes
 #undef VDB_MP
 }
 
-static constexpr size_t kWideStaticLds = 64;  // ivf_scan_wide's static LDS (the queue slot), rounded up
+// static LDS of ivf_scan_wide (queue slots, shared thresholds) and ivf_scan_bounded
+// (the same plus the waves' candidate lists), rounded up
+static constexpr size_t wide_static_lds(int waves) { return waves == 4 ? 256 : 256; }
+static constexpr size_t kBoundedStaticLds = 256 + 4 * 2048;
 
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves) {
     const size_t gw = 4 * (size_t)waves;
@@ -2031,7 +2308,7 @@ size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves) {
 }
 
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves) {
-    return k <= 64 && scan_wide_lds(d4, k, waves) <= kLdsBytes - kWideStaticLds;
+    return k <= 64 && scan_wide_lds(d4, k, waves) <= kLdsBytes - wide_static_lds(waves);
 }
 
 void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
@@ -2053,15 +2330,42 @@ void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanAr
 #undef VDB_SN
 }
 
+size_t scan_bounded_lds(uint32_t d4, uint32_t k) {
+    return (size_t)16 * d4 * sizeof(float4) + (size_t)4 * kWaveQueries * k * (sizeof(float) + sizeof(uint64_t));
+}
+
+bool scan_bounded_fits(uint32_t d4, uint32_t k) {
+    return k <= 64 && scan_bounded_lds(d4, k) <= kLdsBytes - kBoundedStaticLds;
+}
+
+void launch_scan_bounded(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
+    if (!grid_blocks || (metric != kL2 && metric != kIP)) return;
+    static const bool raised = [] {
+        const int dyn = (int)(kLdsBytes - kBoundedStaticLds);
+        (void)hipFuncSetAttribute((const void*)ivf_scan_bounded<kL2>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+        (void)hipFuncSetAttribute((const void*)ivf_scan_bounded<kIP>, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)raised;
+    const size_t lds = scan_bounded_lds(a.d4, a.k);
+    const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
+    if (metric == kL2) ivf_scan_bounded<kL2><<<g, 256, lds, s>>>(a);
+    else ivf_scan_bounded<kIP><<<g, 256, lds, s>>>(a);
+}
+
 void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves) {
     if (!grid_blocks) return;
     static const bool raised = [] {
         // wide items stage up to 16 (32) queries in LDS: allow the whole 160 KB of a CU
-        const int dyn = (int)(kLdsBytes - kWideStaticLds);
-        const void* fns[] = {(const void*)ivf_scan_wide<kL2, 4>, (const void*)ivf_scan_wide<kIP, 4>,
-                             (const void*)ivf_scan_wide<kCos, 4>, (const void*)ivf_scan_wide<kL2, 8>,
-                             (const void*)ivf_scan_wide<kIP, 8>, (const void*)ivf_scan_wide<kCos, 8>};
-        for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
+        const void* f4[] = {(const void*)ivf_scan_wide<kL2, 4>, (const void*)ivf_scan_wide<kIP, 4>,
+                            (const void*)ivf_scan_wide<kCos, 4>};
+        const void* f8[] = {(const void*)ivf_scan_wide<kL2, 8>, (const void*)ivf_scan_wide<kIP, 8>,
+                            (const void*)ivf_scan_wide<kCos, 8>};
+        for (const void* f : f4)
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes - wide_static_lds(4)));
+        for (const void* f : f8)
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes - wide_static_lds(8)));
         (void)hipGetLastError();
         return true;
     }();

@@ -71,7 +71,7 @@ void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint3
                  uint32_t B, uint32_t P, uint32_t group, int wide, uint32_t segs_item, ScanItem* items, ScanItem* items_w,
                  uint32_t* counters, uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp,
                  uint32_t* nseg_qp, uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats,
-                 uint32_t* thr, hipStream_t s);
+                 uint32_t* thr, uint32_t mfma_min, hipStream_t s);
 void launch_merge_partials(int regs, uint32_t grid_items, const uint32_t* probes, const uint32_t* count_global,
                            const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                            const uint2* l1_items, const uint32_t* counters, const float* part_d,
@@ -94,7 +94,7 @@ struct ScanArgs {
     uint32_t d4;
     uint32_t k;
     uint32_t wide_stride;  // wide-item dispatch stride (prime; 0/1 = plan order)
-    uint32_t* work;        // [2] item queues (narrow, wide), reset by the plan kernel
+    uint32_t* work;        // [3] item queues (narrow, wide, bounded), reset by the plan kernel
     uint32_t seg_blocks;   // 64-vector blocks per list segment (one wave's unit of a scan item)
     uint32_t diag;         // diagnostics only (0 in production): 1 skip top-k upkeep, 2 one query pair,
                            // 4 no insertion on a segment's first block, 8 on its later blocks
@@ -104,12 +104,18 @@ struct ScanArgs {
     uint32_t* thr;         // per sorted (query, probe) pair: the best k-th distance any wave has
                            // reached on that list so far (order-preserving uint encoding, reset
                            // by the plan kernel); candidates strictly worse are never inserted
+    uint32_t mfma_min;     // wide items of >= this many queries run the bounded (MFMA) waves (0: never)
+    unsigned long long* mstats;  // diagnostics (null in production): [0] exact re-ranks, [1] bounded blocks
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);
 void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
 // waves 4: items of <= 16 queries, two workgroups per CU; 8: items of <= 32, one per CU
 void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves = 4);
+// wide items of >= a.mfma_min queries (L2 / IP): bounded on the matrix cores, exact re-rank
+size_t scan_bounded_lds(uint32_t d4, uint32_t k);
+bool scan_bounded_fits(uint32_t d4, uint32_t k);
+void launch_scan_bounded(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                        const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,

@@ -76,6 +76,8 @@ typedef struct vdb_ivf_profile {
     uint64_t work_items;       /* sum over batches of scan work items */
     uint64_t scan_bytes;       /* algorithmic bytes read by ivf_scan: 4 * dim * scan_vectors */
     uint64_t pair_vectors;     /* sum over batches and (query, probe) pairs of n_l: distances computed */
+    uint64_t exact_reranks;    /* bounded scan: (query, vector) distances recomputed exactly (option diag & 16) */
+    uint64_t bounded_blocks;   /* bounded scan: 64-vector blocks bounded on the matrix cores (option diag & 16) */
 } vdb_ivf_profile;
 
 const char* vdb_last_error(void);
