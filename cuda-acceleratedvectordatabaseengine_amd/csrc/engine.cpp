@@ -549,6 +549,9 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "wide_group") {
             require(value == 16 || value == 32, "wide_group is 16 or 32");
             h->wide_group = (uint32_t)value;
+        } else if (n == "scan_blocks") {
+            require(value >= 0 && value <= (int64_t)vdbk::kPersistentBlocks, "scan_blocks is 0 (auto) .. 512");
+            h->scan_blocks = (uint32_t)value;
         } else if (n == "scan_mfma_min") {
             require(value >= 0 && value <= 16, "scan_mfma_min is 0 (never) .. 16");
             h->scan_mfma_min = (uint32_t)value;

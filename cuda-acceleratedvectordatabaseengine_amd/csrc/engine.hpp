@@ -270,6 +270,8 @@ struct vdb_ivf {
     // gathered re-read of an evicted vector) cost more than the VALU it saves
     // (DESIGN.md "Bounded scan: measured and rejected as default").
     uint32_t scan_mfma_min = 0;
+    // persistent scan grid in workgroups (0: 2 per CU on the whole chip)
+    uint32_t scan_blocks = 0;
     uint32_t segs_item_opt = 0;   // segments per wide item (0: one per wave, taken dynamically)
     uint32_t wide_group = 16;     // queries per wide item at most: 16 (4-wave workgroups) or 32 (8-wave)
     bool fused_scan = true;       // narrow items inside the wide scan's grid (option fused_scan; +2-3 %)
@@ -1467,7 +1469,9 @@ struct vdb_ivf {
             // (narrow_blocks counts 4-wave workgroups: as many waves start on the narrow queue)
             const uint32_t grid_cap = waves == 8 ? vdbk::kPersistentBlocks / 2 : vdbk::kPersistentBlocks;
             sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks * 4 / waves, grid_cap / 2));
-            vdbk::launch_scan_wide(metric, (uint32_t)std::max<uint64_t>(max_wide, (max_items + 3) / 4), sa, s, waves);
+            const uint64_t want = std::max<uint64_t>(max_wide, (max_items + 3) / 4);
+            vdbk::launch_scan_wide(metric, (uint32_t)(scan_blocks ? std::min<uint64_t>(want, scan_blocks) : want), sa, s,
+                                   waves);
         } else if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));

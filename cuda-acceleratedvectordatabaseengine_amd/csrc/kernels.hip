@@ -661,6 +661,44 @@ __device__ uint32_t plan_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
     return res;
 }
 
+// Exclusive block scans of NB counters at once (one barrier pair): v[b] -> ex[b],
+// tot[b] = block total. sh holds NB * 17 words.
+template <int NB>
+__device__ void plan_excl_scan_multi(const uint32_t* v, uint32_t* ex, uint32_t* tot, uint32_t* sh) {
+    const int lane = lane_id();
+    const uint32_t wid = threadIdx.x >> 6;
+    const uint32_t nw = blockDim.x >> 6;  // <= 16
+    uint32_t x[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        x[b] = v[b];
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x[b], off);
+            if (lane >= off) x[b] += y;
+        }
+        if (lane == 63) sh[b * 17 + wid] = x[b];
+    }
+    __syncthreads();
+    if (threadIdx.x < NB) {  // one thread per counter walks the wave totals
+        const uint32_t b = threadIdx.x;
+        uint32_t run = 0;
+        for (uint32_t w = 0; w < nw; ++w) {
+            const uint32_t t = sh[b * 17 + w];
+            sh[b * 17 + w] = run;
+            run += t;
+        }
+        sh[b * 17 + 16] = run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        ex[b] = sh[b * 17 + wid] + x[b] - v[b];
+        tot[b] = sh[b * 17 + 16];
+    }
+    __syncthreads();
+}
+
 // Query groups of one list with m (query, probe) pairs and ns segments. A list of at
 // least kWideMinSeg segments (with top-k in one register) is scanned by wide items:
 // ceil(m / wg) balanced groups x ceil(ns / segs_item) segment ranges, so each list is
@@ -712,6 +750,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     __shared__ uint32_t base_n[kPlanMaxPairs];
     __shared__ uint32_t base_w[kPlanMaxPairs];
     __shared__ uint32_t sh[33];
+    __shared__ uint32_t sh_multi[2 * 17];
     __shared__ uint32_t s_nvalid;
     const uint32_t tid = threadIdx.x;
     const uint32_t BP = B * P;
@@ -851,7 +890,11 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         const uint32_t l = list_of(st);
         const ListGroups g = list_groups(m, nseg_local[l], gn, wide);
         const uint32_t gi = off % g.wide, quad = off / g.wide;
-        const uint32_t p0 = gi * m / g.wide, p1 = (gi + 1) * m / g.wide;  // balanced groups
+        // groups balanced in query PAIRS (a wave computes two queries per packed op): all
+        // even-sized but the last, so the list costs ceil(m / 2) pair passes, not one more
+        // per odd group (40 queries: 12 + 14 + 14, not 14 + 13 + 13)
+        const uint32_t m2 = (m + 1) / 2;
+        const uint32_t p0 = min(2 * (gi * m2 / g.wide), m), p1 = min(2 * ((gi + 1) * m2 / g.wide), m);
         ScanItem it;
         it.list = l;
         it.seg = quad;
@@ -859,23 +902,42 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         it.npairs = p1 - p0;
         return it;
     };
-    // Wide items of >= mfma_min queries go to the bounded scan kernel: items_w holds the
-    // exact ones first, then the bounded ones, each in list order (a stable partition
-    // over contiguous per-thread ranges).
+    // Queue order of the wide items (a stable bucket sort over contiguous per-thread
+    // ranges): the exact items in list order, then the items of >= mfma_min queries, which
+    // the bounded scan kernel takes. (List order interleaves VALU-heavy hub items with
+    // HBM-bound ones all through the grid; heaviest-first made the scan alone 8 % faster at
+    // a 1/8 shard but two scans in flight 4 % slower at one GPU: both then run their heavy
+    // items at the same time.)
+    constexpr int kBuckets = 2;
+    auto bucket_of = [&](const ScanItem& it) -> uint32_t { return mfma_min && it.npairs >= mfma_min ? 1u : 0u; };
     const uint32_t wper = (n_wide + blockDim.x - 1) / blockDim.x;
     const uint32_t w0 = min(n_wide, tid * wper), w1 = min(n_wide, w0 + wper);
-    uint32_t nb_local = 0;
-    if (mfma_min)
-        for (uint32_t x = w0; x < w1; ++x) nb_local += wide_item(x).npairs >= mfma_min ? 1u : 0u;
-    uint32_t n_bounded;
-    const uint32_t bb_base = plan_excl_scan(nb_local, sh, n_bounded);
-    const uint32_t n_exact = n_wide - n_bounded;
+    uint32_t bcnt[kBuckets], bex[kBuckets], btot[kBuckets];
+#pragma unroll
+    for (int b = 0; b < kBuckets; ++b) bcnt[b] = 0;
+    for (uint32_t x = w0; x < w1; ++x) {
+        const uint32_t b = bucket_of(wide_item(x));
+#pragma unroll
+        for (int bb = 0; bb < kBuckets; ++bb) bcnt[bb] += b == (uint32_t)bb ? 1u : 0u;
+    }
+    plan_excl_scan_multi<kBuckets>(bcnt, bex, btot, sh_multi);
+    const uint32_t n_exact = btot[0], n_bounded = btot[1];
     {
-        uint32_t xb = n_exact + bb_base, xe = w0 - bb_base;
+        uint32_t base = 0;
+#pragma unroll
+        for (int b = 0; b < kBuckets; ++b) {  // bucket base + this thread's offset in it
+            const uint32_t t = btot[b];
+            bex[b] += base;
+            base += t;
+        }
         for (uint32_t x = w0; x < w1; ++x) {
             const ScanItem it = wide_item(x);
-            if (mfma_min && it.npairs >= mfma_min) items_w[xb++] = it;
-            else items_w[xe++] = it;
+            const uint32_t b = bucket_of(it);
+            uint32_t dst = 0;
+#pragma unroll
+            for (int bb = 0; bb < kBuckets; ++bb)
+                if (b == (uint32_t)bb) dst = bex[bb]++;
+            items_w[dst] = it;
         }
     }
     if (tid == 0) {
