@@ -19,7 +19,10 @@ constexpr int kMaxSegBlocks = 16;          // 64-vector blocks per scan segment 
 constexpr int kTilePipe = 16;              // float4 tiles of a list vector in flight per lane (scan)
 constexpr uint32_t kMfmaBlockedRows = 1024;  // coarse bounds: 2x2-blocked MFMA kernel from this many rows
 constexpr uint32_t kMergeBlocks = 256;  // level-1 partial merge: workgroups (grid-stride)
-constexpr int kTilePipeNarrow = 4;         // the same for narrow items (queries held in SGPRs)
+#ifndef VDB_TILE_PIPE_NARROW
+#define VDB_TILE_PIPE_NARROW 4
+#endif
+constexpr int kTilePipeNarrow = VDB_TILE_PIPE_NARROW;  // the same for narrow items (queries held in SGPRs)
 constexpr int kTileAlign = kTilePipe;      // D4 is padded to whole pipeline rounds
 constexpr int kMergeFan = 32;              // segment partials folded per level-1 merge wave
 constexpr int kWideGroup = 16;             // max queries per wide scan item (4-wave items)
