@@ -63,7 +63,8 @@ class Profile(ctypes.Structure):
                 ("coarse_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("scan_vectors", ctypes.c_uint64),
                 ("distinct_lists", ctypes.c_uint64), ("work_items", ctypes.c_uint64),
                 ("scan_bytes", ctypes.c_uint64), ("pair_vectors", ctypes.c_uint64),
-                ("exact_reranks", ctypes.c_uint64), ("bounded_blocks", ctypes.c_uint64)]
+                ("exact_reranks", ctypes.c_uint64), ("bounded_blocks", ctypes.c_uint64),
+                ("computed_vectors", ctypes.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -684,6 +684,7 @@ int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
         p.pair_vectors = st[4];
         p.exact_reranks = st[5];
         p.bounded_blocks = st[6];
+        p.computed_vectors = st[7];
         *out = p;
         hh->set_device();
     });

@@ -630,6 +630,9 @@ __global__ __launch_bounds__(256) void ivf_assign_rerank(const float* __restrict
 // (segment, group) so the groups that re-read a segment sit in one workgroup.
 // ============================================================================
 constexpr uint32_t kInvalidKey = 0xFFFFFFFFu;
+#ifndef VDB_SEED_LEVELS
+#define VDB_SEED_LEVELS 1  // wide-item queue levels by quad index (0: plan order)
+#endif
 
 __device__ uint32_t plan_excl_scan(uint32_t v, uint32_t* sh, uint32_t& total) {
     const int lane = lane_id();
@@ -750,7 +753,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     __shared__ uint32_t base_n[kPlanMaxPairs];
     __shared__ uint32_t base_w[kPlanMaxPairs];
     __shared__ uint32_t sh[33];
-    __shared__ uint32_t sh_multi[2 * 17];
+    __shared__ uint32_t sh_multi[(VDB_SEED_LEVELS + 2) * 17];
     __shared__ uint32_t s_nvalid;
     const uint32_t tid = threadIdx.x;
     const uint32_t BP = B * P;
@@ -863,6 +866,9 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
             bn += g.narrow * ns;
             bw += g.wide * ((ns + segs_item - 1) / segs_item);
             atomicAdd(&stats[1], (unsigned long long)count_local[l]);
+            // distances the scan computes: wide items run query pairs (an odd group pads one)
+            const uint32_t m = starts[cur + 1] - starts[cur];
+            atomicAdd(&stats[7], (unsigned long long)count_local[l] * (g.wide ? 2 * ((m + 1) / 2) : m));
         }
     }
     __syncthreads();
@@ -908,8 +914,17 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     // HBM-bound ones all through the grid; heaviest-first made the scan alone 8 % faster at
     // a 1/8 shard but two scans in flight 4 % slower at one GPU: both then run their heavy
     // items at the same time.)
-    constexpr int kBuckets = 2;
-    auto bucket_of = [&](const ScanItem& it) -> uint32_t { return mfma_min && it.npairs >= mfma_min ? 1u : 0u; };
+    // First quads first (VDB_SEED_LEVELS): every list's first quad is queued ahead of the
+    // other quads of all lists (with L levels: quads 0, .., L-1 each as a level, then the rest). Items of one list are otherwise taken within a fraction
+    // of an item's duration, so all of a hub list's segments would start from the cold
+    // (infinite) shared threshold; queued behind the first quads they start from the k-th
+    // distance of the list's first quad (a.thr), and most insertions never happen.
+    constexpr int kLevels = VDB_SEED_LEVELS;
+    constexpr int kBuckets = kLevels + 2;
+    auto bucket_of = [&](const ScanItem& it) -> uint32_t {
+        if (mfma_min && it.npairs >= mfma_min) return kLevels + 1;
+        return min(it.seg, (uint32_t)kLevels);
+    };
     const uint32_t wper = (n_wide + blockDim.x - 1) / blockDim.x;
     const uint32_t w0 = min(n_wide, tid * wper), w1 = min(n_wide, w0 + wper);
     uint32_t bcnt[kBuckets], bex[kBuckets], btot[kBuckets];
@@ -921,7 +936,10 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         for (int bb = 0; bb < kBuckets; ++bb) bcnt[bb] += b == (uint32_t)bb ? 1u : 0u;
     }
     plan_excl_scan_multi<kBuckets>(bcnt, bex, btot, sh_multi);
-    const uint32_t n_exact = btot[0], n_bounded = btot[1];
+    uint32_t n_exact = 0;
+#pragma unroll
+    for (int b = 0; b <= kLevels; ++b) n_exact += btot[b];
+    const uint32_t n_bounded = btot[kLevels + 1];
     {
         uint32_t base = 0;
 #pragma unroll
@@ -1137,7 +1155,14 @@ constexpr bool kBigGroupPrefetch = VDB_BIG_GROUP_PREFETCH != 0;
 // those k candidates are in that wave's segment partial and beat it — so it is never
 // inserted. Partials may then hold fewer than k entries; the merges take the top-min(k,
 // n_l) of the union, which is unchanged. Ties (equal distance) are always kept.
-template <int GP, int M, bool SPLIT>
+// ODD: the wave's last pair holds one query (an odd query count): that query runs on
+// plain v_sub/v_mul/v_add on the pair's low halves instead of a padded packed pair,
+// which costs the same per lane-op, so the padding half's work is not done at all.
+#ifndef VDB_ODD_PAIRS
+#define VDB_ODD_PAIRS 1
+#endif
+constexpr bool kOddPairs = VDB_ODD_PAIRS != 0;
+template <int GP, int M, bool SPLIT, bool ODD>
 __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds,
                                                const uint32_t pstride_rt, const int q0, const int np, float* tk_d,
                                                uint64_t* tk_i, uint32_t* s_thr, const uint32_t seg) {
@@ -1161,10 +1186,30 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
     }
     float kd[G];
     f2 acc[GP];
+    float acc1 = 0.0f;  // ODD: the single query of the last pair
 #pragma unroll
     for (int g = 0; g < G; ++g) kd[g] = __builtin_inff();
 #pragma unroll
     for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
+    // query g's running sum (g wave-uniform and unrolled: a register, no indexing)
+    auto qsum = [&](int g) -> float {
+        if (ODD && g == 2 * (GP - 1)) return acc1;
+        return (g & 1) ? acc[g >> 1].y : acc[g >> 1].x;
+    };
+    // pair p's four terms of tile (lo, hi) against list values x
+    auto pair_terms = [&](int p, const float4 lo, const float4 hi, const f2 xlo, const f2 xhi, const float4 x) {
+        if (ODD && p == GP - 1) {  // query 2p's dims sit in the low halves: lo.x, lo.z, hi.x, hi.z
+            acc1 = dist_term<M>(acc1, lo.x, x.x);
+            acc1 = dist_term<M>(acc1, lo.z, x.y);
+            acc1 = dist_term<M>(acc1, hi.x, x.z);
+            acc1 = dist_term<M>(acc1, hi.z, x.w);
+        } else {
+            acc[p] = dist_term2<M, 0>(acc[p], f2{lo.x, lo.y}, xlo);
+            acc[p] = dist_term2<M, 1>(acc[p], f2{lo.z, lo.w}, xlo);
+            acc[p] = dist_term2<M, 0>(acc[p], f2{hi.x, hi.y}, xhi);
+            acc[p] = dist_term2<M, 1>(acc[p], f2{hi.z, hi.w}, xhi);
+        }
+    };
 
     // Query pairs of tile t sit at qlds[(t * GP + p) * 2 + {0, 1}]: one address per
     // tile, the pairs at immediate offsets. Each pair's registers are refilled with
@@ -1188,20 +1233,14 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
 #pragma unroll
             for (int p = 0; p < GP; ++p) {
                 const float4 lo = cur[2 * p], hi = cur[2 * p + 1];
-                acc[p] = dist_term2<M, 0>(acc[p], f2{lo.x, lo.y}, xlo);
-                acc[p] = dist_term2<M, 1>(acc[p], f2{lo.z, lo.w}, xlo);
-                acc[p] = dist_term2<M, 0>(acc[p], f2{hi.x, hi.y}, xhi);
-                acc[p] = dist_term2<M, 1>(acc[p], f2{hi.z, hi.w}, xhi);
+                pair_terms(p, lo, hi, xlo, xhi, x);
             }
         } else {
             const float4* nxt = qlds + (size_t)(t + 1 == d4 ? 0 : t + 1) * pstride * 2;
 #pragma unroll
             for (int p = 0; p < GP; ++p) {
                 const float4 lo = qb[p][0], hi = qb[p][1];
-                acc[p] = dist_term2<M, 0>(acc[p], f2{lo.x, lo.y}, xlo);
-                acc[p] = dist_term2<M, 1>(acc[p], f2{lo.z, lo.w}, xlo);
-                acc[p] = dist_term2<M, 0>(acc[p], f2{hi.x, hi.y}, xhi);
-                acc[p] = dist_term2<M, 1>(acc[p], f2{hi.z, hi.w}, xhi);
+                pair_terms(p, lo, hi, xlo, xhi, x);
                 qb[p][0] = nxt[2 * p];
                 qb[p][1] = nxt[2 * p + 1];
             }
@@ -1216,7 +1255,7 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
         uint32_t pend = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const float dist = dist_finish<M>((g & 1) ? acc[g >> 1].y : acc[g >> 1].x);
+            const float dist = dist_finish<M>(qsum(g));
             if (g < np && __ballot(valid && dist <= th[g])) pend |= 1u << g;
         }
         if (a.diag & 1) pend = 0;  // DIAGNOSTIC: no top-k maintenance (results invalid)
@@ -1231,7 +1270,7 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
 #pragma unroll
                 for (int g = 0; g < G; ++g)
                     if (g == gs) {
-                        dist = dist_finish<M>((g & 1) ? acc[g >> 1].y : acc[g >> 1].x);
+                        dist = dist_finish<M>(qsum(g));
                         kdg = th[g];
                     }
                 float* sd = tk_d + gs * k;
@@ -1256,6 +1295,7 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
         }
 #pragma unroll
         for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
+        acc1 = 0.0f;
     };
     // more than 8 pairs: fewer tiles in flight (the pairs' query registers take the rest)
     constexpr int T = GP <= 8 ? kTilePipe : (kBigGroupPrefetch ? kTilePipe / 4 : kTilePipe / 2);
@@ -1600,14 +1640,16 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
             if (sg >= seg1) break;
 #define VDB_WW(GPN)                                                                       \
     case GPN:                                                                             \
-        if (W == 8 && split) scan_wide_wave<GPN, M, true>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg); \
-        else scan_wide_wave<GPN, M, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);           \
+        if (W == 8 && split) scan_wide_wave<GPN, M, true, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg); \
+        else if (kOddPairs && (nq & 1)) scan_wide_wave<GPN, M, false, true>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);  \
+        else scan_wide_wave<GPN, M, false, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);            \
         break;
             switch (gw) {
                 VDB_WW(1) VDB_WW(2) VDB_WW(3) VDB_WW(4) VDB_WW(5) VDB_WW(6) VDB_WW(7)
                 default:
-                    if (W == 8 && split) scan_wide_wave<8, M, true>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
-                    else scan_wide_wave<8, M, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
+                    if (W == 8 && split) scan_wide_wave<8, M, true, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
+                    else if (kOddPairs && (nq & 1)) scan_wide_wave<8, M, false, true>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
+                    else scan_wide_wave<8, M, false, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
                     break;
             }
 #undef VDB_WW

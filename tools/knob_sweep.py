@@ -66,7 +66,9 @@ def main():
             alg = p["scan_bytes"] / max(p["batches"], 1)
             print(json.dumps({"workload": wl, "opts": s, "scan_ms": round(p["scan_ms"] / n, 3),
                               "search_ms": round(p["total_ms"] / n, 3), "wall_ms": round(wall, 3),
-                              "alg_GB": round(alg / 1e9, 2), "frac": round(alg / (p["scan_ms"] / n * 1e-3) / 8e12, 4)}),
+                              "alg_GB": round(alg / 1e9, 2),
+                              "pairs_M": round(p["pair_vectors"] / max(p["batches"], 1) / 1e6, 2),
+                              "computed_M": round(p["computed_vectors"] / max(p["batches"], 1) / 1e6, 2), "frac": round(alg / (p["scan_ms"] / n * 1e-3) / 8e12, 4)}),
                   flush=True)
             for n_, _ in opts:  # back to defaults
                 idx.set_option(n_, DEFAULTS[n_])
