@@ -78,8 +78,8 @@ typedef struct vdb_ivf_profile {
     uint64_t pair_vectors;     /* sum over batches and (query, probe) pairs of n_l: distances computed */
     uint64_t exact_reranks;    /* bounded scan: (query, vector) distances recomputed exactly (option diag & 16) */
     uint64_t bounded_blocks;   /* bounded scan: 64-vector blocks bounded on the matrix cores (option diag & 16) */
-    uint64_t computed_vectors; /* distances the scan kernels compute (pair_vectors + the odd query of a
-                                  wide item's last pair, which runs as a padded pair) */
+    uint64_t computed_vectors; /* query slots the scan streams per vector: pair_vectors plus one per
+                                  odd wide group (its last query runs alone, on scalar ops) */
 } vdb_ivf_profile;
 
 const char* vdb_last_error(void);

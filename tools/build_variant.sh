@@ -6,11 +6,11 @@ set -e
 N=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
 P=$R/cuda-acceleratedvectordatabaseengine_amd
-make -s -C "$P" >/dev/null
+[ -n "$NOMAKE" ] || make -s -C "$P" >/dev/null
 O=$R/_variants/$N
 mkdir -p "$O"
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wall -I$R/include"
-/opt/rocm/bin/hipcc $F "$@" -c "$P/csrc/kernels.hip" -o "$O/kernels.o"
+/opt/rocm/bin/hipcc $F "$@" -c "${SRC:-$P/csrc/kernels.hip}" -I"$P/csrc" -o "$O/kernels.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libvdb_ivf.so" "$O/kernels.o" "$P/build/engine.o" \
     "$P/build/group.o" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f "$O/kernels.o"
