@@ -810,7 +810,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         fsum += fan_of(ns);
         vsum += count_local[list_of(s)];
     }
-    if (vsum) atomicAdd(&stats[4], vsum);
+    // (diagnostic counters: one atomic per wave, not per thread or list, below)
     uint32_t nd, nparts, nl1;
     const uint32_t dl_base = plan_excl_scan(hsum, sh, nd);
     const uint32_t pb_base = plan_excl_scan(nsum, sh, nparts);
@@ -852,6 +852,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     uint32_t n_narrow, n_wide;
     const uint32_t bn_base = plan_excl_scan(nsum_n, sh, n_narrow);
     const uint32_t bw_base = plan_excl_scan(nsum_w, sh, n_wide);
+    unsigned long long lsum = 0, csum = 0;
     {
         int cur = (int)dl_base - 1;
         uint32_t bn = bn_base, bw = bw_base;
@@ -865,48 +866,80 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
             base_w[cur] = bw;
             bn += g.narrow * ns;
             bw += g.wide * ((ns + segs_item - 1) / segs_item);
-            atomicAdd(&stats[1], (unsigned long long)count_local[l]);
-            // distances the scan computes: wide items run query pairs (an odd group pads one)
+            lsum += count_local[l];
+            // query slots streamed: wide items run query pairs (an odd group's last query
+            // runs alone on scalar ops, but holds a pair slot)
             const uint32_t m = starts[cur + 1] - starts[cur];
-            atomicAdd(&stats[7], (unsigned long long)count_local[l] * (g.wide ? 2 * ((m + 1) / 2) : m));
+            csum += (unsigned long long)count_local[l] * (g.wide ? 2 * ((m + 1) / 2) : m);
         }
     }
     __syncthreads();
 
     // Emit items in parallel. Items of one list are ordered (segment or quad, group):
     // the groups re-reading one stretch of the list are adjacent in the grid.
-    for (uint32_t x = tid; x < n_narrow; x += blockDim.x) {
-        const uint32_t dl = find_owner(base_n, nd, x);
-        const uint32_t off = x - base_n[dl];
-        const uint32_t st = starts[dl], m = starts[dl + 1] - st;
-        const uint32_t l = list_of(st);
-        const ListGroups g = list_groups(m, nseg_local[l], gn, wide);
-        const uint32_t gi = off % g.narrow, seg = off / g.narrow;
-        ScanItem it;
-        it.list = l;
-        it.seg = seg;
-        it.pair_start = st + gi * gn;
-        it.npairs = min(gn, m - gi * gn);
-        items_n[x] = it;
+    // Each thread emits a contiguous range of items with a cursor (list, group, segment):
+    // one binary search per thread, then O(1) per item (no per-item search or division).
+    struct Cur {
+        uint32_t dl, st, m, l, ng, nitems, off, gi, seg;
+    };
+    auto cur_open = [&](Cur& c, uint32_t dl, uint32_t off, bool is_wide) {
+        c.dl = dl;
+        c.st = starts[dl];
+        c.m = starts[dl + 1] - c.st;
+        c.l = list_of(c.st);
+        const uint32_t ns = nseg_local[c.l];
+        const ListGroups g = list_groups(c.m, ns, gn, wide);
+        c.ng = is_wide ? g.wide : g.narrow;  // groups (0: the list has no items of this kind)
+        c.nitems = is_wide ? g.wide * ((ns + segs_item - 1) / segs_item) : g.narrow * ns;
+        c.off = off;
+        c.gi = c.ng ? off % c.ng : 0;
+        c.seg = c.ng ? off / c.ng : 0;
+    };
+    auto cur_next = [&](Cur& c, bool is_wide) {  // the next item in plan order
+        if (++c.off < c.nitems) {
+            if (++c.gi == c.ng) c.gi = 0, ++c.seg;
+            return;
+        }
+        uint32_t dl = c.dl;
+        do cur_open(c, ++dl, 0, is_wide);
+        while (c.nitems == 0 && dl + 1 < nd);
+    };
+    {
+        const uint32_t per_n = (n_narrow + blockDim.x - 1) / blockDim.x;
+        const uint32_t x0 = min(n_narrow, tid * per_n), x1 = min(n_narrow, x0 + per_n);
+        Cur c;
+        if (x0 < x1) {
+            const uint32_t dl = find_owner(base_n, nd, x0);
+            cur_open(c, dl, x0 - base_n[dl], false);
+            while (c.off >= c.nitems) cur_next(c, false);  // (lists without narrow items share a base)
+        }
+        for (uint32_t x = x0; x < x1; ++x) {
+            ScanItem it;
+            it.list = c.l;
+            it.seg = c.seg;
+            it.pair_start = c.st + c.gi * gn;
+            it.npairs = min(gn, c.m - c.gi * gn);
+            items_n[x] = it;
+            if (x + 1 < x1) cur_next(c, false);
+        }
     }
-    auto wide_item = [&](uint32_t x) {
-        const uint32_t dl = find_owner(base_w, nd, x);
-        const uint32_t off = x - base_w[dl];
-        const uint32_t st = starts[dl], m = starts[dl + 1] - st;
-        const uint32_t l = list_of(st);
-        const ListGroups g = list_groups(m, nseg_local[l], gn, wide);
-        const uint32_t gi = off % g.wide, quad = off / g.wide;
-        // groups balanced in query PAIRS (a wave computes two queries per packed op): all
-        // even-sized but the last, so the list costs ceil(m / 2) pair passes, not one more
-        // per odd group (40 queries: 12 + 14 + 14, not 14 + 13 + 13)
-        const uint32_t m2 = (m + 1) / 2;
-        const uint32_t p0 = min(2 * (gi * m2 / g.wide), m), p1 = min(2 * ((gi + 1) * m2 / g.wide), m);
+    // groups balanced in query PAIRS (a wave computes two queries per packed op): all
+    // even-sized but the last, so the list costs ceil(m / 2) pair passes, not one more per
+    // odd group (40 queries: 12 + 14 + 14, not 14 + 13 + 13)
+    auto wide_item = [&](const Cur& c) {
+        const uint32_t m2 = (c.m + 1) / 2;
+        const uint32_t p0 = min(2 * (c.gi * m2 / c.ng), c.m), p1 = min(2 * ((c.gi + 1) * m2 / c.ng), c.m);
         ScanItem it;
-        it.list = l;
-        it.seg = quad;
-        it.pair_start = st + p0;
+        it.list = c.l;
+        it.seg = c.seg;
+        it.pair_start = c.st + p0;
         it.npairs = p1 - p0;
         return it;
+    };
+    auto wide_cursor = [&](Cur& c, uint32_t x0) {
+        const uint32_t dl = find_owner(base_w, nd, x0);
+        cur_open(c, dl, x0 - base_w[dl], true);
+        while (c.off >= c.nitems) cur_next(c, true);
     };
     // Queue order of the wide items (a stable bucket sort over contiguous per-thread
     // ranges): the exact items in list order, then the items of >= mfma_min queries, which
@@ -930,10 +963,15 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     uint32_t bcnt[kBuckets], bex[kBuckets], btot[kBuckets];
 #pragma unroll
     for (int b = 0; b < kBuckets; ++b) bcnt[b] = 0;
-    for (uint32_t x = w0; x < w1; ++x) {
-        const uint32_t b = bucket_of(wide_item(x));
+    {
+        Cur c;
+        if (w0 < w1) wide_cursor(c, w0);
+        for (uint32_t x = w0; x < w1; ++x) {
+            const uint32_t b = bucket_of(wide_item(c));
 #pragma unroll
-        for (int bb = 0; bb < kBuckets; ++bb) bcnt[bb] += b == (uint32_t)bb ? 1u : 0u;
+            for (int bb = 0; bb < kBuckets; ++bb) bcnt[bb] += b == (uint32_t)bb ? 1u : 0u;
+            if (x + 1 < w1) cur_next(c, true);
+        }
     }
     plan_excl_scan_multi<kBuckets>(bcnt, bex, btot, sh_multi);
     uint32_t n_exact = 0;
@@ -948,15 +986,29 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
             bex[b] += base;
             base += t;
         }
+        Cur c;
+        if (w0 < w1) wide_cursor(c, w0);
         for (uint32_t x = w0; x < w1; ++x) {
-            const ScanItem it = wide_item(x);
+            const ScanItem it = wide_item(c);
             const uint32_t b = bucket_of(it);
             uint32_t dst = 0;
 #pragma unroll
             for (int bb = 0; bb < kBuckets; ++bb)
                 if (b == (uint32_t)bb) dst = bex[bb]++;
             items_w[dst] = it;
+            if (x + 1 < w1) cur_next(c, true);
         }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        vsum += __shfl_xor(vsum, off);
+        lsum += __shfl_xor(lsum, off);
+        csum += __shfl_xor(csum, off);
+    }
+    if ((tid & 63) == 0) {
+        if (vsum) atomicAdd(&stats[4], vsum);
+        if (lsum) atomicAdd(&stats[1], lsum);
+        if (csum) atomicAdd(&stats[7], csum);
     }
     if (tid == 0) {
         counters[0] = n_narrow;
@@ -967,7 +1019,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         counters[5] = 0;  // bounded workgroups)
         counters[6] = 0;
         counters[7] = n_bounded;  // bounded items: items_w[n_exact, n_exact + n_bounded)
-        atomicAdd(&stats[0], (unsigned long long)nd);
+        atomicAdd(&stats[0], (unsigned long long)nd);  // (the per-wave sums follow)
         atomicAdd(&stats[2], (unsigned long long)(n_narrow + n_wide));
         atomicAdd(&stats[3], 1ull);
     }
