@@ -773,22 +773,32 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     }
     __syncthreads();
 
+    // Bitonic sort in LDS, one compare-exchange per thread and step: pair p is (i, i + j)
+    // with i = 2j (p / j) + p % j. A wave's 64 pairs then lie inside one 128-key block for
+    // every j <= 64, so those steps need no workgroup barrier (a wave's LDS operations
+    // complete in order); only the steps with j >= 128 (and the step before one) do.
+    const uint32_t npairs = NP >> 1;
     for (uint32_t kk = 2; kk <= NP; kk <<= 1) {
         for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = tid; i < NP; i += blockDim.x) {
-                const uint32_t x = i ^ j;
-                if (x > i) {
-                    const uint32_t a = keys[i], b = keys[x];
-                    const bool asc = (i & kk) == 0;
-                    if ((a > b) == asc) {
-                        keys[i] = b;
-                        keys[x] = a;
-                    }
+            for (uint32_t p = tid; p < npairs; p += blockDim.x) {
+                const uint32_t i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), x = i + j;
+                const uint32_t a = keys[i], b = keys[x];
+                if ((a > b) == ((i & kk) == 0)) {
+                    keys[i] = b;
+                    keys[x] = a;
                 }
             }
-            __syncthreads();
+            const uint32_t jn = j > 1 ? j >> 1 : kk;  // the next step's distance
+            if (j >= 128 || jn >= 128) {
+                __syncthreads();
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
         }
     }
+    __syncthreads();
     for (uint32_t i = tid; i < NP; i += blockDim.x)
         if (keys[i] != kInvalidKey && (i + 1 == NP || keys[i + 1] == kInvalidKey)) s_nvalid = i + 1;
     __syncthreads();
