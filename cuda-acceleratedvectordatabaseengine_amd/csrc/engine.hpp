@@ -91,6 +91,12 @@ int guarded(F&& f) {
 // stream. hipFreeAsync never synchronises the device the way hipFree does; the engine only
 // releases a pooled buffer once no queued work can read it (stream synchronised, searches
 // quiesced, or the workspace slot's previous call done).
+// Off by default: on ROCm 7 buffers from the pool serialised the three batches a device
+// runs in flight (1/8-shard rehearsal, 3 in flight: 93.7K QPS before the pool, 81.3K with
+// it, 0.68 -> 0.79 ms per batch at an unchanged scan time); plain hipMalloc buffers overlap.
+#ifndef VDB_DEVICE_POOL
+#define VDB_DEVICE_POOL 0
+#endif
 struct DevicePool {
     hipMemPool_t pool = nullptr;
     hipStream_t stream = nullptr;
@@ -124,7 +130,7 @@ struct DevBuf {
     bool pooled = false;  // device memory from the device's stream-ordered pool
     int dev = 0;          // (pooled) the device the memory belongs to
     DevBuf() = default;
-    explicit DevBuf(bool pool) : pooled(pool) {}
+    explicit DevBuf(bool pool) : pooled(pool && VDB_DEVICE_POOL) {}
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() { release(); }

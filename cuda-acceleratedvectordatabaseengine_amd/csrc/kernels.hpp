@@ -18,7 +18,10 @@ constexpr int kMaxSegBlocks = 16;          // 64-vector blocks per scan segment 
                                            // size is 1..8, chosen per shard size by the engine)
 constexpr int kTilePipe = 16;              // float4 tiles of a list vector in flight per lane (scan)
 constexpr uint32_t kMfmaBlockedRows = 1024;  // coarse bounds: 2x2-blocked MFMA kernel from this many rows
-constexpr uint32_t kMergeBlocks = 256;  // level-1 partial merge: workgroups (grid-stride)
+#ifndef VDB_MERGE_BLOCKS
+#define VDB_MERGE_BLOCKS 1024  // measured: 53 -> 27 us per batch vs 256, throughput unchanged
+#endif
+constexpr uint32_t kMergeBlocks = VDB_MERGE_BLOCKS;  // level-1 partial merge: workgroups (grid-stride)
 #ifndef VDB_TILE_PIPE_NARROW
 #define VDB_TILE_PIPE_NARROW 4
 #endif
