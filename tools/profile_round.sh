@@ -29,6 +29,9 @@ run() {  # run <name> <seconds> <cmd...>
     if [ $rc -ne 0 ]; then tail -30 "$O/$name.log"; exit $rc; fi
 }
 SHORT="--steps 5 --warmup 1 --no-cpu --prof-steps 2"
+# the bench lines read this call's PMC traffic, or the committed file when no traffic step ran
+TJ="$O/traffic.json"
+[[ ",$STEPS," == *",traffic"* ]] || TJ="$R/profiles/traffic.json"
 CFG4="--cfg cfg4 --emulate-shard 8 --no-cpu --inflight 3"
 if has traffic; then
     run pmc_iid 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ivf_scan_ -d "$O/pmc_iid" -o f -f csv -- python3 bench.py $SHORT
@@ -49,9 +52,9 @@ if has mfma; then
     python3 tools/mfma_report.py "$O/pmc_mfma" "$O/trace_mfma" "$O/mfma.json" | tail -30
 fi
 if has bench; then
-    run bench 400 python3 -u bench.py --traffic-json "$O/traffic.json" --host-api
+    run bench 400 python3 -u bench.py --traffic-json "$TJ" --host-api
     grep '^{' "$O/bench.log" > "$O/bench.json" && cut -c 1-400 "$O/bench.json"
-    run bench_mix 400 python3 -u bench.py --traffic-json "$O/traffic.json" --data mixture --host-api
+    run bench_mix 400 python3 -u bench.py --traffic-json "$TJ" --data mixture --host-api
     grep '^{' "$O/bench_mix.log" > "$O/bench_mix.json" && cut -c 1-400 "$O/bench_mix.json"
 fi
 if has trace; then
@@ -65,7 +68,7 @@ if has trace; then
     head -6 "$O/kernel_stats_mixture.csv"
 fi
 if has shard; then
-    run shard 600 python3 -u bench.py $CFG4 --shard-check 4 --traffic-json "$O/traffic.json"
+    run shard 600 python3 -u bench.py $CFG4 --shard-check 4 --traffic-json "$TJ"
     grep '^{' "$O/shard.log" > "$O/shard.json" && cut -c 1-400 "$O/shard.json"
 fi
 if has shardtrace; then
