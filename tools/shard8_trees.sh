@@ -1,4 +1,6 @@
-# 1/8-shard emulation (3 in flight) of whole trees built under _variants/<tree>/ and of HEAD.
+# 1/8-shard emulation (3 in flight) of whole trees built under _variants/<tree>/ (a git
+# worktree's bench.py + package + built lib) and of the working tree ("-"), one GPU call.
+#   usage: bash tools/shard8_trees.sh <tree or -> ...
 set -o pipefail
 O=$PWD/gpurun_out/s15; mkdir -p $O
 for t in "$@"; do
