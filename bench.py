@@ -90,7 +90,7 @@ def build_index(vdb, args, device, rank, world):
     fill_rows(vdb, args, data, 0, n, 12345, stream)
     ids = torch.arange(n, dtype=torch.int64, device=device)
     torch.cuda.synchronize()
-    idx = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, args.nlist, vdb.Metric.L2, device=device.index))
+    idx = new_index(vdb, args, device)
     t0 = time.perf_counter()
     idx.train_device(data.data_ptr(), min(args.train, n))
     t1 = time.perf_counter()
@@ -102,21 +102,25 @@ def build_index(vdb, args, device, rank, world):
     return idx, {"train_s": round(t1 - t0, 3), "add_s": round(t2 - t1, 3)}
 
 
-def build_index_sharded(vdb, args, device, rank, world):
-    """Sharded build for an index larger than one GPU (configs[3]: 100M x 768 = 307 GB).
+def new_index(vdb, args, device):
+    # max_gpu_memory=0: every list HBM-resident (the reference's 8 GiB default Config cap
+    # would put a 31 GB index on the list-cache tier)
+    return vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(args.dim, args.nlist, vdb.Metric.L2, max_gpu_memory=0,
+                                                    device=device.index))
 
-    The database is generated chunk by chunk (the same counter-based draws as one
-    whole-array generation). Pass 1 assigns every chunk (exact argmin, assign_to_lists,
-    ivf_flat_index.cpp:259-295) into a resident list-id array; the final list sizes give
-    the LPT plan (plan_shard); pass 2 regenerates each chunk and appends only the lists
-    this rank owns. `world` here is the number of shards (ranks, or --emulate-shard)."""
+
+def sharded_assign(vdb, args, device, rank):
+    """Pass 1 of the sharded build for an index larger than one GPU (configs[3]: 100M x 768
+    = 307 GB): train on the first rows, then generate the database chunk by chunk (the
+    same counter-based draws as one whole-array generation) and assign every row (exact
+    argmin, assign_to_lists, ivf_flat_index.cpp:259-295) into a resident list-id array.
+    Returns the trained (empty) index, the assignment and the final list sizes."""
     dim, n = args.dim, args.nvec
     stream = torch.cuda.current_stream().cuda_stream
     chunk = min(n, args.build_chunk)
     data = torch.empty((chunk, dim), dtype=torch.float32, device=device)
-    ids = torch.empty(chunk, dtype=torch.int64, device=device)
     asg = torch.empty(n, dtype=torch.int32, device=device)
-    idx = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, args.nlist, vdb.Metric.L2, device=device.index))
+    idx = new_index(vdb, args, device)
     t0 = time.perf_counter()
     ntrain = min(args.train, n)
     fill_rows(vdb, args, data, 0, ntrain, 12345, stream)
@@ -131,6 +135,21 @@ def build_index_sharded(vdb, args, device, rank, world):
         log(rank, f"[bench] assigned {a + m} of {n} ({time.perf_counter() - t1:.1f}s)")
     sizes = torch.bincount(asg, minlength=args.nlist).cpu().numpy().astype(np.uint64)
     t2 = time.perf_counter()
+    del data
+    torch.cuda.empty_cache()
+    return idx, asg, sizes, {"train_s": round(t1 - t0, 3), "assign_s": round(t2 - t1, 3)}
+
+
+def sharded_append(vdb, args, device, idx, asg, sizes, rank, world):
+    """Pass 2: the LPT plan from the final list sizes fixes this shard's lists (plan_shard),
+    then every chunk is regenerated and only the owned lists' rows are appended. `world`
+    is the number of shards (ranks, or --emulate-shard)."""
+    dim, n = args.dim, args.nvec
+    stream = torch.cuda.current_stream().cuda_stream
+    chunk = min(n, args.build_chunk)
+    data = torch.empty((chunk, dim), dtype=torch.float32, device=device)
+    ids = torch.empty(chunk, dtype=torch.int64, device=device)
+    t0 = time.perf_counter()
     idx.plan_shard(rank, world, sizes)
     for a in range(0, n, chunk):
         m = min(chunk, n - a)
@@ -138,13 +157,20 @@ def build_index_sharded(vdb, args, device, rank, world):
         torch.arange(a, a + m, dtype=torch.int64, device=device, out=ids[:m])
         torch.cuda.synchronize()
         idx.add_to_lists_device(data.data_ptr(), ids.data_ptr(), asg[a:].data_ptr(), m)
-    t3 = time.perf_counter()
-    del data, ids, asg
+    t1 = time.perf_counter()
+    del data, ids
     torch.cuda.empty_cache()
-    log(rank, f"[bench] sharded build: train {t1 - t0:.2f}s assign {t2 - t1:.2f}s append {t3 - t2:.2f}s; "
-              f"shard {rank}/{world} {idx.gpu_bytes_allocated() / 2**30:.1f} GiB, largest list {int(sizes.max())}")
-    return idx, {"train_s": round(t1 - t0, 3), "assign_s": round(t2 - t1, 3), "append_s": round(t3 - t2, 3),
-                 "sharded_build": f"shard {rank} of {world}"}
+    log(0, f"[bench] shard {rank}/{world}: append {t1 - t0:.2f}s, {idx.gpu_bytes_allocated() / 2**30:.1f} GiB, "
+           f"largest list {int(sizes.max())}")
+    return {"append_s": round(t1 - t0, 3), "sharded_build": f"shard {rank} of {world}"}
+
+
+def build_index_sharded(vdb, args, device, rank, world):
+    idx, asg, sizes, info = sharded_assign(vdb, args, device, rank)
+    info.update(sharded_append(vdb, args, device, idx, asg, sizes, rank, world))
+    del asg
+    torch.cuda.empty_cache()
+    return idx, info
 
 
 def host_cpu_share():
@@ -289,20 +315,29 @@ def host_api_leg(idx, args, queries, out_d, out_i):
 
 
 def tier_leg(vdb, idx, args, device, queries):
-    """configs[4]'s mechanism on one GPU: the index is written to a file larger than the
-    HBM list cache (vdb_ivf_save), a fresh handle serves it from that file through the
+    """configs[4]'s mechanism on one GPU: the index (or, for a sharded build, this rank's
+    shard: a shard file with only its own lists' rows) is written to a file larger than
+    the HBM list cache (vdb_ivf_save), a fresh handle serves it from that file through the
     list-cache tier (vdb_ivf_open_lists: io_uring reads, sub-batches cut to the cache,
     next sub-batch's lists loaded while the current one scans, next-use eviction), and
     calls of --tier-call queries are timed. Bytes read per batch of --batch queries are
-    reported against the batch's algorithmic list bytes (the floor without a cache)."""
+    reported against the batch's algorithmic list bytes (the floor without a cache); the
+    first call is checked bit for bit against the HBM-resident index it was saved from."""
     import tempfile
     d = args.tier_dir or tempfile.gettempdir()
     path = os.path.join(d, f"vdb_tier_{os.getpid()}.ivf")
+    call = args.tier_call
+    st = torch.cuda.current_stream()
+    ref_d = torch.empty((call, args.k), dtype=torch.float32, device=device)
+    ref_i = torch.empty((call, args.k), dtype=torch.int64, device=device)
+    idx.search_device(queries.data_ptr(), call, args.nprobe, args.k, ref_d.data_ptr(), ref_i.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     idx.save(path)
     t_save = time.perf_counter() - t0
     file_bytes = os.path.getsize(path)
-    cfg = vdb.IVFFlatIndex.Config(args.dim, args.nlist, vdb.Metric.L2, device=device.index)
+    shard_bytes = idx.get_gpu_memory_usage()  # this handle's lists, count * (dim * 4 + 8)
+    cfg = vdb.IVFFlatIndex.Config(args.dim, args.nlist, vdb.Metric.L2, max_gpu_memory=0, device=device.index)
     idx.close()  # the HBM-resident index is gone: only the tier's cache holds lists now
     torch.cuda.empty_cache()
     try:
@@ -310,13 +345,12 @@ def tier_leg(vdb, idx, args, device, queries):
         h.set_option("list_cache_bytes", int(args.tier_cache_gib * (1 << 30)))
         h.set_option("batch", args.batch)
         h.open_lists(path)
-        call = args.tier_call
-        st = torch.cuda.current_stream()
         od = torch.empty((call, args.k), dtype=torch.float32, device=device)
         oi = torch.empty((call, args.k), dtype=torch.int64, device=device)
         calls = min(args.tier_calls, len(queries) // call)
         h.search_device(queries.data_ptr(), call, args.nprobe, args.k, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
         torch.cuda.synchronize()  # (warm-up call: code objects, staging, the cache's first contents)
+        same = bool(torch.equal(oi, ref_i) and torch.equal(od.view(torch.int32), ref_d.view(torch.int32)))
         s0 = h.cache_stats()
         h.profile_enable(True)
         h.profile_reset()
@@ -334,13 +368,15 @@ def tier_leg(vdb, idx, args, device, queries):
         read = (s1["file_bytes_read"] - s0["file_bytes_read"]) / batches
         return {"value": round(nq / el, 1), "unit": "queries/s", "calls": calls - 1, "queries_per_call": call,
                 "file": path, "file_gb": round(file_bytes / 1e9, 2), "save_s": round(t_save, 1),
-                "cache_gib": args.tier_cache_gib, "cache_fraction_of_file": round(args.tier_cache_gib * (1 << 30) / file_bytes, 3),
+                "lists_gb": round(shard_bytes / 1e9, 2),
+                "shard_file": args.emulate_shard > 1 or args.sharded_build,
+                "cache_gib": args.tier_cache_gib, "cache_fraction_of_lists": round(args.tier_cache_gib * (1 << 30) / shard_bytes, 3),
                 "file_bytes_read_per_batch": int(read), "algorithmic_bytes_per_batch": int(alg),
                 "read_over_algorithmic": round(read / alg, 3) if alg else None,
                 "file_read_gbps": round((s1["file_bytes_read"] - s0["file_bytes_read"]) / el / 1e9, 2),
                 "subbatches": s1["subbatches"] - s0["subbatches"], "prefetches": s1["prefetches"] - s0["prefetches"],
                 "sync_loads": s1["sync_loads"] - s0["sync_loads"], "io_uring": s1["io_uring"], "o_direct": s1["o_direct"],
-                "batch": args.batch}
+                "batch": args.batch, "parity_with_resident_index": same}
     finally:
         os.unlink(path)
 
@@ -375,6 +411,24 @@ def shard_parity(vdb, idx, args, queries_host, rank, world):
     same = bool(np.array_equal(I, Ig) and np.array_equal(D.view(np.uint32), Dg.view(np.uint32)))
     return {"queries": len(sample), "shard": f"{rank} of {world}", "vectors_exported": loaded,
             "oracle_s": round(t_cpu, 2), "bit_identical": same}
+
+
+def lookup_traffic(path, key, build_id):
+    """PMC HBM bytes per scan launch for workload `key`, measured by tools/pmc_traffic.py
+    (rocprofv3 FETCH_SIZE, x2 gfx950 correction) ON A LIBRARY OF THIS BUILD ID: an entry
+    taken on other kernel sources is stale, and the line then carries traffic null.
+    Returns (bytes or None, a note saying which)."""
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, f"no traffic file ({os.path.basename(path)})"
+    entry = tj.get("workloads", {}).get(key)
+    if not entry:
+        return None, f"no PMC entry for {key}"
+    if entry.get("build_id") != build_id:
+        return None, f"PMC entry for {key} was measured on build {entry.get('build_id')}, this library is {build_id}"
+    return entry.get("hbm_bytes_per_scan_launch"), f"rocprofv3 FETCH_SIZE x2, build {build_id}"
 
 
 def launch_ranks(n):
@@ -421,8 +475,14 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per ivf_scan launch for this workload (or null)")
     ap.add_argument("--emulate-shard", type=int, default=0, metavar="W",
-                    help="diagnostic: one process keeps rank 0's LPT shard of W and runs its partial search "
+                    help="diagnostic: one process keeps one rank's LPT shard of W and runs its partial search "
                          "(the per-GPU work of a W-GPU node, without the all-gather); not a bench line")
+    ap.add_argument("--emulate-rank", default="0", metavar="R",
+                    help="with --emulate-shard: the rank emulated (0..W-1), or 'all' to time every rank's shard in "
+                         "turn (sharded build) and report the per-rank balance")
+    ap.add_argument("--comm-timeout", type=float, default=120.0,
+                    help="N ranks, engine exchange: seconds before a communicator init or an exchange that has not "
+                         "completed fails the run with an error naming the rank (option comm_timeout_ms)")
     ap.add_argument("--cfg", choices=["cfg2", "cfg3", "cfg4"], default=None,
                     help="BASELINE.json configs preset: cfg2 1M/256/16, cfg3 10M/4096/32 (default), "
                          "cfg4 100M/16384/64 (sharded build; on one GPU only with --emulate-shard 8)")
@@ -453,6 +513,9 @@ def main():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning knob (vdb_ivf_set_option), e.g. wide_stride=1; results never change")
     args = ap.parse_args()
+    if args.emulate_rank == "all":
+        args.sharded_build = True  # every rank's shard from one assignment pass
+        args.emulate_shard = args.emulate_shard or 8
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # One process per GPU: launch the N ranks as children before anything touches
         # the GPU, wait for them, and exit with their status.
@@ -493,50 +556,53 @@ def main():
         dist.destroy_process_group()
 
 
-def run(vdb, args, device, rank, world):
-    if args.data == "mixture":
-        args.centers = mixture_centers(vdb, args.mix_components or args.nlist, args.mix_group or args.nprobe,
-                                       args.dim, args.mix_spread, device)
-    if args.sharded_build:
-        shards = world if world > 1 else max(args.emulate_shard, 1)
-        idx, build_info = build_index_sharded(vdb, args, device, rank if world > 1 else 0, shards)
-    else:
-        idx, build_info = build_index(vdb, args, device, rank, world)
-    for o in args.opt:
-        name, val = o.split("=", 1)
-        idx.set_option(name, int(val))
-    if args.prewarm:  # list-cache tier: load every list up front, in list order (vdb.QueryService/Warmup)
-        idx.warmup_lists(list(range(args.nlist)))
-    if args.emulate_shard > 1 and world == 1 and not args.sharded_build:
-        idx.set_shard(0, args.emulate_shard)
-    B, k = args.batch, args.k
-    nq = (args.warmup + args.steps + args.prof_steps) * B
-    main_stream = torch.cuda.current_stream()
-    queries = torch.empty((nq, args.dim), dtype=torch.float32, device=device)
-    fill_rows(vdb, args, queries, 0, nq, 12346, main_stream.cuda_stream)
-    out_d = torch.empty((nq, k), dtype=torch.float32, device=device)
-    out_i = torch.empty((nq, k), dtype=torch.int64, device=device)
-    check = None
-    if world > 1 and not args.sharded_build:
-        # Reference for the end-to-end check: the whole (unsharded) index answers the
-        # first timed batches on this rank before it keeps only its LPT shard.
-        nchk = min(args.check_batches, args.steps) * B
-        q0 = args.warmup * B
-        chk_d = torch.empty((nchk, k), dtype=torch.float32, device=device)
-        chk_i = torch.empty((nchk, k), dtype=torch.int64, device=device)
-        for b0 in range(0, nchk, B):
-            idx.search_device(queries[q0 + b0:].data_ptr(), B, args.nprobe, k, chk_d[b0:].data_ptr(),
-                              chk_i[b0:].data_ptr(), main_stream.cuda_stream)
+def device_wait(args, world, idx, streams, rank):
+    """Wait for `streams` (torch.cuda.synchronize semantics). With the engine's own
+    communicator a stalled peer must not hang the run: the engine's watchdog marks an
+    exchange that misses comm_timeout_ms failed, and this rank then prints the error naming
+    itself and exits non-zero (the driver's launcher tears the other ranks down)."""
+    if world == 1 or args.exchange != "engine" or idx is None:
         torch.cuda.synchronize()
-        check = (q0, nchk, chk_d, chk_i)
-        idx.set_shard(rank, world)
-    if world > 1 and args.exchange == "engine":
-        # the engine's own communicator: rank 0 draws the RCCL id, the others receive it
-        cid = torch.zeros(vdb.COMM_ID_BYTES, dtype=torch.uint8)
-        if rank == 0:
-            cid.copy_(torch.frombuffer(bytearray(vdb.comm_unique_id()), dtype=torch.uint8))
-        dist.broadcast(cid, src=0)
+        return
+    evs = []
+    for st in streams:
+        e = torch.cuda.Event()
+        e.record(st)
+        evs.append(e)
+    while not all(e.query() for e in evs):
+        err, issued, done = idx.comm_status()
+        if err:
+            print(json.dumps({"error": err, "rank": rank, "exchanges_issued": issued, "exchanges_done": done}),
+                  flush=True)
+            print(f"[bench] rank {rank}: {err}", file=sys.stderr, flush=True)
+            os._exit(3)  # (no teardown: the stalled collective is still queued on the device)
+        time.sleep(0.001)
+    torch.cuda.synchronize()
+
+
+def attach_engine_comm(vdb, idx, args, rank, world):
+    """The engine's own communicator: rank 0 draws the RCCL id, the others receive it over
+    the control group; init is non-blocking with a deadline (option comm_timeout_ms)."""
+    idx.set_option("comm_timeout_ms", int(args.comm_timeout * 1000))
+    cid = torch.zeros(vdb.COMM_ID_BYTES, dtype=torch.uint8)
+    if rank == 0:
+        cid.copy_(torch.frombuffer(bytearray(vdb.comm_unique_id()), dtype=torch.uint8))
+    dist.broadcast(cid, src=0)
+    try:
         idx.attach_comm(bytes(cid.numpy().tobytes()), rank, world)
+    except Exception as e:  # noqa: BLE001 — report which rank failed, exit non-zero
+        print(json.dumps({"error": str(e), "rank": rank}), flush=True)
+        print(f"[bench] rank {rank}: attach_comm failed: {e}", file=sys.stderr, flush=True)
+        os._exit(3)
+
+
+def timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, check=None):
+    """W warm-up steps, then exactly K timed steps with `inflight` batches in flight,
+    bracketed by barrier + synchronize, max over ranks; then the roofline pass: the same
+    steps one at a time on one stream, so the engine's per-batch events time each scan
+    launch on its own (and give the latency of a batch with nothing else in flight)."""
+    B, k = args.batch, args.k
+    main_stream = torch.cuda.current_stream()
     # Batches in flight: step s runs on streams[s % inflight]; the engine gives each
     # concurrent search its own workspace slot, so one batch's small kernels and scan
     # tail overlap the next batch's scan. Rank partials and gathers are per stream.
@@ -548,6 +614,7 @@ def run(vdb, args, device, rank, world):
     part = [torch.empty(rec, dtype=torch.uint8, device=device) for _ in streams]
     gat = [torch.empty(world * rec, dtype=torch.uint8, device=device) for _ in streams]
     torch.cuda.synchronize()
+    ctrl = device if args.ctrl_dev == "cuda" else "cpu"
 
     def step(s, slot):
         st = streams[slot]
@@ -570,7 +637,7 @@ def run(vdb, args, device, rank, world):
 
     for s in range(args.warmup):
         step(s, s % len(streams))
-    torch.cuda.synchronize()
+    device_wait(args, world, idx, streams, rank)
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
@@ -582,7 +649,7 @@ def run(vdb, args, device, rank, world):
         starts[j].record(streams[slot])
         step(args.warmup + j, slot)
         ends[j].record(streams[slot])
-    torch.cuda.synchronize()
+    device_wait(args, world, idx, streams, rank)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -591,20 +658,17 @@ def run(vdb, args, device, rank, world):
         q0, nchk, chk_d, chk_i = check
         same = bool(torch.equal(out_i[q0:q0 + nchk], chk_i) and
                     torch.equal(out_d[q0:q0 + nchk].view(torch.int32), chk_d.view(torch.int32)))
-        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=device if args.ctrl_dev == "cuda" else "cpu")
+        flag = torch.tensor([1 if same else 0], dtype=torch.int32, device=ctrl)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         parity_multi = bool(int(flag.item()) == 1)
     lat = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     p99 = percentile(lat, 0.99)
     if world > 1:
-        t = torch.tensor([elapsed, p99], dtype=torch.float64, device=device if args.ctrl_dev == "cuda" else "cpu")
+        t = torch.tensor([elapsed, p99], dtype=torch.float64, device=ctrl)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, p99 = float(t[0]), float(t[1])
 
-    # Roofline pass (untimed for `value`): the same steps one at a time on one stream,
-    # so the engine's per-batch events time each scan launch on its own.
-    # Its per-step events also give the latency of a batch with nothing else in flight.
-    torch.cuda.synchronize()
+    device_wait(args, world, idx, streams, rank)
     idx.profile_enable(True)
     idx.profile_reset()
     s_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.prof_steps)]
@@ -613,35 +677,163 @@ def run(vdb, args, device, rank, world):
         s_ev[j].record(streams[0])
         step(args.warmup + args.steps + j, 0)
         e_ev[j].record(streams[0])
-    torch.cuda.synchronize()
+    device_wait(args, world, idx, streams, rank)
     prof = idx.profile_read()
     idx.profile_enable(False)
-    p99_single = percentile([a.elapsed_time(b) for a, b in zip(s_ev, e_ev)], 0.99)
+    step_ms_single = [a.elapsed_time(b) for a, b in zip(s_ev, e_ev)]
+    p99_single = percentile(step_ms_single, 0.99)
+    mine = rank_breakdown(rank, prof, elapsed * 1e3 / max(args.steps, 1), step_ms_single)
+    per_rank = None
     if world > 1:
-        t = torch.tensor([p99_single], dtype=torch.float64, device=device if args.ctrl_dev == "cuda" else "cpu")
+        t = torch.tensor([p99_single], dtype=torch.float64, device=ctrl)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         p99_single = float(t[0])
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    return {"elapsed": elapsed, "p99": p99, "p99_single": p99_single, "prof": prof, "parity_multi": parity_multi,
+            "per_rank": per_rank, "mine": mine}
+
+
+def rank_breakdown(rank, prof, ms_per_step, step_ms_single):
+    """One rank's per-batch phases from the engine's HIP events (roofline pass, one batch
+    in flight): scan, the merges after it, and at N>1 the exchange (this rank's record
+    ready -> all-gather done: the wait for the slowest rank plus the collective) and the
+    rank merge."""
+    n = max(prof["scan_launches"], 1)
+    x = max(prof.get("exchanges", 0), 1)
+    return {"rank": rank, "scan_ms": round(prof["scan_ms"] / n, 4),
+            "coarse_ms": round(prof["coarse_ms"] / n, 4),
+            "local_merge_ms": round(prof.get("local_merge_ms", 0.0) / n, 4),
+            "search_ms": round(prof["total_ms"] / n, 4),
+            "exchange_wait_ms": round(prof.get("exchange_ms", 0.0) / x, 4) if prof.get("exchanges") else None,
+            "rank_merge_ms": round(prof.get("rank_merge_ms", 0.0) / x, 4) if prof.get("exchanges") else None,
+            "step_ms_one_in_flight": round(sum(step_ms_single) / max(len(step_ms_single), 1), 4),
+            "ms_per_step": round(ms_per_step, 4),
+            "scan_bytes_per_batch": int(prof["scan_bytes"] / max(prof["batches"], 1)),
+            "distinct_lists_per_batch": round(prof["distinct_lists"] / max(prof["batches"], 1), 1)}
+
+
+def balance(per_rank):
+    """max / min over ranks of the per-rank phases (1.0 = perfectly balanced shards)."""
+    out = {}
+    for key in ("scan_ms", "search_ms", "ms_per_step", "scan_bytes_per_batch"):
+        v = [r[key] for r in per_rank if r and r.get(key)]
+        if v:
+            out[key] = {"max": max(v), "min": min(v), "max_over_min": round(max(v) / min(v), 4),
+                        "argmax_rank": per_rank[[r[key] if r else None for r in per_rank].index(max(v))]["rank"]}
+    return out
+
+
+def make_queries(vdb, args, device):
+    B, k = args.batch, args.k
+    nq = (args.warmup + args.steps + args.prof_steps) * B
+    queries = torch.empty((nq, args.dim), dtype=torch.float32, device=device)
+    fill_rows(vdb, args, queries, 0, nq, 12346, torch.cuda.current_stream().cuda_stream)
+    out_d = torch.empty((nq, k), dtype=torch.float32, device=device)
+    out_i = torch.empty((nq, k), dtype=torch.int64, device=device)
+    return queries, out_d, out_i
+
+
+def run_emulated_ranks(vdb, args, device):
+    """--emulate-rank all: the per-GPU work of every rank of a W-GPU node, timed in turn on
+    this one GPU. One sharded-build assignment pass; then for each rank r a fresh index
+    holding exactly rank r's LPT lists (plan_shard + append), the same K timed steps of its
+    partial search, and its per-batch phases; the line reports every rank and the
+    max/min balance (the 8-GPU step is the max over ranks). Partial results only: a
+    diagnostic line, not the bench line."""
+    W = args.emulate_shard
+    trained, asg, sizes, info = sharded_assign(vdb, args, device, 0)
+    centroids = trained.centroids
+    trained.close()
+    queries, out_d, out_i = make_queries(vdb, args, device)
+    ranks = []
+    for r in range(W):
+        idx = new_index(vdb, args, device)
+        idx.centroids = centroids
+        binfo = sharded_append(vdb, args, device, idx, asg, sizes, r, W)
+        for o in args.opt:
+            name, val = o.split("=", 1)
+            idx.set_option(name, int(val))
+        res = timed_region(vdb, idx, args, device, 0, 1, queries, out_d, out_i)
+        row = dict(res["mine"], rank=r, qps=round(args.steps * args.batch / res["elapsed"], 1),
+                   p99_ms=round(res["p99"], 4), p99_ms_one_in_flight=round(res["p99_single"], 4),
+                   shard_gib=round(idx.gpu_bytes_allocated() / 2**30, 2), append_s=binfo["append_s"])
+        log(0, f"[bench] emulated rank {r}/{W}: " + json.dumps(row))
+        ranks.append(row)
+        idx.close()
+        torch.cuda.empty_cache()
+    plan = vdb.shard_plan(sizes, W)
+    lists = [int((plan == r).sum()) for r in range(W)]
+    vecs = [int(sizes[plan == r].sum()) for r in range(W)]
+    return {
+        "metric": f"per-rank balance of the {W}-GPU LPT shard plan (emulated on one GPU)",
+        "unit": "ms", "n_gpus": 1, "emulated_ranks": W, "steps": args.steps, "warmup": args.warmup,
+        "config": {"workload": f"{args.nvec // 1_000_000}M x {args.dim}D IVF-Flat L2, nlist {args.nlist}, "
+                               f"nprobe {args.nprobe}, batch {args.batch}, k {args.k}",
+                   "inflight": args.inflight, "data": args.data},
+        "ranks": ranks, "balance": balance(ranks),
+        "shard_lists": lists, "shard_vectors": vecs,
+        "predicted_8gpu_qps_from_max_rank_step": round(args.batch * 1e3 / max(r["ms_per_step"] for r in ranks), 1),
+        "build": info, "note": "partial (per-rank) results; exchange excluded; each rank's search timed alone",
+    }
+
+
+def run(vdb, args, device, rank, world):
+    if args.data == "mixture":
+        args.centers = mixture_centers(vdb, args.mix_components or args.nlist, args.mix_group or args.nprobe,
+                                       args.dim, args.mix_spread, device)
+    if args.emulate_rank == "all":
+        line = run_emulated_ranks(vdb, args, device)
+        print(json.dumps(line), flush=True)
+        return
+    er = int(args.emulate_rank)
+    if args.sharded_build:
+        shards = world if world > 1 else max(args.emulate_shard, 1)
+        idx, build_info = build_index_sharded(vdb, args, device, rank if world > 1 else er, shards)
+    else:
+        idx, build_info = build_index(vdb, args, device, rank, world)
+    for o in args.opt:
+        name, val = o.split("=", 1)
+        idx.set_option(name, int(val))
+    if args.prewarm:  # list-cache tier: load every list up front, in list order (vdb.QueryService/Warmup)
+        idx.warmup_lists(list(range(args.nlist)))
+    if args.emulate_shard > 1 and world == 1 and not args.sharded_build:
+        idx.set_shard(er, args.emulate_shard)
+    B, k = args.batch, args.k
+    queries, out_d, out_i = make_queries(vdb, args, device)
+    main_stream = torch.cuda.current_stream()
+    check = None
+    if world > 1 and not args.sharded_build:
+        # Reference for the end-to-end check: the whole (unsharded) index answers the
+        # first timed batches on this rank before it keeps only its LPT shard.
+        nchk = min(args.check_batches, args.steps) * B
+        q0 = args.warmup * B
+        chk_d = torch.empty((nchk, k), dtype=torch.float32, device=device)
+        chk_i = torch.empty((nchk, k), dtype=torch.int64, device=device)
+        for b0 in range(0, nchk, B):
+            idx.search_device(queries[q0 + b0:].data_ptr(), B, args.nprobe, k, chk_d[b0:].data_ptr(),
+                              chk_i[b0:].data_ptr(), main_stream.cuda_stream)
+        torch.cuda.synchronize()
+        check = (q0, nchk, chk_d, chk_i)
+        idx.set_shard(rank, world)
+    if world > 1 and args.exchange == "engine":
+        attach_engine_comm(vdb, idx, args, rank, world)
+    res = timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, check)
+    elapsed, p99, p99_single, prof = res["elapsed"], res["p99"], res["p99_single"], res["prof"]
+    parity_multi = res["parity_multi"]
 
     launches = max(prof["scan_launches"], 1)
     scan_ms = prof["scan_ms"] / launches
     bytes_per_launch = prof["scan_bytes"] / max(prof["batches"], 1)
     achieved = bytes_per_launch / (scan_ms * 1e-3) / 1e9 if scan_ms > 0 else 0.0
-    traffic = None
-    try:
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        key = f"{args.nvec}x{args.dim}/{args.nlist}/{args.nprobe}/{B}/{k}/N{world}"
-        if args.data != "iid":
-            key += f"/{args.data}"
-        if args.emulate_shard > 1:
-            key += f"/shard0of{args.emulate_shard}"
-        if args.opt:  # knobs can change the traffic (never the results)
-            key += "/" + ",".join(sorted(args.opt))
-        entry = tj.get("workloads", {}).get(key) or (tj if tj.get("workload") == key else None)
-        if entry:
-            traffic = entry.get("hbm_bytes_per_scan_launch")
-    except (OSError, ValueError):
-        pass
+    key = f"{args.nvec}x{args.dim}/{args.nlist}/{args.nprobe}/{B}/{k}/N{world}"
+    if args.data != "iid":
+        key += f"/{args.data}"
+    if args.emulate_shard > 1:
+        key += f"/shard{er}of{args.emulate_shard}"
+    if args.opt:  # knobs can change the traffic (never the results)
+        key += "/" + ",".join(sorted(args.opt))
+    traffic, traffic_note = lookup_traffic(args.traffic_json, key, vdb.build_id())
 
     result = {
         "metric": METRIC,
@@ -681,6 +873,7 @@ def run(vdb, args, device, rank, world):
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_note,
             "algorithmic_bytes_per_launch": int(bytes_per_launch),
             "scan_ms_per_launch": round(scan_ms, 4),
             "coarse_ms_per_batch": round(prof["coarse_ms"] / launches, 4),
@@ -696,9 +889,12 @@ def run(vdb, args, device, rank, world):
         "engine_options": dict(o.split("=", 1) for o in args.opt),
         **({"rehearsal": f"{world} ranks on {torch.cuda.device_count()} GPU(s), host-staged exchange: "
                          "protocol check, not a scaling number"} if args.rehearsal else {}),
-        **({"emulated_shard": f"rank 0 of {args.emulate_shard} (partial results; diagnostic, not a bench line)"}
+        **({"emulated_shard": f"rank {er} of {args.emulate_shard} (partial results; diagnostic, not a bench line)"}
            if args.emulate_shard > 1 else {}),
     }
+    if res["per_rank"]:
+        result["per_rank"] = res["per_rank"]
+        result["rank_balance"] = balance(res["per_rank"])
     if parity_multi is not None:
         result["parity_vs_single_gpu"] = {"batches": min(args.check_batches, args.steps), "bit_identical": parity_multi}
     if args.host_api and world == 1:
@@ -708,7 +904,7 @@ def run(vdb, args, device, rank, world):
         result["cpu_baseline"] = cpu_baseline(vdb, idx, args, qh, args.cpu_budget)
     if world == 1 and args.emulate_shard > 1 and args.shard_check > 0:
         qh = queries[: args.shard_check].cpu().numpy()
-        result["shard_parity"] = shard_parity(vdb, idx, args, qh, 0, args.emulate_shard)
+        result["shard_parity"] = shard_parity(vdb, idx, args, qh, er, args.emulate_shard)
     if args.tier_cache_gib > 0 and world == 1:  # (last: it releases the HBM-resident index)
         tq = torch.empty((args.tier_call * args.tier_calls, args.dim), dtype=torch.float32, device=device)
         fill_rows(vdb, args, tq, 1 << 40, tq.shape[0], 12346, torch.cuda.current_stream().cuda_stream)

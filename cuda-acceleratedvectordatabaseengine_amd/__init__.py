@@ -64,7 +64,8 @@ class Profile(ctypes.Structure):
                 ("distinct_lists", ctypes.c_uint64), ("work_items", ctypes.c_uint64),
                 ("scan_bytes", ctypes.c_uint64), ("pair_vectors", ctypes.c_uint64),
                 ("exact_reranks", ctypes.c_uint64), ("bounded_blocks", ctypes.c_uint64),
-                ("computed_vectors", ctypes.c_uint64)]
+                ("computed_vectors", ctypes.c_uint64), ("local_merge_ms", ctypes.c_double),
+                ("exchanges", ctypes.c_uint64), ("exchange_ms", ctypes.c_double), ("rank_merge_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -94,6 +95,7 @@ def lib() -> ctypes.CDLL:
     sigs = {
         "vdb_last_error": (ctypes.c_char_p, []),
         "vdb_version": (ctypes.c_char_p, []),
+        "vdb_build_id": (ctypes.c_char_p, []),
         "vdb_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
         "vdb_ivf_create": (ctypes.c_int, [ctypes.POINTER(_Config), ctypes.POINTER(vp)]),
         "vdb_ivf_destroy": (ctypes.c_int, [vp]),
@@ -139,6 +141,7 @@ def lib() -> ctypes.CDLL:
         "vdb_comm_unique_id": (ctypes.c_int, [vp]),
         "vdb_ivf_attach_comm": (ctypes.c_int, [vp, vp, u32, u32]),
         "vdb_ivf_detach_comm": (ctypes.c_int, [vp]),
+        "vdb_ivf_comm_status": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "vdb_ivf_create_group": (ctypes.c_int, [ctypes.POINTER(_Config), vp, u32, ctypes.POINTER(vp)]),
         "vdb_ivf_group_size": (u32, [vp]),
         "vdb_ivf_list_owners": (ctypes.c_int, [vp, vp]),
@@ -158,6 +161,11 @@ def _check(rc: int):
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def build_id() -> str:
+    """Hash of the sources behind the scan kernels of the loaded library (vdb_build_id)."""
+    return lib().vdb_build_id().decode()
 
 
 def device_count() -> int:
@@ -354,6 +362,13 @@ class IVFFlatIndex:
     def detach_comm(self):
         _check(lib().vdb_ivf_detach_comm(self._h))
 
+    def comm_status(self):
+        """(error message or None, exchanges issued, exchanges completed) of the attached
+        communicator (vdb_ivf_comm_status)."""
+        a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        rc = lib().vdb_ivf_comm_status(self._h, ctypes.byref(a), ctypes.byref(b))
+        return (lib().vdb_last_error().decode() if rc != 0 else None), a.value, b.value
+
     @property
     def group_size(self) -> int:
         return int(lib().vdb_ivf_group_size(self._h))
@@ -419,7 +434,7 @@ class IVFFlatIndex:
         _check(lib().vdb_ivf_set_coarse_mode(self._h, mode))
 
     def set_option(self, name: str, value: int):
-        """Engine tuning knob (vdb_ivf_set_option); never changes results."""
+        """Engine option (vdb_ivf_set_option): tuning knobs and residency; never changes results."""
         _check(lib().vdb_ivf_set_option(self._h, name.encode(), int(value)))
 
     def coalesce_stats(self):

@@ -25,6 +25,10 @@ extern "C" {
 
 const char* vdb_last_error(void) { return g_last_error.c_str(); }
 const char* vdb_version(void) { return "vdb_ivf 0.1.0 (gfx950)"; }
+#ifndef VDB_BUILD_ID
+#define VDB_BUILD_ID "unknown"
+#endif
+const char* vdb_build_id(void) { return VDB_BUILD_ID; }
 
 int vdb_device_count(int* count) {
     return guarded([&] {
@@ -50,7 +54,7 @@ int vdb_ivf_create(const vdb_ivf_config* cfg, vdb_ivf** out) {
             h->dp = h->d4 * 4;
             h->metric = cfg->metric;
             h->device = cfg->device;
-            h->max_gpu_memory = cfg->max_gpu_memory;
+            h->max_gpu_memory = cfg->max_gpu_memory == ~0ull ? 0 : cfg->max_gpu_memory;  // 0: no cap
             h->set_device();
             HIPCHECK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
             for (auto& sl : h->slots) {
@@ -215,6 +219,9 @@ int vdb_ivf_plan_shard(vdb_ivf* h, uint32_t rank, uint32_t world, const uint64_t
 
 // Index file: "VDBIVF01", u32 dim, u32 nlist, i32 metric, u32 reserved, centroids
 // f32[nlist][dim], then per list: u64 count, u64 ids[count], f32 vectors[count][dim].
+// Shard file: "VDBIVS01", u32 dim, u32 nlist, i32 metric, u32 rank, u32 world, u32 reserved,
+// centroids, then per list: u64 count (global), u64 stored (count if the rank owns the
+// list, else 0), u64 ids[stored], f32 vectors[stored][dim].
 int vdb_ivf_save(vdb_ivf* h, const char* path) {
     return guarded([&] {
         require(h && path, "null argument");
@@ -222,8 +229,11 @@ int vdb_ivf_save(vdb_ivf* h, const char* path) {
         // disagree with the rows written.
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
-        require(h->is_group() || h->world == 1, "save a sharded handle from every rank's full copy instead",
-                VDB_ERR_STATE);
+        // A sharded handle (set_shard / plan_shard, world > 1) writes a shard file: every
+        // list's global count (emptiness semantics) but only its own lists' rows, served
+        // later by vdb_ivf_open_lists on that rank (configs[4]: each rank's lists on its
+        // own NVMe). A group or an unsharded handle writes the whole index.
+        const bool shard_file = !h->is_group() && h->world > 1;
         if (h->file_home()) {  // fopen("wb") would truncate the file the lists are served from
             struct stat a, b;
             if (::stat(path, &a) == 0 && ::fstat(h->home_fd, &b) == 0)
@@ -239,9 +249,15 @@ int vdb_ivf_save(vdb_ivf* h, const char* path) {
             if (b && std::fwrite(p, 1, b, f) != b) throw VdbError(VDB_ERR_STATE, "short write");
         };
         try {
-            const uint32_t hdr[4] = {h->dim, h->nlist, (uint32_t)h->metric, 0};
-            put("VDBIVF01", 8);
-            put(hdr, sizeof(hdr));
+            if (shard_file) {
+                const uint32_t hdr[6] = {h->dim, h->nlist, (uint32_t)h->metric, h->rank, h->world, 0};
+                put("VDBIVS01", 8);
+                put(hdr, sizeof(hdr));
+            } else {
+                const uint32_t hdr[4] = {h->dim, h->nlist, (uint32_t)h->metric, 0};
+                put("VDBIVF01", 8);
+                put(hdr, sizeof(hdr));
+            }
             std::vector<float> c((size_t)h->nlist * h->dim);
             h->head()->set_device();
             h->head()->export_centroids(c.data());
@@ -250,13 +266,15 @@ int vdb_ivf_save(vdb_ivf* h, const char* path) {
             std::vector<uint64_t> ids;
             for (uint32_t l = 0; l < h->nlist; ++l) {
                 const uint64_t cnt = h->count[l];
-                v.resize(cnt * h->dim);
-                ids.resize(cnt);
+                const uint64_t stored = shard_file && !h->owned[l] ? 0 : cnt;
+                v.resize(stored * h->dim);
+                ids.resize(stored);
                 vdb_ivf* st = h->store_of(l);  // (a group: the member storing the list)
                 st->set_device();
-                st->export_list(l, v.data(), ids.data());
+                if (stored) st->export_list(l, v.data(), ids.data());
                 put(&cnt, 8);
-                put(ids.data(), cnt * 8);
+                if (shard_file) put(&stored, 8);
+                put(ids.data(), stored * 8);
                 put(v.data(), v.size() * 4);
             }
         } catch (...) {
@@ -294,6 +312,10 @@ int vdb_ivf_load(vdb_ivf* h, const char* path) {
         uint32_t hdr[4];
         get(magic, 8);
         get(hdr, sizeof(hdr));
+        if (std::memcmp(magic, "VDBIVS01", 8) == 0) {
+            std::fclose(f);
+            throw VdbError(VDB_ERR_INVALID_ARGUMENT, "a shard file holds one rank's lists: serve it with open_lists");
+        }
         if (std::memcmp(magic, "VDBIVF01", 8) != 0 || hdr[0] != h->dim || hdr[1] != h->nlist ||
             (int)hdr[2] != h->metric) {
             std::fclose(f);
@@ -343,7 +365,11 @@ int vdb_ivf_search(vdb_ivf* h, const float* q, uint32_t n, uint32_t nprobe, uint
         require(h && ((q && dist && ids) || n == 0 || k == 0), "null argument");
         if (n == 0 || k == 0) return;
         require(k <= (uint32_t)vdbk::kMaxK, "k above 1024 is not supported", VDB_ERR_UNSUPPORTED);
-        if (h->coalesce) {
+        // With a communicator of world > 1 every rank must issue the same collectives in the
+        // same order; the coalescer's grouping of concurrent callers depends on timing, so
+        // such a handle serves calls one at a time, in the order they take the lock.
+        const bool ranked = h->comm && h->comm_world > 1;
+        if (h->coalesce && !ranked) {
             h->search_coalesced(q, n, nprobe, k, dist, ids);  // concurrent callers share device batches
         } else {
             std::lock_guard<std::mutex> g(h->mu);
@@ -429,12 +455,17 @@ int vdb_ivf_warmup(vdb_ivf* h, const uint32_t* lists, uint32_t n) {
         for (uint32_t i = 0; i < n; ++i) require(lists[i] < h->nlist, "list id out of range");
         // Without the list-cache tier every list is already HBM-resident. In the tier,
         // each list is loaded like load_list_to_gpu (ivf_flat_index.cpp:387-444): one
-        // that cannot fit the cache is skipped (the reference returns false).
+        // that cannot fit the cache is skipped (the reference returns false). A group
+        // loads each list on the member storing it.
         std::lock_guard<std::mutex> g(h->mu);
-        if (h->is_group() || !h->tiered()) return;  // (a group keeps every list HBM-resident)
+        for (uint32_t i = 0; i < n; ++i) {
+            vdb_ivf* st = h->store_of(lists[i]);
+            if (!st->tiered()) continue;
+            st->set_device();
+            (void)st->make_resident(lists + i, 1, st->stream);
+            HIPCHECK(hipStreamSynchronize(st->stream));
+        }
         h->set_device();
-        for (uint32_t i = 0; i < n; ++i) (void)h->make_resident(lists + i, 1, h->stream);
-        HIPCHECK(hipStreamSynchronize(h->stream));
     });
 }
 
@@ -444,10 +475,12 @@ int vdb_ivf_evict(vdb_ivf* h, uint32_t list) {
         // Without the tier residency is permanent and eviction is a no-op; in the tier
         // the list leaves the cache (evict_list_from_gpu, ivf_flat_index.cpp:447-471).
         std::lock_guard<std::mutex> g(h->mu);
-        if (h->is_group() || !h->tiered() || h->cache_off[list] == vdb_ivf::kAbsent) return;
+        vdb_ivf* st = h->store_of(list);
+        if (!st->tiered() || st->cache_off[list] == vdb_ivf::kAbsent) return;
+        st->set_device();
+        st->quiesce();
+        st->cache_free(list);
         h->set_device();
-        h->quiesce();
-        h->cache_free(list);
     });
 }
 
@@ -564,8 +597,17 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             require(value >= 0, "list_cache_bytes out of range");
             h->set_device();
             h->set_list_cache((uint64_t)value);
-        } else if (n == "diag") {
-            h->diag = (uint32_t)value;  // timing experiments only: results are invalid when non-zero
+            h->max_gpu_memory = 0;  // explicit residency control replaces the Config cap
+        } else if (n == "max_gpu_memory") {
+            require(value >= 0, "max_gpu_memory out of range");
+            h->set_device();
+            h->max_gpu_memory = (uint64_t)value;
+            h->apply_memory_cap(h->count);
+        } else if (n == "bounded_stats") {
+            h->bounded_stats = value != 0;  // statistics only: results never change
+        } else if (n == "comm_timeout_ms") {
+            require(value > 0 && value < (1ll << 31), "comm_timeout_ms out of range");
+            h->comm_timeout_ms = (uint32_t)value;
         } else if (n == "batch") {
             require(value > 0 && value < (1ll << 31), "batch out of range");
             h->batch = (uint32_t)value;
@@ -581,20 +623,27 @@ int vdb_ivf_cache_stats(vdb_ivf* h, vdb_ivf_cache_stats_t* out) {
     return guarded([&] {
         require(h && out, "null argument");
         std::lock_guard<std::mutex> g(h->mu);
-        out->capacity_bytes = h->cache_blocks * vdb_ivf::block_bytes(h->dp);
-        out->resident_bytes = h->cache_used * vdb_ivf::block_bytes(h->dp);
-        out->loads = h->cache_loads;
-        out->evictions = h->cache_evictions;
-        out->bytes_loaded = h->cache_bytes_in;
-        uint64_t n = 0;
-        for (uint32_t l = 0; l < h->nlist && h->tiered(); ++l) n += h->cache_off[l] != vdb_ivf::kAbsent;
-        out->resident_lists = n;
-        out->file_bytes_read = h->file_bytes_read;
-        out->subbatches = h->tier_subbatches;
-        out->prefetches = h->tier_prefetches;
-        out->sync_loads = h->tier_sync_loads;
-        out->io_uring = h->uring && h->uring->uring() ? 1 : 0;
-        out->o_direct = h->home_fd_direct >= 0 ? 1 : 0;
+        *out = vdb_ivf_cache_stats_t{};
+        // (a group: the sums over its members' caches)
+        std::vector<vdb_ivf*> hs;
+        if (h->is_group())
+            for (auto& mb : h->members) hs.push_back(mb.get());
+        else
+            hs.push_back(h);
+        for (vdb_ivf* m : hs) {
+            out->capacity_bytes += m->cache_blocks * vdb_ivf::block_bytes(m->dp);
+            out->resident_bytes += m->cache_used * vdb_ivf::block_bytes(m->dp);
+            out->loads += m->cache_loads;
+            out->evictions += m->cache_evictions;
+            out->bytes_loaded += m->cache_bytes_in;
+            for (uint32_t l = 0; l < m->nlist && m->tiered(); ++l) out->resident_lists += m->cache_off[l] != vdb_ivf::kAbsent;
+            out->file_bytes_read += m->file_bytes_read;
+            out->subbatches += m->tier_subbatches;
+            out->prefetches += m->tier_prefetches;
+            out->sync_loads += m->tier_sync_loads;
+            out->io_uring |= m->uring && m->uring->uring() ? 1 : 0;
+            out->o_direct |= m->home_fd_direct >= 0 ? 1 : 0;
+        }
     });
 }
 
@@ -665,14 +714,24 @@ int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
         vdb_ivf_profile p{};
         for (size_t i = 0; i < h->events_used; ++i) {
             const EventSet& e = h->events[i];
-            float a = 0, b = 0, c = 0;
+            float a = 0, b = 0, c = 0, m = 0;
             HIPCHECK(hipEventElapsedTime(&a, e.scan_begin, e.scan_end));
             HIPCHECK(hipEventElapsedTime(&b, e.begin, e.coarse_end));
             HIPCHECK(hipEventElapsedTime(&c, e.begin, e.end));
+            HIPCHECK(hipEventElapsedTime(&m, e.scan_end, e.end));
             p.scan_ms += a;
             p.coarse_ms += b;
             p.total_ms += c;
+            p.local_merge_ms += m;
             p.scan_launches++;
+            if (e.xchg) {  // (the exchange of a batch, or of the whole call in the tier)
+                float x = 0, r = 0;
+                HIPCHECK(hipEventElapsedTime(&x, e.end, e.x_end));
+                HIPCHECK(hipEventElapsedTime(&r, e.x_end, e.m_end));
+                p.exchange_ms += x;
+                p.rank_merge_ms += r;
+                p.exchanges++;
+            }
         }
         unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (h->stats.p) HIPCHECK(hipMemcpy(st, h->stats.p, 64, hipMemcpyDeviceToHost));

@@ -185,6 +185,8 @@ inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 struct EventSet {
     hipEvent_t begin, coarse_end, scan_begin, scan_end, end;
+    hipEvent_t x_end, m_end;  // multi-GPU: the all-gather done (comm stream), the rank merge done
+    bool xchg = false;        // this batch (or call) ended in an exchange
 };
 
 // One host-API search() call waiting in the coalescing queue.
@@ -269,7 +271,7 @@ struct vdb_ivf {
     uint32_t wide_stride = 1;  // wide-item dispatch permutation (1 = plan order; measured best)
     uint32_t seg_blocks = 8;  // current segment size (blocks of 64 vectors; upload_directory sets it)
     uint32_t seg_blocks_opt = 0;                // 0 = automatic (upload_directory)
-    uint32_t diag = 0;                          // scan diagnostics (results invalid when set, but 16)
+    bool bounded_stats = false;                 // count the bounded scan's re-ranks and blocks (profile_read)
     // wide items of at least this many queries are bounded on the matrix cores and
     // re-ranked exactly (ivf_scan_bounded); 0 = never. Off by default: on the bench
     // workloads the exact re-ranks (per-list top-k insertions, ~5% of pairs, each a
@@ -426,17 +428,24 @@ struct vdb_ivf {
 
     ~vdb_ivf() {
         stop_coalescer();
+        // An exchange that missed its deadline never completes: nothing is waited for and
+        // the communicator is left to the process's exit (destroying or aborting it could
+        // hang, or free what a still-queued collective reads).
+        const bool failed = comm_failed();
+        stop_watch();
         members.clear();  // each member waits for and frees its own device work
         (void)hipSetDevice(device);
-        try {
-            quiesce();  // pooled buffers are freed stream-ordered: no search may still read them
-        } catch (...) {
+        if (!failed) {
+            try {
+                quiesce();  // pooled buffers are freed stream-ordered: no search may still read them
+            } catch (...) {
+            }
+            if (stream) (void)hipStreamSynchronize(stream);
+            for (auto& sl : slots)
+                if (sl.gstream) (void)hipStreamSynchronize(sl.gstream);
         }
-        if (stream) (void)hipStreamSynchronize(stream);
-        for (auto& sl : slots)
-            if (sl.gstream) (void)hipStreamSynchronize(sl.gstream);
         if (comm) {
-            if (comm_owned) (void)ncclCommDestroy(comm);
+            if (comm_owned && !failed) (void)ncclCommDestroy(comm);
             comm = nullptr;
         }
         for (auto& e : gev) (void)hipEventDestroy(e);
@@ -448,13 +457,9 @@ struct vdb_ivf {
             if (e) (void)hipEventDestroy(e);
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
         if (home_fd_direct >= 0) ::close(home_fd_direct);
-        for (auto& e : events) {
-            (void)hipEventDestroy(e.begin);
-            (void)hipEventDestroy(e.coarse_end);
-            (void)hipEventDestroy(e.scan_begin);
-            (void)hipEventDestroy(e.scan_end);
-            (void)hipEventDestroy(e.end);
-        }
+        for (auto& e : events)
+            for (hipEvent_t x : {e.begin, e.coarse_end, e.scan_begin, e.scan_end, e.end, e.x_end, e.m_end})
+                (void)hipEventDestroy(x);
         for (auto& sl : slots) {
             if (sl.fork) (void)hipEventDestroy(sl.fork);
             if (sl.join) (void)hipEventDestroy(sl.join);
@@ -990,54 +995,64 @@ struct vdb_ivf {
         };
         size_t next = 0;
         int reading = 0;
-        while (next < chunks.size() || reading > 0) {
-            for (int si = 0; si < kStages && next < chunks.size(); ++si) {
-                Stage& st = stages[si];
-                if (st.reads) continue;
-                if (st.copying) {
-                    const hipError_t q = hipEventQuery(st.copied);
-                    if (q == hipErrorNotReady) continue;
-                    HIPCHECK(q);
-                    st.copying = false;
-                }
-                const Chunk& c = chunks[next++];
-                const uint64_t base = file_off[c.l];
-                st.m = c.m;
-                st.dst_block = c.dst_block;
-                st.ids_delta = read_into(si, st.buf.p, base + c.r0 * 8, c.m * 8, 0);
-                st.vec_delta = read_into(si, st.buf.p + ids_cap, base + count[c.l] * 8 + c.r0 * dim * 4, c.m * dim * 4, 1);
-                st.reads = 2;
-                ++reading;
-                file_bytes_read += c.m * 8 + c.m * dim * 4;
-            }
-            if (reading == 0) {  // every buffer waits for its copies: wait for one
-                for (Stage& st : stages)
+        try {
+            while (next < chunks.size() || reading > 0) {
+                for (int si = 0; si < kStages && next < chunks.size(); ++si) {
+                    Stage& st = stages[si];
+                    if (st.reads) continue;
                     if (st.copying) {
-                        HIPCHECK(hipEventSynchronize(st.copied));
+                        const hipError_t q = hipEventQuery(st.copied);
+                        if (q == hipErrorNotReady) continue;
+                        HIPCHECK(q);
                         st.copying = false;
-                        break;
                     }
-                continue;
+                    const Chunk& c = chunks[next++];
+                    const uint64_t base = file_off[c.l];
+                    st.m = c.m;
+                    st.dst_block = c.dst_block;
+                    st.ids_delta = read_into(si, st.buf.p, base + c.r0 * 8, c.m * 8, 0);
+                    st.vec_delta = read_into(si, st.buf.p + ids_cap, base + count[c.l] * 8 + c.r0 * dim * 4, c.m * dim * 4, 1);
+                    st.reads = 2;
+                    ++reading;
+                    file_bytes_read += c.m * 8 + c.m * dim * 4;
+                }
+                if (reading == 0) {  // every buffer waits for its copies: wait for one
+                    for (Stage& st : stages)
+                        if (st.copying) {
+                            HIPCHECK(hipEventSynchronize(st.copied));
+                            st.copying = false;
+                            break;
+                        }
+                    continue;
+                }
+                for (const UringReader::Done& d : uring->wait(1)) {
+                    Stage& st = stages[d.tag >> 1];
+                    const bool vec = d.tag & 1;
+                    const int64_t want = (int64_t)((vec ? st.vec_delta : st.ids_delta) + st.m * (vec ? (uint64_t)dim * 4 : 8));
+                    require(d.result >= want, "short read from the list file" +
+                                                  (d.result < 0 ? std::string(": ") + std::strerror((int)-d.result) : ""),
+                            VDB_ERR_STATE);
+                    if (--st.reads) continue;
+                    --reading;
+                    HIPCHECK(hipMemcpyAsync(cache_ids.p + st.dst_block * 64, st.buf.p + st.ids_delta, st.m * 8,
+                                            hipMemcpyHostToDevice, s));
+                    HIPCHECK(hipMemcpyAsync(rows_d.p, st.buf.p + ids_cap + st.vec_delta, st.m * dim * 4,
+                                            hipMemcpyHostToDevice, s));
+                    HIPCHECK(hipEventRecord(st.copied, s));
+                    st.copying = true;
+                    vdbk::launch_pad_rows(rows_d.p, st.m, dim, dp, pad_d.p, s);
+                    vdbk::launch_interleave(pad_d.p, st.m, dp, cache.p + st.dst_block * d4 * 64, s);
+                    HIPCHECK(hipGetLastError());
+                }
             }
-            for (const UringReader::Done& d : uring->wait(1)) {
-                Stage& st = stages[d.tag >> 1];
-                const bool vec = d.tag & 1;
-                const int64_t want = (int64_t)((vec ? st.vec_delta : st.ids_delta) + st.m * (vec ? (uint64_t)dim * 4 : 8));
-                require(d.result >= want, "short read from the list file" +
-                                              (d.result < 0 ? std::string(": ") + std::strerror((int)-d.result) : ""),
-                        VDB_ERR_STATE);
-                if (--st.reads) continue;
-                --reading;
-                HIPCHECK(hipMemcpyAsync(cache_ids.p + st.dst_block * 64, st.buf.p + st.ids_delta, st.m * 8,
-                                        hipMemcpyHostToDevice, s));
-                HIPCHECK(hipMemcpyAsync(rows_d.p, st.buf.p + ids_cap + st.vec_delta, st.m * dim * 4,
-                                        hipMemcpyHostToDevice, s));
-                HIPCHECK(hipEventRecord(st.copied, s));
-                st.copying = true;
-                vdbk::launch_pad_rows(rows_d.p, st.m, dim, dp, pad_d.p, s);
-                vdbk::launch_interleave(pad_d.p, st.m, dp, cache.p + st.dst_block * d4 * 64, s);
-                HIPCHECK(hipGetLastError());
-            }
+        } catch (...) {
+            // A failed read (or submission) leaves other reads in flight: reap them and
+            // reset the staging ring, and forget the cache map (the lists planned for this
+            // load may be partly written), so the next load starts clean.
+            uring->drain();
+            for (Stage& st : stages) st.reads = 0;
+            cache_reset();
+            throw;
         }
     }
 
@@ -1053,38 +1068,56 @@ struct vdb_ivf {
         // lists are read with O_DIRECT where the file system allows it (no page-cache copy)
         home_fd_direct = ::open(path, O_RDONLY | O_CLOEXEC | O_DIRECT);
         char magic[8];
-        uint32_t hdr[4];
+        uint32_t hdr[6] = {0, 0, 0, 0, 0, 0};
         pread_all(magic, 8, 0);
-        pread_all(hdr, sizeof(hdr), 8);
-        if (std::memcmp(magic, "VDBIVF01", 8) != 0 || hdr[0] != dim || hdr[1] != nlist || (int)hdr[2] != metric) {
+        const bool shard_file = std::memcmp(magic, "VDBIVS01", 8) == 0;  // (vdb_ivf_save of a sharded handle)
+        pread_all(hdr, shard_file ? 24 : 16, 8);
+        auto refuse = [&](const std::string& why) {
             ::close(home_fd);
             home_fd = -1;
             if (home_fd_direct >= 0) ::close(home_fd_direct);
             home_fd_direct = -1;
-            throw VdbError(VDB_ERR_INVALID_ARGUMENT, "index file does not match this index's configuration");
-        }
+            throw VdbError(VDB_ERR_INVALID_ARGUMENT, why);
+        };
+        if ((!shard_file && std::memcmp(magic, "VDBIVF01", 8) != 0) || hdr[0] != dim || hdr[1] != nlist ||
+            (int)hdr[2] != metric)
+            refuse("index file does not match this index's configuration");
+        if (shard_file && (hdr[4] == 0 || hdr[3] >= hdr[4])) refuse("shard file with an invalid (rank, world)");
+        const uint64_t hdr_bytes = shard_file ? 32 : 24;
         std::vector<float> c((size_t)nlist * dim);
-        pread_all(c.data(), c.size() * 4, 24);
+        pread_all(c.data(), c.size() * 4, hdr_bytes);
+        uint64_t at = hdr_bytes + (uint64_t)c.size() * 4;
+        std::vector<uint64_t> cnt(nlist, 0), stored(nlist, 0), off(nlist, 0);
+        for (uint32_t l = 0; l < nlist; ++l) {
+            uint64_t h2[2] = {0, 0};
+            pread_all(h2, shard_file ? 16 : 8, at);
+            cnt[l] = h2[0];
+            stored[l] = shard_file ? h2[1] : h2[0];
+            off[l] = at + (shard_file ? 16 : 8);
+            at = off[l] + stored[l] * 8 + stored[l] * (uint64_t)dim * 4;
+        }
+        std::vector<uint8_t> own(nlist, 1);
+        if (shard_file) {  // the stored lists must be exactly the rank's LPT lists
+            std::vector<uint32_t> plan(nlist);
+            vdb_shard_plan(cnt.data(), nlist, hdr[4], plan.data());
+            for (uint32_t l = 0; l < nlist; ++l) {
+                own[l] = plan[l] == hdr[3];
+                if (cnt[l] && stored[l] != (own[l] ? cnt[l] : 0)) refuse("shard file lists differ from the LPT plan");
+            }
+        }
         HIPCHECK(hipMemcpy2DAsync(cent_rm.p, dp * 4, c.data(), dim * 4, dim * 4, nlist, hipMemcpyHostToDevice, stream));
         refresh_centroid_layout();
-        uint64_t at = 24 + (uint64_t)c.size() * 4;
-        file_off.assign(nlist, 0);
+        file_off = off;
+        count = cnt;
         total = 0;
-        for (uint32_t l = 0; l < nlist; ++l) {
-            uint64_t cnt = 0;
-            pread_all(&cnt, 8, at);
-            file_off[l] = at + 8;
-            count[l] = cnt;
-            total += cnt;
-            at += 8 + cnt * 8 + cnt * (uint64_t)dim * 4;
-        }
+        for (uint32_t l = 0; l < nlist; ++l) total += cnt[l];
         arena.release();  // no home copy in memory: the file is the home
         arena_ids.release();
         arena_blocks = 0;
         block_off.assign(nlist, 0);
-        owned.assign(nlist, 1);
-        rank = 0;
-        world = 1;
+        owned = own;
+        rank = shard_file ? hdr[3] : 0;
+        world = shard_file ? hdr[4] : 1;
         cache_reset();
         upload_directory();
     }
@@ -1092,7 +1125,6 @@ struct vdb_ivf {
     // Turn the tier on (bytes > 0: HBM cache of that many bytes, arena moved to host
     // memory) or off (arena back in HBM).
     void set_list_cache(uint64_t bytes) {
-        require(bytes == 0 || !comm, "the list-cache tier cannot be combined with a communicator", VDB_ERR_STATE);
         quiesce();
         const uint64_t nb = bytes / block_bytes(dp);
         require(bytes == 0 || nb > 0, "list_cache_bytes is below one block of 64 vectors");
@@ -1108,6 +1140,26 @@ struct vdb_ivf {
         }
         cache_reset();
         upload_directory();
+    }
+
+    // Config::max_gpu_memory: the reference caps the bytes of GPU-resident lists
+    // (count * (dim * 4 + 8) each, gpu_memory_used_) and searches lists beyond the cap on
+    // the CPU (ivf_flat_index.cpp:398-402, 526-530). Here, once the stored lists outgrow
+    // the cap, the handle switches to the list-cache tier with an HBM cache of that many
+    // bytes: lists home in page-locked host memory and the lists a batch probes are made
+    // resident before it scans, so results are unchanged. 0 = no cap.
+    uint64_t stored_list_bytes(const std::vector<uint64_t>& cnt) const {
+        uint64_t b = 0;
+        for (uint32_t l = 0; l < nlist; ++l)
+            if (owned[l]) b += cnt[l] * ((uint64_t)dim * 4 + 8);
+        return b;
+    }
+    void apply_memory_cap(const std::vector<uint64_t>& cnt) {
+        if (max_gpu_memory == 0 || max_gpu_memory == ~0ull || tiered() || file_home()) return;
+        if (stored_list_bytes(cnt) <= max_gpu_memory) return;
+        require(max_gpu_memory >= block_bytes(dp),
+                "max_gpu_memory is below one block of 64 vectors (set 0 for no cap)", VDB_ERR_OUT_OF_MEMORY);
+        set_list_cache(max_gpu_memory);
     }
 
     // Row-major [n][dim] device input -> zero-padded [n][dp] (or the input itself).
@@ -1306,6 +1358,7 @@ struct vdb_ivf {
         std::vector<uint64_t> new_count(count);
         for (uint32_t l = 0; l < nlist; ++l) new_count[l] += added[l];
         const std::vector<uint64_t> old_count = count;
+        apply_memory_cap(new_count);  // (before the relayout: the arena moves home at most once)
         relayout(new_count, owned);
 
         std::vector<uint64_t> group_start(nlist, 0), base(nlist, ~0ull);
@@ -1374,13 +1427,11 @@ struct vdb_ivf {
     EventSet& next_events() {
         if (events_used == events.size()) {
             EventSet e;
-            HIPCHECK(hipEventCreate(&e.begin));
-            HIPCHECK(hipEventCreate(&e.coarse_end));
-            HIPCHECK(hipEventCreate(&e.scan_begin));
-            HIPCHECK(hipEventCreate(&e.scan_end));
-            HIPCHECK(hipEventCreate(&e.end));
+            for (hipEvent_t* p : {&e.begin, &e.coarse_end, &e.scan_begin, &e.scan_end, &e.end, &e.x_end, &e.m_end})
+                HIPCHECK(hipEventCreate(p));
             events.push_back(e);
         }
+        events[events_used].xchg = false;
         return events[events_used++];
     }
 
@@ -1458,7 +1509,7 @@ struct vdb_ivf {
         // segments per item: one per wave (more adds tail latency, no throughput)
         const uint32_t segs_item = segs_item_opt ? segs_item_opt : (uint32_t)waves;
         // wide items of many queries: bounded on the matrix cores (L2 / IP, 16-query items)
-        const uint32_t mfma_min = wide && waves == 4 && metric != 2 && !(diag & 2) && vdbk::scan_bounded_fits(d4, k)
+        const uint32_t mfma_min = wide && waves == 4 && metric != 2 && !(VDB_SCAN_DIAG & 2) && vdbk::scan_bounded_fits(d4, k)
                                       ? scan_mfma_min : 0u;
         vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? (int)wide_group : 0, segs_item, w.items.p, w.items_w.p,
                           w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, w.thr.p,
@@ -1466,8 +1517,8 @@ struct vdb_ivf {
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
         vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
-                                wide_stride, w.counters.p + 4, seg_blocks, diag, segs_item, 0, w.thr.p,
-                                mfma_min, (diag & 16) ? stats.p + 5 : nullptr};
+                                wide_stride, w.counters.p + 4, seg_blocks, segs_item, 0, w.thr.p,
+                                mfma_min, bounded_stats ? stats.p + 5 : nullptr};
         // the bounded items first (the batch's most-probed lists), on the same stream
         if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
         if (wide && fused_scan) {
@@ -1704,6 +1755,11 @@ struct vdb_ivf {
     // Group handle (group.cpp): the same call over every member's shard.
     void group_search_device(const float* d_q, uint32_t n, uint32_t P, uint32_t k, float* d_dist, uint64_t* d_ids,
                              hipStream_t s, const uint32_t* req_start);
+    bool group_tiered() const {
+        for (auto& mb : members)
+            if (mb->tiered()) return true;
+        return false;
+    }
 
     // req_start: null (one reference search() call) or, for a coalesced batch of calls,
     // per query the call-global index of its request's first query (device memory).
@@ -1729,8 +1785,20 @@ struct vdb_ivf {
             require(comm_world == world && comm_rank == rank,
                     "the attached communicator's (rank, world) differs from the handle's shard", VDB_ERR_STATE);
         SearchSlot& w = begin_call(n, P, k, s, xchg ? comm_world : 0);
+        if (xchg && tiered()) {
+            // A sharded index larger than HBM (configs[4]): this rank serves its shard
+            // through its own cache. The tier cuts the call into sub-batches by what this
+            // rank's cache holds, which differs between ranks, so the exchange is per
+            // CALL: the whole call's partials in one record, ONE all-gather, one merge.
+            // (Every rank takes this path whenever its tier is on, so all ranks issue the
+            // same collectives whatever their cache contents.)
+            slot_buf(w, w.xgat, vdb_rank_record_bytes(n, k) * comm_world);
+            call_to_record(w, d_q, n, P, k, s, req_start);
+            exchange(w, n, k, d_dist, d_ids, s);
+            end_call(w, s);
+            return;
+        }
         if (tiered() && resident_n < storable_n) {  // (every stored list cached: the plain path)
-            require(!xchg, "the list-cache tier cannot be combined with a communicator", VDB_ERR_STATE);
             search_tiered(w, d_q, n, P, k, d_dist, d_ids, s, req_start);
             end_call(w, s);
             return;
@@ -1740,13 +1808,176 @@ struct vdb_ivf {
             float* od = xchg ? rec_dist(w) : d_dist + (size_t)b0 * k;
             uint64_t* oi = xchg ? rec_ids(w, B, k) : d_ids + (size_t)b0 * k;
             run_batch(w, d_q + (size_t)b0 * dim, B, P, k, od, oi, s, req_start, b0);
-            if (xchg) {
-                const hipStream_t cs = comm_enter(w, s);
-                NCCLCHECK(ncclAllGather(w.xrec.p, w.xgat.p, vdb_rank_record_bytes(B, k), ncclUint8, comm, cs));
-                comm_leave(w, s);
-                merge_gathered(w, comm_world, B, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s);
-            }
+            if (xchg) exchange(w, B, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s);
         }
         end_call(w, s);
+    }
+
+    // This shard's partial results of a whole call (n queries) into the slot's packed
+    // record: through the tier when some stored list is not cached, else the plain batches.
+    void call_to_record(SearchSlot& w, const float* d_q, uint32_t n, uint32_t P, uint32_t k, hipStream_t s,
+                        const uint32_t* req_start) {
+        slot_buf(w, w.xrec, vdb_rank_record_bytes(n, k));
+        float* rd = rec_dist(w);
+        uint64_t* ri = rec_ids(w, n, k);
+        if (tiered() && resident_n < storable_n) {
+            search_tiered(w, d_q, n, P, k, rd, ri, s, req_start);
+            return;
+        }
+        const uint32_t bmax = batch_cap(P);
+        for (uint32_t b0 = 0, B = std::min(bmax, n); b0 < n; b0 += B, B = std::min(B, n - b0))
+            run_batch(w, d_q + (size_t)b0 * dim, B, P, k, rd + (size_t)b0 * k, ri + (size_t)b0 * k, s, req_start,
+                      b0);
+    }
+
+    // ONE all-gather of the slot's packed record (B queries) over the attached
+    // communicator, on comm_stream fenced against s, then the on-device merge into the
+    // final results. The enqueue is settled against the communicator's deadline and the
+    // completion is handed to the watchdog (watch_exchange).
+    void exchange(SearchSlot& w, uint32_t B, uint32_t k, float* od, uint64_t* oi, hipStream_t s) {
+        if (comm_failed()) throw VdbError(VDB_ERR_DEVICE, comm_error_msg());
+        EventSet* ev = prof && events_used ? &events[events_used - 1] : nullptr;  // (the call's last batch)
+        const hipStream_t cs = comm_enter(w, s);
+        nccl_settle(ncclAllGather(w.xrec.p, w.xgat.p, vdb_rank_record_bytes(B, k), ncclUint8, comm, cs),
+                    "ncclAllGather");
+        if (ev) HIPCHECK(hipEventRecord(ev->x_end, cs));
+        watch_exchange(cs);
+        comm_leave(w, s);
+        merge_gathered(w, comm_world, B, k, od, oi, s);
+        if (ev) {
+            HIPCHECK(hipEventRecord(ev->m_end, s));
+            ev->xchg = true;
+        }
+    }
+
+    // ---- the communicator's deadline (option comm_timeout_ms) ----
+    // Non-blocking RCCL (ncclCommInitRankConfig, blocking = 0): init and every collective
+    // may return ncclInProgress and are polled to completion here, so a rank that never
+    // joins or a connection that never forms ends in an error naming this rank instead of
+    // a silent hang. Device-side completion of each exchange is watched by a host thread:
+    // an all-gather still pending after the deadline (a peer stalled or died) marks the
+    // communicator failed; later calls fail with that message, and vdb_ivf_comm_status
+    // lets a caller that waits on its streams stop waiting. (The communicator is not
+    // aborted from the watchdog: a collective still queued behind other work would then
+    // run on released resources. The process is expected to exit.)
+    uint32_t comm_timeout_ms = 120000;
+    std::string rank_tag() const {
+        return "rank " + std::to_string(comm_rank) + " of " + std::to_string(comm_world) + ": ";
+    }
+    void nccl_settle(ncclResult_t r, const char* what) {
+        if (r == ncclSuccess) return;
+        if (r != ncclInProgress) throw VdbError(VDB_ERR_DEVICE, rank_tag() + what + ": " + ncclGetErrorString(r));
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t spin = 0;; ++spin) {
+            ncclResult_t st = ncclSuccess;
+            const ncclResult_t q = ncclCommGetAsyncError(comm, &st);
+            if (q != ncclSuccess) st = q;
+            if (st == ncclSuccess) return;
+            if (st != ncclInProgress)
+                throw VdbError(VDB_ERR_DEVICE, rank_tag() + what + " failed: " + ncclGetErrorString(st));
+            const double ms =
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            if (ms > comm_timeout_ms) {
+                set_comm_error(rank_tag() + what + " still in progress after " + std::to_string((int)ms) +
+                               " ms (comm_timeout_ms): a peer rank is missing or stalled");
+                throw VdbError(VDB_ERR_DEVICE, comm_error_msg());
+            }
+            if (spin > 1000) std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+    }
+    struct Watch {
+        std::mutex m;
+        std::condition_variable cv;
+        std::deque<std::pair<hipEvent_t, std::chrono::steady_clock::time_point>> pending;  // issue order
+        std::vector<hipEvent_t> spare;
+        std::thread th;
+        bool stop = false;
+        uint64_t issued = 0, completed = 0;
+        std::string error;  // the first deadline miss (sticky until detach / a new attach)
+    };
+    std::unique_ptr<Watch> watch;
+    bool comm_failed() {
+        if (!watch) return false;
+        std::lock_guard<std::mutex> g(watch->m);
+        return !watch->error.empty();
+    }
+    std::string comm_error_msg() {
+        if (!watch) return std::string();
+        std::lock_guard<std::mutex> g(watch->m);
+        return watch->error;
+    }
+    void set_comm_error(const std::string& e) {
+        start_watch();
+        std::lock_guard<std::mutex> g(watch->m);
+        if (watch->error.empty()) {
+            watch->error = e;
+            std::fprintf(stderr, "[vdb_ivf] %s\n", e.c_str());
+        }
+    }
+    void start_watch() {
+        if (watch) return;
+        watch.reset(new Watch());
+        watch->th = std::thread([this] { watch_loop(); });
+    }
+    void stop_watch() {
+        if (!watch) return;
+        {
+            std::lock_guard<std::mutex> g(watch->m);
+            watch->stop = true;
+        }
+        watch->cv.notify_all();
+        if (watch->th.joinable()) watch->th.join();
+        for (auto& p : watch->pending) (void)hipEventDestroy(p.first);
+        for (hipEvent_t e : watch->spare) (void)hipEventDestroy(e);
+        watch.reset();
+    }
+    void watch_exchange(hipStream_t cs) {
+        start_watch();
+        hipEvent_t e = nullptr;
+        {
+            std::lock_guard<std::mutex> g(watch->m);
+            if (!watch->spare.empty()) {
+                e = watch->spare.back();
+                watch->spare.pop_back();
+            }
+        }
+        if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHECK(hipEventRecord(e, cs));
+        {
+            std::lock_guard<std::mutex> g(watch->m);
+            watch->pending.push_back({e, std::chrono::steady_clock::now()});
+            ++watch->issued;
+        }
+        watch->cv.notify_one();
+    }
+    void watch_loop() {
+        (void)hipSetDevice(device);
+        std::unique_lock<std::mutex> lk(watch->m);
+        while (!watch->stop) {
+            if (watch->pending.empty()) {
+                watch->cv.wait_for(lk, std::chrono::milliseconds(200));
+                continue;
+            }
+            const hipEvent_t e = watch->pending.front().first;
+            const auto t = watch->pending.front().second;
+            lk.unlock();
+            const hipError_t q = hipEventQuery(e);
+            lk.lock();
+            if (q == hipSuccess) {
+                watch->pending.pop_front();
+                watch->spare.push_back(e);
+                ++watch->completed;
+                continue;
+            }
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+            if (watch->error.empty() && (q != hipErrorNotReady || ms > comm_timeout_ms)) {
+                watch->error = rank_tag() + "exchange " + std::to_string(watch->completed) + " (all-gather) " +
+                               (q != hipErrorNotReady ? std::string("failed: ") + hipGetErrorString(q)
+                                                      : "not complete after " + std::to_string((int)ms) +
+                                                            " ms (comm_timeout_ms): a peer rank stalled or died");
+                std::fprintf(stderr, "[vdb_ivf] %s\n", watch->error.c_str());
+            }
+            watch->cv.wait_for(lk, std::chrono::milliseconds(q == hipErrorNotReady ? 2 : 200));
+        }
     }
 };

@@ -223,8 +223,6 @@ void set_option(vdb_ivf* g, const std::string& name, int64_t value) {
         g->coalesce_window_us = (uint32_t)value;
         return;
     }
-    require(name != "list_cache_bytes", "the list-cache tier is per GPU: not available on a group handle",
-            VDB_ERR_UNSUPPORTED);
     DeviceGuard dg;
     for (auto& mb : g->members)
         if (vdb_ivf_set_option(mb.get(), name.c_str(), value) != VDB_OK) throw VdbError(VDB_ERR_INVALID_ARGUMENT, g_last_error);
@@ -313,16 +311,9 @@ void vdb_ivf::group_search_device(const float* d_q, uint32_t n, uint32_t P, uint
             }
         }
     }
-    const uint32_t bmax = members[0]->batch_cap(P);
-    for (uint32_t b0 = 0, B = std::min(bmax, n); b0 < n; b0 += B, B = std::min(B, n - b0)) {
-        for (uint32_t m = 0; m < M; ++m) {
-            vdb_ivf& mb = *members[m];
-            mb.set_device();
-            if (!group_rccl && m > 0 && b0 > 0) HIPCHECK(hipStreamWaitEvent(ms[m], gev[1 + M], 0));
-            require(mb.run_batch(*w[m], qm[m] + (size_t)b0 * dim, B, P, k, rec_dist(*w[m]), rec_ids(*w[m], B, k), ms[m],
-                                 rm[m], b0),
-                    "group batch failed", VDB_ERR_STATE);
-        }
+    // ONE exchange of every member's record of B queries, then member 0 merges them
+    // into the caller's buffers (RCCL all-gather, or device copies on one device).
+    auto exchange = [&](uint32_t B, float* od, uint64_t* oi) {
         const uint64_t rb = vdb_rank_record_bytes(B, k);
         if (group_rccl) {
             std::vector<hipStream_t> cs(M);
@@ -350,7 +341,34 @@ void vdb_ivf::group_search_device(const float* d_q, uint32_t n, uint32_t P, uint
             HIPCHECK(hipEventRecord(gev[1 + M], s));  // members may overwrite their records after this
         }
         members[0]->set_device();
-        merge_gathered(*w[0], M, B, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s);
+        merge_gathered(*w[0], M, B, k, od, oi, s);
+    };
+    if (group_tiered()) {
+        // Members serving their lists through list caches (an index larger than HBM):
+        // each member's tier cuts the call into sub-batches by what its own cache holds,
+        // so every member writes the whole call's partials into one record (a member per
+        // host thread: the tier plans loads and reads list files on the host), then ONE
+        // exchange and one merge for the call.
+        const uint64_t rb = vdb_rank_record_bytes(n, k);
+        for (uint32_t m = 0; m < M; ++m) {
+            members[m]->set_device();
+            if (group_rccl || m == 0) members[m]->slot_buf(*w[m], w[m]->xgat, rb * M);
+        }
+        for_members(this, [&](size_t m) { members[m]->call_to_record(*w[m], qm[m], n, P, k, ms[m], rm[m]); });
+        exchange(n, d_dist, d_ids);
+    } else {
+        const uint32_t bmax = members[0]->batch_cap(P);
+        for (uint32_t b0 = 0, B = std::min(bmax, n); b0 < n; b0 += B, B = std::min(B, n - b0)) {
+            for (uint32_t m = 0; m < M; ++m) {
+                vdb_ivf& mb = *members[m];
+                mb.set_device();
+                if (!group_rccl && m > 0 && b0 > 0) HIPCHECK(hipStreamWaitEvent(ms[m], gev[1 + M], 0));
+                require(mb.run_batch(*w[m], qm[m] + (size_t)b0 * dim, B, P, k, rec_dist(*w[m]), rec_ids(*w[m], B, k),
+                                     ms[m], rm[m], b0),
+                        "group batch failed", VDB_ERR_STATE);
+            }
+            exchange(B, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k);
+        }
     }
     for (uint32_t m = 0; m < M; ++m) {
         vdb_ivf& mb = *members[m];
@@ -441,22 +459,83 @@ int vdb_ivf_attach_comm(vdb_ivf* h, const void* id, uint32_t rank, uint32_t worl
         require(h && id && world > 0 && rank < world, "invalid argument");
         require(!h->is_group(), "a group handle owns its communicators", VDB_ERR_STATE);
         std::lock_guard<std::mutex> g(h->mu);
-        require(!h->tiered(), "the list-cache tier cannot be combined with a communicator", VDB_ERR_STATE);
         require(h->rank == rank && h->world == world,
                 "attach_comm after set_shard / plan_shard with the same (rank, world)", VDB_ERR_STATE);
         h->set_device();
         h->quiesce();
+        h->stop_watch();  // a new communicator starts with a clean deadline record
         if (h->comm && h->comm_owned) (void)ncclCommDestroy(h->comm);
         h->comm = nullptr;
-        ncclUniqueId u;
-        std::memcpy(&u, id, sizeof(u));
-        ncclComm_t c = nullptr;
-        NCCLCHECK(ncclCommInitRank(&c, (int)world, u, (int)rank));  // blocks until every rank joins
-        h->comm = c;
-        h->comm_owned = true;
         h->comm_rank = rank;
         h->comm_world = world;
-        h->make_comm_stream();
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        // Non-blocking init polled against comm_timeout_ms: a rank that never joins ends
+        // in an error naming this rank (the communicator is aborted: no kernel has used
+        // it yet) instead of a hang inside ncclCommInitRank.
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        ncclComm_t c = nullptr;
+        const ncclResult_t r = ncclCommInitRankConfig(&c, (int)world, u, (int)rank, &cfg);
+        h->comm = c;
+        try {
+            if (r != ncclSuccess && r != ncclInProgress)
+                throw VdbError(VDB_ERR_DEVICE, h->rank_tag() + "ncclCommInitRankConfig: " + ncclGetErrorString(r));
+            if (!c) throw VdbError(VDB_ERR_DEVICE, h->rank_tag() + "ncclCommInitRankConfig returned no communicator");
+            h->nccl_settle(r, "communicator init (ncclCommInitRankConfig)");
+            h->make_comm_stream();
+            // Every rank must run the same collectives: compare the settings that decide
+            // them (one all-gather, which also proves the communicator end to end).
+            uint64_t mine[4] = {((uint64_t)h->dim << 32) | h->nlist, ((uint64_t)h->metric << 32) | h->batch,
+                                (uint64_t)h->tiered(), (uint64_t)h->stale};
+            DevBuf<uint64_t> dm, dall;
+            HIPCHECK(hipMemcpyAsync(dm.ensure(4), mine, sizeof(mine), hipMemcpyHostToDevice, h->comm_stream));
+            h->nccl_settle(ncclAllGather(dm.p, dall.ensure(4 * (size_t)world), 4, ncclUint64, c, h->comm_stream),
+                           "settings all-gather at attach");
+            std::vector<uint64_t> all(4 * (size_t)world);
+            HIPCHECK(hipMemcpyAsync(all.data(), dall.p, all.size() * 8, hipMemcpyDeviceToHost, h->comm_stream));
+            const auto t0 = std::chrono::steady_clock::now();
+            for (;;) {  // the deadline holds for the first collective too
+                const hipError_t q = hipStreamQuery(h->comm_stream);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) HIPCHECK(q);
+                const double ms =
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                if (ms > h->comm_timeout_ms)
+                    throw VdbError(VDB_ERR_DEVICE, h->rank_tag() + "settings all-gather at attach not complete after " +
+                                                       std::to_string((int)ms) + " ms (comm_timeout_ms)");
+                std::this_thread::sleep_for(std::chrono::microseconds(200));
+            }
+            for (uint32_t q = 0; q < world; ++q)
+                require(std::equal(mine, mine + 4, all.data() + 4 * (size_t)q),
+                        h->rank_tag() + "rank " + std::to_string(q) +
+                            " differs in dimension, nlist, metric, batch, list-cache tier or stale_slots",
+                        VDB_ERR_STATE);
+        } catch (...) {
+            if (h->comm) (void)ncclCommAbort(h->comm);
+            h->comm = nullptr;
+            h->comm_rank = 0;
+            h->comm_world = 1;
+            throw;
+        }
+        h->comm_owned = true;
+    });
+}
+
+int vdb_ivf_comm_status(vdb_ivf* h, uint64_t* exchanges_issued, uint64_t* exchanges_done) {
+    return guarded([&] {
+        require(h != nullptr, "null handle");
+        uint64_t is = 0, dn = 0;
+        std::string err;
+        if (h->watch) {
+            std::lock_guard<std::mutex> g(h->watch->m);
+            is = h->watch->issued;
+            dn = h->watch->completed;
+            err = h->watch->error;
+        }
+        if (exchanges_issued) *exchanges_issued = is;
+        if (exchanges_done) *exchanges_done = dn;
+        if (!err.empty()) throw VdbError(VDB_ERR_DEVICE, err);
     });
 }
 
@@ -466,8 +545,16 @@ int vdb_ivf_detach_comm(vdb_ivf* h) {
         require(!h->is_group(), "a group handle owns its communicators", VDB_ERR_STATE);
         std::lock_guard<std::mutex> g(h->mu);
         h->set_device();
-        h->quiesce();
-        if (h->comm && h->comm_owned) NCCLCHECK(ncclCommDestroy(h->comm));
+        // After a missed deadline the communicator is aborted, not destroyed (destroy
+        // would wait for the stalled exchange): detach only once no stream still holds
+        // that exchange queued (or let the process exit instead).
+        const bool failed = h->comm_failed();
+        if (!failed) h->quiesce();
+        h->stop_watch();
+        if (h->comm && h->comm_owned) {
+            if (failed) (void)ncclCommAbort(h->comm);
+            else NCCLCHECK(ncclCommDestroy(h->comm));
+        }
         h->comm = nullptr;
         h->comm_rank = 0;
         h->comm_world = 1;

@@ -1320,9 +1320,9 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
             const float dist = dist_finish<M>(qsum(g));
             if (g < np && __ballot(valid && dist <= th[g])) pend |= 1u << g;
         }
-        if (a.diag & 1) pend = 0;  // DIAGNOSTIC: no top-k maintenance (results invalid)
-        if ((a.diag & 4) && j == 0) pend = 0;  // DIAGNOSTIC: no insertion on a segment's first block
-        if ((a.diag & 8) && j != 0) pend = 0;  // DIAGNOSTIC: insertions on the first block only
+        if (VDB_SCAN_DIAG & 1) pend = 0;  // DIAGNOSTIC: no top-k maintenance (results invalid)
+        if ((VDB_SCAN_DIAG & 4) && j == 0) pend = 0;  // DIAGNOSTIC: no insertion on a segment's first block
+        if ((VDB_SCAN_DIAG & 8) && j != 0) pend = 0;  // DIAGNOSTIC: insertions on the first block only
         if (pend) {
             const uint64_t vid = valid ? id : kNoId;
             do {
@@ -1493,7 +1493,7 @@ __device__ __forceinline__ void scan_wide_wave_mfma(const ScanArgs& a, const Sca
             for (int r = 0; r < 16; ++r) bits |= !(lb[r] > T) ? 1u << r : 0u;
             bits &= vmask;
         }
-        if (a.diag & 1) bits = 0;  // DIAGNOSTIC: no exact pass / top-k (results invalid)
+        if (VDB_SCAN_DIAG & 1) bits = 0;  // DIAGNOSTIC: no exact pass / top-k (results invalid)
         // compact the candidates: (vector << 4 | query) per entry, lanes in order
         const uint32_t cnt = (uint32_t)__builtin_popcount(bits);
         uint32_t inc = cnt;
@@ -1670,7 +1670,7 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
         const int gp = (np + 1) / 2;
         if (threadIdx.x < 2) s_seg[threadIdx.x] = 0;  // visible after the staging barrier below
         if (threadIdx.x < (uint32_t)np) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
-        const int gpv = (a.diag & 2) ? 1 : gp;  // (DIAGNOSTIC diag&2: one pair only, results invalid)
+        const int gpv = (VDB_SCAN_DIAG & 2) ? 1 : gp;  // (DIAGNOSTIC diag&2: one pair only, results invalid)
         for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
             const uint32_t t = e / gpv, p = e - t * gpv;
             const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
@@ -1688,7 +1688,7 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
         const int p0 = split ? (int)half * gh : 0;
         const int gw = split ? (half ? gpv - gh : gh) : gpv;
         const int q0 = 2 * p0;
-        const int nq = split ? (half ? np - q0 : min(np, 2 * gh)) : ((a.diag & 2) ? min(np, 2) : np);
+        const int nq = split ? (half ? np - q0 : min(np, 2 * gh)) : ((VDB_SCAN_DIAG & 2) ? min(np, 2) : np);
         const float4* qw = qlds + (size_t)p0 * 2;
         // the item's segments [seg0, seg1) go to the waves (of each half) dynamically: a
         // wave that finishes early takes the next one, so waves idle only at the item's end

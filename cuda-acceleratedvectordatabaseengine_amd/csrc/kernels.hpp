@@ -26,6 +26,12 @@ constexpr uint32_t kMergeBlocks = VDB_MERGE_BLOCKS;  // level-1 partial merge: w
 #define VDB_TILE_PIPE_NARROW 4
 #endif
 constexpr int kTilePipeNarrow = VDB_TILE_PIPE_NARROW;  // the same for narrow items (queries held in SGPRs)
+// Scan timing experiments (a separate build, tools/build_variant.sh; never a runtime option):
+// 1 skip top-k upkeep, 2 one query pair per wave, 4 no insertion on a segment's first block,
+// 8 insertions on its first block only. Every non-zero value makes search results INVALID.
+#ifndef VDB_SCAN_DIAG
+#define VDB_SCAN_DIAG 0
+#endif
 constexpr int kTileAlign = kTilePipe;      // D4 is padded to whole pipeline rounds
 constexpr int kMergeFan = 32;              // segment partials folded per level-1 merge wave
 constexpr int kWideGroup = 16;             // max queries per wide scan item (4-wave items)
@@ -102,16 +108,15 @@ struct ScanArgs {
     uint32_t wide_stride;  // wide-item dispatch stride (prime; 0/1 = plan order)
     uint32_t* work;        // [3] item queues (narrow, wide, bounded), reset by the plan kernel
     uint32_t seg_blocks;   // 64-vector blocks per list segment (one wave's unit of a scan item)
-    uint32_t diag;         // diagnostics only (0 in production): 1 skip top-k upkeep, 2 one query pair,
-                           // 4 no insertion on a segment's first block, 8 on its later blocks
-    uint32_t segs_item;    // segments per wide item (>= 4; the 4 waves take them dynamically)
+    uint32_t segs_item;   // segments per wide item (>= 4; the 4 waves take them dynamically)
     uint32_t fused;        // ivf_scan_wide also drains the narrow queue (R = 1); the last `fused`
                            // workgroups start on narrow items (0: narrow items on their own kernel)
     uint32_t* thr;         // per sorted (query, probe) pair: the best k-th distance any wave has
                            // reached on that list so far (order-preserving uint encoding, reset
                            // by the plan kernel); candidates strictly worse are never inserted
     uint32_t mfma_min;     // wide items of >= this many queries run the bounded (MFMA) waves (0: never)
-    unsigned long long* mstats;  // diagnostics (null in production): [0] exact re-ranks, [1] bounded blocks
+    unsigned long long* mstats;  // bounded-scan statistics (option bounded_stats; null by default):
+                                 // [0] exact re-ranks, [1] bounded blocks
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);

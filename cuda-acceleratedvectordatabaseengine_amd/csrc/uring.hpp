@@ -107,17 +107,24 @@ public:
             out.swap(ready_);
             return out;
         }
-        const unsigned submit = pending_;
-        if (submit || min_done) {
-            const unsigned want = std::min(min_done, inflight_ + submit);
-            for (;;) {
-                const int r = (int)::syscall(__NR_io_uring_enter, fd_, submit, want,
-                                             want ? IORING_ENTER_GETEVENTS : 0u, nullptr, 0);
-                if (r >= 0) break;
-                if (errno != EINTR) throw std::runtime_error(std::string("io_uring_enter: ") + std::strerror(errno));
+        // io_uring_enter returns how many queued entries the kernel consumed; a partial
+        // submission (or an EINTR after some were taken) leaves the rest queued, so submit
+        // until none is pending. Completions already in the ring count toward `want`.
+        const unsigned want = std::min(min_done, inflight_ + pending_);
+        bool waited = want == 0;
+        while (pending_ || !waited) {
+            const unsigned submit = pending_;
+            const int r = (int)::syscall(__NR_io_uring_enter, fd_, submit, want, want ? IORING_ENTER_GETEVENTS : 0u,
+                                         nullptr, 0);
+            if (r < 0) {
+                if (errno == EINTR) continue;
+                throw std::runtime_error(std::string("io_uring_enter: ") + std::strerror(errno));
             }
-            inflight_ += submit;
-            pending_ = 0;
+            if ((unsigned)r > submit) throw std::runtime_error("io_uring_enter consumed more entries than queued");
+            if (r == 0 && submit) throw std::runtime_error("io_uring_enter consumed none of the queued reads");
+            inflight_ += (unsigned)r;
+            pending_ -= (unsigned)r;
+            waited = true;  // a successful enter with GETEVENTS has waited for `want`
         }
         unsigned head = *cq_head_;
         std::atomic_thread_fence(std::memory_order_acquire);
@@ -130,6 +137,17 @@ public:
         std::atomic_thread_fence(std::memory_order_release);
         *cq_head_ = head;
         return out;
+    }
+
+    // Forget every read: submit what is queued, wait for every read in flight and drop
+    // the completions (after a failed load, so no stale completion reaches the next one).
+    void drain() noexcept {
+        try {
+            while (pending_ || inflight_) (void)wait(inflight_ ? 1 : 0);
+        } catch (...) {
+            pending_ = inflight_ = 0;  // the ring is unusable; the owner discards the reader
+        }
+        ready_.clear();
     }
 
 private:

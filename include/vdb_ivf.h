@@ -59,8 +59,14 @@ typedef struct vdb_ivf_config {
     uint32_t nlist;
     int32_t metric;
     int32_t use_gpu;          /* accepted for API parity; the engine always runs on the GPU */
-    uint64_t max_gpu_memory;  /* accepted, not a cap: the whole index stays HBM-resident (288 GB/GPU); the
-                                 reference-style capped residency is the "list_cache_bytes" option */
+    uint64_t max_gpu_memory;  /* HBM cap on resident list bytes (count * (dim * 4 + 8) per list, the
+                                 reference's gpu_memory_used_, ivf_flat_index.cpp:398-402). Once an add
+                                 takes the lists above it, the handle switches to the list-cache tier
+                                 with an HBM cache of this many bytes (lists home in page-locked host
+                                 memory; results unchanged). 0 = no cap: every list HBM-resident
+                                 (288 GB per GPU). The reference searches lists that do not fit on the
+                                 CPU; here a search whose single query probes more than the cap fails
+                                 with VDB_ERR_OUT_OF_MEMORY. */
     int32_t device;           /* HIP device ordinal */
 } vdb_ivf_config;
 
@@ -76,14 +82,22 @@ typedef struct vdb_ivf_profile {
     uint64_t work_items;       /* sum over batches of scan work items */
     uint64_t scan_bytes;       /* algorithmic bytes read by ivf_scan: 4 * dim * scan_vectors */
     uint64_t pair_vectors;     /* sum over batches and (query, probe) pairs of n_l: distances computed */
-    uint64_t exact_reranks;    /* bounded scan: (query, vector) distances recomputed exactly (option diag & 16) */
-    uint64_t bounded_blocks;   /* bounded scan: 64-vector blocks bounded on the matrix cores (option diag & 16) */
+    uint64_t exact_reranks;    /* bounded scan: (query, vector) distances recomputed exactly (option bounded_stats) */
+    uint64_t bounded_blocks;   /* bounded scan: 64-vector blocks bounded on the matrix cores (option bounded_stats) */
     uint64_t computed_vectors; /* query slots the scan streams per vector: pair_vectors plus one per
                                   odd wide group (its last query runs alone, on scalar ops) */
+    double local_merge_ms;     /* summed per-batch merges after the scan (segment, slot, query top-k) */
+    uint64_t exchanges;        /* multi-GPU: exchanges timed below */
+    double exchange_ms;        /* summed: this rank's results ready -> all-gather done (the wait for the
+                                  slowest rank plus the collective itself) */
+    double rank_merge_ms;      /* summed: all-gather done -> final results merged */
 } vdb_ivf_profile;
 
 const char* vdb_last_error(void);
 const char* vdb_version(void);
+/* Hash of the sources that shape the scan kernels and their launches (16 hex digits):
+ * measurements (PMC traffic) are tied to the library they were taken on. */
+const char* vdb_build_id(void);
 int vdb_device_count(int* count);
 
 int vdb_ivf_create(const vdb_ivf_config* config, vdb_ivf** out);
@@ -155,12 +169,25 @@ int vdb_shard_plan(const uint64_t* list_sizes, uint32_t nlist, uint32_t world, u
  * vdb_ivf_search on that handle all-gather every batch's per-rank partials (ONE RCCL
  * all-gather per batch of vdb_rank_record_bytes per rank) and merge them on the device,
  * so every rank receives the FINAL results. Every rank must issue the same search calls
- * (same n, nprobe, k and batch option) in the same order. Not combined with the
- * list-cache tier. */
+ * (same n, nprobe, k and batch option) in the same order; on such a handle vdb_ivf_search
+ * does not coalesce concurrent callers (the grouping would depend on each rank's timing):
+ * calls run one at a time. With the list-cache tier on (the same setting on every rank),
+ * each rank serves its shard through its own cache and a call ends in ONE all-gather of
+ * the whole call's partials instead of one per batch. */
 #define VDB_COMM_ID_BYTES 128
 int vdb_comm_unique_id(void* id); /* VDB_COMM_ID_BYTES bytes (ncclGetUniqueId) */
 int vdb_ivf_attach_comm(vdb_ivf* index, const void* id, uint32_t rank, uint32_t world);
 int vdb_ivf_detach_comm(vdb_ivf* index);
+/* The communicator's deadline (option "comm_timeout_ms", default 120000): init is
+ * non-blocking and polled, so a rank that never joins makes vdb_ivf_attach_comm fail with
+ * VDB_ERR_DEVICE naming this rank; at attach every rank's dimension, nlist, metric, batch,
+ * tier setting and stale_slots are compared. Each exchange's completion is watched; one
+ * still pending after the deadline marks the communicator failed (later searches fail with
+ * the message). vdb_ivf_comm_status returns VDB_OK, or VDB_ERR_DEVICE with that message,
+ * and the exchanges issued / completed so far (either pointer may be NULL): a caller
+ * waiting on its streams polls it to stop waiting on a stalled peer. After a failure the
+ * process is expected to exit; vdb_ivf_detach_comm then aborts the communicator. */
+int vdb_ivf_comm_status(vdb_ivf* index, uint64_t* exchanges_issued, uint64_t* exchanges_done);
 /* One process driving several GPUs: a group handle with one member index per device
  * (devices[0] holds the host-API staging; device pointers passed to the group's calls
  * live on devices[0]). The group is used through every call of this header like a
@@ -170,8 +197,10 @@ int vdb_ivf_detach_comm(vdb_ivf* index);
  * add) and every member stores its lists; a search broadcasts the queries (RCCL), runs
  * each member's shard and all-gathers + merges per batch, with results bit-identical to
  * one device. Members on distinct devices use ncclCommInitAll; members sharing a device
- * (a one-GPU rehearsal) exchange through device copies. Not available on a group:
- * set_shard, plan_shard, open_lists, the list-cache tier. */
+ * (a one-GPU rehearsal) exchange through device copies. The list-cache tier and the
+ * max_gpu_memory cap act per member (per GPU); a call on a group with tiered members ends
+ * in one exchange for the whole call. Not available on a group: set_shard, plan_shard,
+ * open_lists. */
 int vdb_ivf_create_group(const vdb_ivf_config* config, const int* devices, uint32_t ndevices, vdb_ivf** out);
 uint32_t vdb_ivf_group_size(const vdb_ivf* index); /* members; 1 for a single-device handle */
 /* Per list the member (group) or rank (sharded handle) storing it; UINT32_MAX: none. */
@@ -208,7 +237,11 @@ int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
  * Centroids and list sizes are read at once; a list is read (pread -> pinned staging ->
  * HBM -> pad + interleave on the device) when a batch first probes it or on
  * vdb_ivf_warmup, and evicted like any cached list. Needs "list_cache_bytes" > 0 set
- * first; the handle becomes read-only (add fails with VDB_ERR_STATE). */
+ * first; the handle becomes read-only (add fails with VDB_ERR_STATE). A shard file
+ * (vdb_ivf_save of a handle with world > 1: every list's count, only the rank's own lists'
+ * rows) makes this handle that rank's shard (rank and world from the file, checked against
+ * the LPT plan); vdb_ivf_attach_comm then serves a sharded index larger than the node's
+ * HBM from every rank's own file. */
 int vdb_ivf_open_lists(vdb_ivf* index, const char* path);
 
 /* get_gpu_memory_usage's definition: count * (dim * 4 + 8) bytes per GPU-resident list. */
@@ -242,7 +275,10 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * "fused_scan" (1, default: one persistent scan grid takes both the wide and the narrow
  * items; 0: narrow items on a second stream), "list_cache_bytes" (0 = every list HBM-resident; > 0 = the list-cache tier above with an
  * HBM cache of that many bytes; a search whose single query probes more fails with
- * VDB_ERR_OUT_OF_MEMORY, a batch probing more is split). */
+ * VDB_ERR_OUT_OF_MEMORY, a batch probing more is split; setting it replaces the
+ * max_gpu_memory cap), "max_gpu_memory" (the Config cap, applied at once), "bounded_stats"
+ * (0/1: count the opt-in bounded scan's re-ranks in vdb_ivf_profile). Timing experiments
+ * that change results exist only as separate builds (VDB_SCAN_DIAG), never as options. */
 int vdb_ivf_set_option(vdb_ivf* index, const char* name, int64_t value);
 /* Host-API coalescing counters: device batches run and search() calls they served. */
 int vdb_ivf_coalesce_stats(vdb_ivf* index, uint64_t* batches, uint64_t* requests);

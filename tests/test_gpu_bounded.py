@@ -91,11 +91,11 @@ def test_bounded_path_is_taken_and_prunes():
     X, ids, lists, C, Q = hub_data(64, seed=5)
     g, o = lists_pair(X, ids, lists, C, 0)
     g.set_option("scan_mfma_min", 1)
-    g.set_option("diag", 16)  # statistics only: results stay valid
+    g.set_option("bounded_stats", 1)  # statistics only: results stay valid
     g.profile_reset()
     D, I = search_all(g, Q, 3, 10, 130)
     p = g.profile_read()
-    g.set_option("diag", 0)
+    g.set_option("bounded_stats", 0)
     assert_same(D, I, *o.search(Q, 3, 10))
     assert p["bounded_blocks"] > 0, p
     # every query scans the 30000-vector hub list: iid data prunes most pairs
@@ -119,11 +119,11 @@ def test_bounded_cancellation_every_pair_a_candidate(metric):
     g, o = lists_pair(X, ids, lists, C, metric)
     Dr, Ir = o.search(Q, 2, 10)
     g.set_option("scan_mfma_min", 1)
-    g.set_option("diag", 16)
+    g.set_option("bounded_stats", 1)
     g.profile_reset()
     D, I = search_all(g, Q, 2, 10, 96)
     p = g.profile_read()
-    g.set_option("diag", 0)
+    g.set_option("bounded_stats", 0)
     g.set_option("scan_mfma_min", 0)
     assert_same(D, I, Dr, Ir)
     if metric == 0:  # (IP: -<q, x> ~ -1e4 spreads by ~6, wider than its bound; pruning still works)

@@ -7,11 +7,12 @@
   fused persistent scan all run at their real shape. The oracle (ivf_flat_index.cpp:205-256
   restated) gets the GPU's centroids and every probed list; each search_device call is one
   reference search() call.
-* cfg4 — 100M x 768, nlist 16384, nprobe 64: rank 0 of the 8-way list-sharded build (the
-  per-GPU index of the 8-GPU configuration, 307 GB in total, too large for one GPU): exact
-  assignment of all 100M rows, LPT plan from the final list sizes, append of the owned
-  lists only. Four queries' rank-0 partial results against oracle_search_shard (owned
-  lists scanned, the others kept as counts for the empty-list rule, cpp:225).
+* cfg4 — 100M x 768, nlist 16384, nprobe 64 over 8 GPUs (307 GB in total, too large for
+  one GPU): exact assignment of all 100M rows, the LPT plan from the final list sizes, and
+  EVERY rank's shard built in turn (append of its owned lists only), its partial results
+  against oracle_search_shard (owned lists scanned, the others kept as counts for the
+  empty-list rule, cpp:225), then the device merge of the 8 rank records against the
+  oracle's merge: the whole configuration's answer for four queries.
 """
 import numpy as np
 import pytest
@@ -53,7 +54,7 @@ def test_cfg3_10m_x_768_nlist4096_nprobe32_two_batches_in_flight():
         vdb.gen_normal_device(data.data_ptr(), n * dim, seed=12345, stream=s)
         ids = torch.arange(n, dtype=torch.int64, device=dev)
         torch.cuda.synchronize()
-        g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist))
+        g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, max_gpu_memory=0))
         g.train_device(data.data_ptr(), 100_000)
         g.add_device(data.data_ptr(), ids.data_ptr(), n)
         del data, ids
@@ -82,7 +83,15 @@ def test_cfg3_10m_x_768_nlist4096_nprobe32_two_batches_in_flight():
 
 
 @pytest.mark.timeout(900)
-def test_cfg4_rank0_of_8_sharded_100m_x_768_nlist16384_nprobe64():
+def test_cfg4_all_8_shards_and_final_merge_100m_x_768_nlist16384_nprobe64():
+    """configs[3] whole: "100M x 768, nlist 16384, nprobe 64, lists sharded across 8 GPUs
+    with the top-k merge". One exact assignment pass over the 100M rows; then, one shard
+    at a time on this GPU, every rank r of the LPT plan (plan_shard + append of its rows):
+    its partial results for the queries (one search call, written as its packed rank
+    record) against oracle_search_shard over only that shard's probed lists (host memory
+    freed before the next shard). Finally the 8 GPU records are merged on the device
+    (vdb_merge_ranks_packed_device, the merge every rank runs after the all-gather) and
+    compared with the oracle's merge of its 8 partials: the final cfg4 answer."""
     import torch
     n, dim, nlist, nprobe, k, world, chunk, nq = 100_000_000, 768, 16384, 64, 10, 8, 10_000_000, 4
     dev = torch.device("cuda", 0)
@@ -91,7 +100,7 @@ def test_cfg4_rank0_of_8_sharded_100m_x_768_nlist16384_nprobe64():
         data = torch.empty((chunk, dim), dtype=torch.float32, device=dev)
         rid = torch.empty(chunk, dtype=torch.int64, device=dev)
         asg = torch.empty(n, dtype=torch.int32, device=dev)
-        g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist))
+        g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, max_gpu_memory=0))
         vdb.gen_normal_device(data.data_ptr(), 100_000 * dim, seed=12345, offset=0, stream=s)
         torch.cuda.synchronize()
         g.train_device(data.data_ptr(), 100_000)
@@ -100,25 +109,69 @@ def test_cfg4_rank0_of_8_sharded_100m_x_768_nlist16384_nprobe64():
             torch.cuda.synchronize()
             g.assign_device(data.data_ptr(), chunk, asg[a:].data_ptr())
         sizes = torch.bincount(asg, minlength=nlist).cpu().numpy().astype(np.uint64)
-        g.plan_shard(0, world, sizes)
-        for a in range(0, n, chunk):  # pass 2: rank 0 appends its LPT lists only
-            vdb.gen_normal_device(data.data_ptr(), chunk * dim, seed=12345, offset=a * dim, stream=s)
-            torch.arange(a, a + chunk, dtype=torch.int64, device=dev, out=rid)
-            torch.cuda.synchronize()
-            g.add_to_lists_device(data.data_ptr(), rid.data_ptr(), asg[a:].data_ptr(), chunk)
-        del data, rid, asg
-        torch.cuda.empty_cache()
+        cent = g.centroids
+        g.close()
         q = torch.empty((nq, dim), dtype=torch.float32, device=dev)
         vdb.gen_normal_device(q.data_ptr(), nq * dim, seed=12346, stream=s)
         torch.cuda.synchronize()
         Q = q.cpu().numpy()
-    assert np.array_equal(g.list_sizes(), sizes) and int(sizes.sum()) == n
-    owned = vdb.shard_plan(sizes, world) == 0
-    D, I = g.search(Q, nprobe=nprobe, k=k)  # rank 0's partial results
-    o = oracle.OracleIndex(dim, nlist, 0)
-    o.centroids = g.centroids
-    _export_probed(g, o, Q, nprobe, owned=owned)
-    Dr, Ir = o.search_shard(Q, nprobe, k, owned.astype(np.uint8), threads=THREADS)
-    assert np.array_equal(I, Ir)
-    assert np.array_equal(bits(D), bits(Dr))
-    assert (I != np.iinfo(np.uint64).max).any(), "rank 0 owns none of the probed lists"
+        rb = vdb.rank_record_bytes(nq, k)
+        ids_off = vdb.rank_record_ids_offset(nq, k)
+        records = torch.empty(world * rb, dtype=torch.uint8, device=dev)
+        plan = vdb.shard_plan(sizes, world)
+        o = oracle.OracleIndex(dim, nlist, 0)
+        o.centroids = cent
+        probed = {int(l) for qv in Q for l in o.select_nprobe(qv, nprobe)}
+        del o
+        oD = np.empty((world, nq, k), dtype=np.float32)
+        oI = np.empty((world, nq, k), dtype=np.uint64)
+        scanned = []
+        for r in range(world):
+            g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, max_gpu_memory=0))
+            g.centroids = cent
+            g.plan_shard(r, world, sizes)
+            for a in range(0, n, chunk):  # pass 2: rank r appends its LPT lists only
+                vdb.gen_normal_device(data.data_ptr(), chunk * dim, seed=12345, offset=a * dim, stream=s)
+                torch.arange(a, a + chunk, dtype=torch.int64, device=dev, out=rid)
+                torch.cuda.synchronize()
+                g.add_to_lists_device(data.data_ptr(), rid.data_ptr(), asg[a:].data_ptr(), chunk)
+            assert np.array_equal(g.list_sizes(), sizes)
+            owned = plan == r
+            assert np.array_equal(g.list_owners() == r, owned)
+            rec = records[r * rb:]
+            g.search_device(q.data_ptr(), nq, nprobe, k, rec.data_ptr(), rec.data_ptr() + ids_off, s)
+            torch.cuda.synchronize()
+            Dg = rec[:nq * k * 4].cpu().numpy().view(np.float32).reshape(nq, k)
+            Ig = rec[ids_off:ids_off + nq * k * 8].cpu().numpy().view(np.uint64).reshape(nq, k)
+            o = oracle.OracleIndex(dim, nlist, 0)
+            o.centroids = cent
+            loaded = 0
+            for l in range(nlist):
+                if l in probed and owned[l] and sizes[l]:
+                    v, i = o.list_buffers(l, int(sizes[l]))
+                    g.get_list_into(l, v, i)
+                    loaded += int(sizes[l])
+                else:
+                    o.set_list_count(l, int(sizes[l]))
+            Dr, Ir = o.search_shard(Q, nprobe, k, owned.astype(np.uint8), threads=THREADS)
+            del o
+            g.close()
+            torch.cuda.empty_cache()
+            assert np.array_equal(Ig, Ir), f"rank {r}: ids differ"
+            assert np.array_equal(bits(Dg), bits(Dr)), f"rank {r}: distance bits differ"
+            oD[r], oI[r] = Dr, Ir
+            scanned.append(loaded)
+        del data, rid, asg
+        torch.cuda.empty_cache()
+        od = torch.empty((nq, k), dtype=torch.float32, device=dev)
+        oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
+        vdb.merge_ranks_packed_device(records.data_ptr(), world, nq, k, od.data_ptr(), oi.data_ptr(), s)
+        torch.cuda.synchronize()
+        D, I = od.cpu().numpy(), oi.cpu().numpy().view(np.uint64)
+    Df, If = oracle.merge_ranks(oD, oI, k)
+    assert np.array_equal(I, If), "final (merged) ids differ"
+    assert np.array_equal(bits(D), bits(Df)), "final (merged) distance bits differ"
+    assert int(sizes.sum()) == n
+    assert sum(1 for x in scanned if x) >= 2, "the probed lists should span several shards"
+    # gpu_vs_cpu_test.cpp:209-219 validity rules on the final answer
+    assert np.all(np.isfinite(D)) and np.all(D >= 0) and np.all(I < n)

@@ -1,8 +1,8 @@
 #!/bin/bash
 # One GPU-box session (run via gpurun from the repo root): parity tests, the default
-# bench line, the kernel-trace summary of the bench command, PMC passes, index dump.
+# bench line, the kernel-trace summary of the bench command, PMC passes.
 #   usage: bash tools/gpu_session.sh <tag> [steps, comma-separated:
-#          tests,smoke,bench,dump,prof,pmc]  [extra bench args...]
+#          tests,smoke,bench,multi,grpc,prof,pmc]  [extra bench args...]
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 TAG=${1:-run}
@@ -30,7 +30,7 @@ run() {  # run <name> <seconds> <cmd...>: stop the session on any failure
 nproc > "$O/nproc.txt"
 lscpu > "$O/lscpu.txt" 2>/dev/null
 if has tests; then
-    run pytest 1100 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread
+    run pytest 1100 python -u -m pytest tests -m gpu ${PYTEST_X--x} -v --durations=25 --timeout 600 --timeout-method thread ${PYTEST_K}
     tail -3 "$O/pytest.log"
 fi
 if has smoke; then
@@ -54,9 +54,6 @@ if has grpc; then
     run grpc 600 python -u tools/grpc_load.py
     grep '^{' "$O/grpc.log" > "$O/grpc.json"
     cat "$O/grpc.json"
-fi
-if has dump; then
-    run dump 600 python -u tools/debug_dump_index.py 10000000 4096
 fi
 if has prof; then
     run prof 600 rocprofv3 --kernel-trace --stats -d "$O/prof" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight 1 $BARGS

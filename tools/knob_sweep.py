@@ -3,8 +3,9 @@
 
 Builds the workload's index once (bench.build_index / build_index_sharded), then times
 the scan for each engine option set (HIP events of the engine's profile, one batch in
-flight) and the wall time per batch. Options never change results except diag (timing
-experiments only).
+flight) and the wall time per batch. Options never change results (the result-changing
+timing experiments are separate builds: tools/build_variant.sh -DVDB_SCAN_DIAG=n, selected
+with VDB_IVF_LIB).
 usage: tools/knob_sweep.py cfg3|cfg4|mix "wide_group=32" "seg_vectors=1024,segs_per_item=8" ...
   cfg4 = rank 0 of the 8-way sharded 100M x 768 index (the per-GPU work of 8 GPUs)
 """
@@ -19,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
-DEFAULTS = {"seg_vectors": 0, "segs_per_item": 0, "wide_stride": 1, "diag": 0, "fused_scan": 1, "narrow_blocks": 64,
+DEFAULTS = {"seg_vectors": 0, "segs_per_item": 0, "wide_stride": 1, "fused_scan": 1, "narrow_blocks": 64,
             "wide_group": 16}
 
 

@@ -9,6 +9,9 @@ value is doubled. rocprofv3 reports FETCH_SIZE in KiB. The scan phase of one bat
 ivf_scan_wide dispatch (plus ivf_scan_narrow when the fused scan is off): the bytes of
 all scan dispatches are summed and divided by the number of batches.
 
+Every entry is stamped with the build id of the library it was measured on (vdb_build_id,
+a hash of the scan kernel sources); bench.py uses an entry only on a library of that id.
+
 usage: tools/pmc_traffic.py <out.json> (<pmc-output-dir> <batches> <workload-key>)...
 """
 import csv
@@ -17,6 +20,17 @@ import json
 import os
 import sys
 from collections import defaultdict
+
+
+def build_id():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "cuda-acceleratedvectordatabaseengine_amd")
+    spec = importlib.util.spec_from_file_location("vdb_amd", os.path.join(pkg, "__init__.py"),
+                                                  submodule_search_locations=[pkg])
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.build_id()
 
 
 def summarise(d, batches, key):
@@ -36,6 +50,7 @@ def summarise(d, batches, key):
     kib = sum(scan.values())
     return {
         "workload": key,
+        "build_id": build_id(),
         "hbm_bytes_per_scan_launch": int(kib * 1024.0 * 2.0 / batches),
         "source": "rocprofv3 --pmc FETCH_SIZE (KiB, x2 gfx950 correction) summed over the ivf_scan_* "
                   f"dispatches of {batches} batches",
