@@ -96,6 +96,7 @@ def build_index(vdb, args, device, rank, world):
     t1 = time.perf_counter()
     idx.add_device(data.data_ptr(), ids.data_ptr(), n)
     t2 = time.perf_counter()
+    census(vdb, idx, args, data, min(args.train, n))
     del data, ids
     torch.cuda.empty_cache()
     log(rank, f"[bench] train {t1 - t0:.2f}s add {t2 - t1:.2f}s; index {idx.gpu_bytes_allocated() / 2**30:.1f} GiB on rank 0")
@@ -107,6 +108,23 @@ def new_index(vdb, args, device):
     # would put a 31 GB index on the list-cache tier)
     return vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(args.dim, args.nlist, vdb.Metric.L2, max_gpu_memory=0,
                                                     device=device.index))
+
+
+def census(vdb, idx, args, rows, nrows):
+    """--plan weighted: how many of the first --census rows of the database (query-like
+    draws; the training sample) probe each list at the search's nprobe."""
+    if getattr(args, "plan", "lpt") == "weighted" and getattr(args, "census_counts", None) is None:
+        n = min(args.census, nrows)
+        args.census_counts = (idx.probe_census(rows.data_ptr(), n, args.nprobe), n)
+
+
+def shard_owners(vdb, args, sizes, world):
+    """The shard plan: LPT on list sizes (default), or LPT on the expected scan cost per
+    batch from the probe census (--plan weighted, vdb_shard_plan_probe_weighted)."""
+    if getattr(args, "plan", "lpt") != "weighted":
+        return None
+    counts, n = args.census_counts
+    return vdb.shard_plan_probe_weighted(sizes, counts, n, args.batch, world)
 
 
 def sharded_assign(vdb, args, device, rank):
@@ -126,6 +144,7 @@ def sharded_assign(vdb, args, device, rank):
     fill_rows(vdb, args, data, 0, ntrain, 12345, stream)
     torch.cuda.synchronize()
     idx.train_device(data.data_ptr(), ntrain)
+    census(vdb, idx, args, data, ntrain)
     t1 = time.perf_counter()
     for a in range(0, n, chunk):
         m = min(chunk, n - a)
@@ -150,7 +169,7 @@ def sharded_append(vdb, args, device, idx, asg, sizes, rank, world):
     data = torch.empty((chunk, dim), dtype=torch.float32, device=device)
     ids = torch.empty(chunk, dtype=torch.int64, device=device)
     t0 = time.perf_counter()
-    idx.plan_shard(rank, world, sizes)
+    idx.plan_shard(rank, world, sizes, owners=shard_owners(vdb, args, sizes, world))
     for a in range(0, n, chunk):
         m = min(chunk, n - a)
         fill_rows(vdb, args, data, a, m, 12345, stream)
@@ -480,6 +499,10 @@ def main():
     ap.add_argument("--emulate-rank", default="0", metavar="R",
                     help="with --emulate-shard: the rank emulated (0..W-1), or 'all' to time every rank's shard in "
                          "turn (sharded build) and report the per-rank balance")
+    ap.add_argument("--plan", choices=["lpt", "weighted"], default="lpt",
+                    help="shard plan: LPT on list sizes, or LPT on each list's expected scan cost per batch from a "
+                         "probe census of --census training rows (vdb_shard_plan_probe_weighted)")
+    ap.add_argument("--census", type=int, default=65536, help="rows of the probe census (--plan weighted)")
     ap.add_argument("--comm-timeout", type=float, default=120.0,
                     help="N ranks, engine exchange: seconds before a communicator init or an exchange that has not "
                          "completed fails the run with an error naming the rank (option comm_timeout_ms)")
@@ -663,6 +686,7 @@ def timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, che
         parity_multi = bool(int(flag.item()) == 1)
     lat = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     p99 = percentile(lat, 0.99)
+    lat_mean = sum(lat) / max(len(lat), 1)
     if world > 1:
         t = torch.tensor([elapsed, p99], dtype=torch.float64, device=ctrl)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -690,7 +714,8 @@ def timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, che
         p99_single = float(t[0])
         per_rank = [None] * world
         dist.all_gather_object(per_rank, mine)
-    return {"elapsed": elapsed, "p99": p99, "p99_single": p99_single, "prof": prof, "parity_multi": parity_multi,
+    return {"elapsed": elapsed, "p99": p99, "lat_mean": lat_mean, "p99_single": p99_single, "prof": prof,
+            "parity_multi": parity_multi,
             "per_rank": per_rank, "mine": mine}
 
 
@@ -710,13 +735,14 @@ def rank_breakdown(rank, prof, ms_per_step, step_ms_single):
             "step_ms_one_in_flight": round(sum(step_ms_single) / max(len(step_ms_single), 1), 4),
             "ms_per_step": round(ms_per_step, 4),
             "scan_bytes_per_batch": int(prof["scan_bytes"] / max(prof["batches"], 1)),
+            "distances_per_batch": int(prof["pair_vectors"] / max(prof["batches"], 1)),
             "distinct_lists_per_batch": round(prof["distinct_lists"] / max(prof["batches"], 1), 1)}
 
 
 def balance(per_rank):
     """max / min over ranks of the per-rank phases (1.0 = perfectly balanced shards)."""
     out = {}
-    for key in ("scan_ms", "search_ms", "ms_per_step", "scan_bytes_per_batch"):
+    for key in ("scan_ms", "search_ms", "ms_per_step", "scan_bytes_per_batch", "distances_per_batch"):
         v = [r[key] for r in per_rank if r and r.get(key)]
         if v:
             out[key] = {"max": max(v), "min": min(v), "max_over_min": round(max(v) / min(v), 4),
@@ -756,13 +782,16 @@ def run_emulated_ranks(vdb, args, device):
             idx.set_option(name, int(val))
         res = timed_region(vdb, idx, args, device, 0, 1, queries, out_d, out_i)
         row = dict(res["mine"], rank=r, qps=round(args.steps * args.batch / res["elapsed"], 1),
-                   p99_ms=round(res["p99"], 4), p99_ms_one_in_flight=round(res["p99_single"], 4),
+                   p99_ms=round(res["p99"], 4), latency_mean_ms=round(res["lat_mean"], 4),
+                   p99_ms_one_in_flight=round(res["p99_single"], 4),
                    shard_gib=round(idx.gpu_bytes_allocated() / 2**30, 2), append_s=binfo["append_s"])
         log(0, f"[bench] emulated rank {r}/{W}: " + json.dumps(row))
         ranks.append(row)
         idx.close()
         torch.cuda.empty_cache()
-    plan = vdb.shard_plan(sizes, W)
+    plan = shard_owners(vdb, args, sizes, W)
+    if plan is None:
+        plan = vdb.shard_plan(sizes, W)
     lists = [int((plan == r).sum()) for r in range(W)]
     vecs = [int(sizes[plan == r].sum()) for r in range(W)]
     return {
@@ -771,7 +800,7 @@ def run_emulated_ranks(vdb, args, device):
         "config": {"workload": f"{args.nvec // 1_000_000}M x {args.dim}D IVF-Flat L2, nlist {args.nlist}, "
                                f"nprobe {args.nprobe}, batch {args.batch}, k {args.k}",
                    "inflight": args.inflight, "data": args.data},
-        "ranks": ranks, "balance": balance(ranks),
+        "plan": args.plan, "ranks": ranks, "balance": balance(ranks),
         "shard_lists": lists, "shard_vectors": vecs,
         "predicted_8gpu_qps_from_max_rank_step": round(args.batch * 1e3 / max(r["ms_per_step"] for r in ranks), 1),
         "build": info, "note": "partial (per-rank) results; exchange excluded; each rank's search timed alone",
@@ -798,7 +827,7 @@ def run(vdb, args, device, rank, world):
     if args.prewarm:  # list-cache tier: load every list up front, in list order (vdb.QueryService/Warmup)
         idx.warmup_lists(list(range(args.nlist)))
     if args.emulate_shard > 1 and world == 1 and not args.sharded_build:
-        idx.set_shard(er, args.emulate_shard)
+        idx.set_shard(er, args.emulate_shard, owners=shard_owners(vdb, args, idx.list_sizes(), args.emulate_shard))
     B, k = args.batch, args.k
     queries, out_d, out_i = make_queries(vdb, args, device)
     main_stream = torch.cuda.current_stream()
@@ -815,7 +844,7 @@ def run(vdb, args, device, rank, world):
                               chk_i[b0:].data_ptr(), main_stream.cuda_stream)
         torch.cuda.synchronize()
         check = (q0, nchk, chk_d, chk_i)
-        idx.set_shard(rank, world)
+        idx.set_shard(rank, world, owners=shard_owners(vdb, args, idx.list_sizes(), world))
     if world > 1 and args.exchange == "engine":
         attach_engine_comm(vdb, idx, args, rank, world)
     res = timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, check)
@@ -845,6 +874,9 @@ def run(vdb, args, device, rank, world):
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "p99_ms": round(p99, 4),
         "p99_ms_one_in_flight": round(p99_single, 4),
+        # with `inflight` batches in flight a batch's latency is at least inflight x ms_per_step
+        # on average (Little's law); p99 / mean shows the spread around that
+        "latency_mean_ms": round(res["lat_mean"], 4),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -860,7 +892,7 @@ def run(vdb, args, device, rank, world):
                         f"batch {B}, k {k}",
             "nvec": args.nvec, "dim": args.dim, "nlist": args.nlist, "nprobe": args.nprobe, "batch": B, "k": k,
             "train_vectors": min(args.train, args.nvec),
-            "parallelism": (f"lists sharded over {world} rank(s) (LPT), one all-gather per batch of per-rank top-k "
+            "parallelism": (f"lists sharded over {world} rank(s) ({'probe-weighted ' if args.plan == 'weighted' else ''}LPT), one all-gather per batch of per-rank top-k "
                             + (" (engine RCCL communicator, vdb_ivf_attach_comm)" if args.exchange == "engine" else
                                f" (torch.distributed {'RCCL' if args.dist_backend == 'nccl' else 'gloo, host-staged'})")
                             if world > 1 else "single GPU") + f"; {args.inflight} batches in flight",

@@ -115,6 +115,10 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_load": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "vdb_merge_ranks_device": (ctypes.c_int, [vp, vp, u32, u32, u32, vp, vp, vp]),
         "vdb_shard_plan": (ctypes.c_int, [vp, u32, u32, vp]),
+        "vdb_shard_plan_probe_weighted": (ctypes.c_int, [vp, vp, u64, u32, u32, u32, vp]),
+        "vdb_ivf_probe_census": (ctypes.c_int, [vp, vp, u64, u32, vp]),
+        "vdb_ivf_set_shard_owners": (ctypes.c_int, [vp, u32, u32, vp]),
+        "vdb_ivf_plan_shard_owners": (ctypes.c_int, [vp, u32, u32, vp, vp]),
         "vdb_rank_record_bytes": (u64, [u32, u32]),
         "vdb_merge_ranks_packed_device": (ctypes.c_int, [vp, u32, u32, u32, vp, vp, vp]),
         "vdb_ivf_warmup": (ctypes.c_int, [vp, vp, u32]),
@@ -179,6 +183,15 @@ def shard_plan(list_sizes, world: int) -> np.ndarray:
     s = np.ascontiguousarray(list_sizes, dtype=np.uint64)
     out = np.empty(len(s), dtype=np.uint32)
     _check(lib().vdb_shard_plan(_ptr(s), len(s), world, _ptr(out)))
+    return out
+
+
+def shard_plan_probe_weighted(list_sizes, probe_counts, n_sample: int, batch: int, world: int) -> np.ndarray:
+    """LPT owner of every list over the expected scan cost per batch (probe census weights)."""
+    s = np.ascontiguousarray(list_sizes, dtype=np.uint64)
+    c = np.ascontiguousarray(probe_counts, dtype=np.uint64)
+    out = np.empty(len(s), dtype=np.uint32)
+    _check(lib().vdb_shard_plan_probe_weighted(_ptr(s), _ptr(c), n_sample, batch, len(s), world, _ptr(out)))
     return out
 
 
@@ -349,8 +362,19 @@ class IVFFlatIndex:
         return self.config.dimension
 
     # ---- sharding ----
-    def set_shard(self, rank: int, world: int):
-        _check(lib().vdb_ivf_set_shard(self._h, rank, world))
+    def set_shard(self, rank: int, world: int, owners=None):
+        """Keep rank's lists of `world` (the LPT plan, or an explicit `owners` array)."""
+        if owners is None:
+            _check(lib().vdb_ivf_set_shard(self._h, rank, world))
+        else:
+            o = np.ascontiguousarray(owners, dtype=np.uint32)
+            _check(lib().vdb_ivf_set_shard_owners(self._h, rank, world, _ptr(o)))
+
+    def probe_census(self, rows_ptr: int, n: int, nprobe: int) -> np.ndarray:
+        """Per list: how many of n device rows probe it (vdb_ivf_probe_census)."""
+        out = np.empty(self.config.nlist, dtype=np.uint64)
+        _check(lib().vdb_ivf_probe_census(self._h, ctypes.c_void_p(rows_ptr), n, nprobe, _ptr(out)))
+        return out
 
     def attach_comm(self, comm_id: bytes, rank: int, world: int):
         """Join the RCCL communicator `comm_id` as `rank` of `world` (after set_shard /
@@ -379,12 +403,17 @@ class IVFFlatIndex:
         _check(lib().vdb_ivf_list_owners(self._h, _ptr(out)))
         return out
 
-    def plan_shard(self, rank: int, world: int, final_sizes):
-        """Sharded build: fix this rank's lists from the final list sizes before any add."""
+    def plan_shard(self, rank: int, world: int, final_sizes, owners=None):
+        """Sharded build: fix this rank's lists from the final list sizes before any add
+        (the LPT plan, or an explicit `owners` array)."""
         s = np.ascontiguousarray(final_sizes, dtype=np.uint64)
         if len(s) != self.config.nlist:
             raise ValueError("final_sizes needs one entry per list")
-        _check(lib().vdb_ivf_plan_shard(self._h, rank, world, _ptr(s)))
+        if owners is None:
+            _check(lib().vdb_ivf_plan_shard(self._h, rank, world, _ptr(s)))
+        else:
+            o = np.ascontiguousarray(owners, dtype=np.uint32)
+            _check(lib().vdb_ivf_plan_shard_owners(self._h, rank, world, _ptr(s), _ptr(o)))
 
     # ---- residency / stats ----
     def warmup_lists(self, list_ids):

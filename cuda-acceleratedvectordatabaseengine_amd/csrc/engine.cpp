@@ -2,6 +2,8 @@
 // gfx950 kernels of kernels.hip.
 #include "engine.hpp"
 
+#include <cmath>
+
 namespace vdbe {
 thread_local std::string g_last_error;
 
@@ -430,22 +432,92 @@ int vdb_merge_ranks_packed_device(const void* d_records, uint32_t nranks, uint32
     });
 }
 
+// Longest-processing-time placement: lists by decreasing cost (ties: lower list id) each
+// to the least-loaded rank (ties: lower rank). Integer costs: identical on every rank.
+static void lpt_plan(const uint64_t* cost, uint32_t nlist, uint32_t world, uint32_t* owner) {
+    std::vector<uint32_t> order(nlist);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+    using Load = std::pair<uint64_t, uint32_t>;  // (load, rank): least load, then lowest rank
+    std::priority_queue<Load, std::vector<Load>, std::greater<Load>> pq;
+    for (uint32_t r = 0; r < world; ++r) pq.push({0, r});
+    for (uint32_t l : order) {
+        Load top = pq.top();
+        pq.pop();
+        owner[l] = top.second;
+        top.first += cost[l];
+        pq.push(top);
+    }
+}
+
 int vdb_shard_plan(const uint64_t* sizes, uint32_t nlist, uint32_t world, uint32_t* owner) {
     return guarded([&] {
         require(sizes && owner && world > 0, "invalid argument");
-        std::vector<uint32_t> order(nlist);
-        std::iota(order.begin(), order.end(), 0u);
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return sizes[a] > sizes[b]; });
-        using Load = std::pair<uint64_t, uint32_t>;  // (load, rank): least load, then lowest rank
-        std::priority_queue<Load, std::vector<Load>, std::greater<Load>> pq;
-        for (uint32_t r = 0; r < world; ++r) pq.push({0, r});
-        for (uint32_t l : order) {
-            Load top = pq.top();
-            pq.pop();
-            owner[l] = top.second;
-            top.first += sizes[l];
-            pq.push(top);
+        lpt_plan(sizes, nlist, world, owner);
+    });
+}
+
+int vdb_shard_plan_probe_weighted(const uint64_t* sizes, const uint64_t* probe_counts, uint64_t n_sample,
+                                  uint32_t batch, uint32_t nlist, uint32_t world, uint32_t* owner) {
+    return guarded([&] {
+        require(sizes && probe_counts && owner && world > 0 && n_sample > 0 && batch > 0, "invalid argument");
+        // Expected scan cost of list l per batch of `batch` queries, in units of one read
+        // of one vector: M ~ Binomial(batch, p_l) queries probe it (p_l from the census);
+        // the list is streamed once per group of kWideGroup queries (E[ceil(M / 16)]) and
+        // every query adds its distance arithmetic (VALU ~ one read's time per 16 queries
+        // at 768-D on MI355X, half-overlapped with the stream: 0.5 E[M] / 16).
+        const uint32_t G = (uint32_t)vdbk::kWideGroup;
+        std::vector<uint64_t> cost(nlist);
+        std::vector<double> pm(batch + 1);
+        for (uint32_t l = 0; l < nlist; ++l) {
+            const double p = std::min(1.0, (double)probe_counts[l] / (double)n_sample);
+            double reads = 0.0;
+            if (p > 0.0) {  // E[ceil(M / G)] over the binomial pmf (log-space terms)
+                const double lp = std::log(p), lq = p < 1.0 ? std::log1p(-p) : -INFINITY;
+                double lc = 0.0;  // log C(batch, m)
+                for (uint32_t m = 0; m <= batch; ++m) {
+                    if (m) lc += std::log((double)(batch - m + 1)) - std::log((double)m);
+                    const double lt = lc + (m ? m * lp : 0.0) + (batch - m ? (batch - m) * lq : 0.0);
+                    reads += std::exp(lt) * (double)((m + G - 1) / G);
+                }
+            }
+            const double c = (double)sizes[l] * (reads + 0.5 * (double)batch * p / (double)G);
+            cost[l] = (uint64_t)std::llround(c * 1024.0) + (sizes[l] ? 1 : 0);  // (a stored list costs > 0)
         }
+        lpt_plan(cost.data(), nlist, world, owner);
+    });
+}
+
+int vdb_ivf_probe_census(vdb_ivf* h, const float* d_rows, uint64_t n, uint32_t nprobe, uint64_t* counts) {
+    return guarded([&] {
+        require(h && counts && (d_rows || n == 0), "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        std::fill(counts, counts + h->nlist, 0ull);
+        vdb_ivf* a = h->head();  // (a group: its first member, the device of d_rows)
+        a->set_device();
+        a->probe_census(d_rows, n, nprobe, counts);
+        h->set_device();
+    });
+}
+
+int vdb_ivf_set_shard_owners(vdb_ivf* h, uint32_t rank, uint32_t world, const uint32_t* owner) {
+    return guarded([&] {
+        require(h && owner && world > 0 && rank < world, "invalid shard");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        no_group(h, "set_shard");
+        h->set_shard(rank, world, owner);
+    });
+}
+
+int vdb_ivf_plan_shard_owners(vdb_ivf* h, uint32_t rank, uint32_t world, const uint64_t* final_sizes,
+                              const uint32_t* owner) {
+    return guarded([&] {
+        require(h && final_sizes && owner && world > 0 && rank < world, "invalid shard");
+        std::lock_guard<std::mutex> g(h->mu);
+        h->set_device();
+        no_group(h, "plan_shard");
+        h->plan_shard(rank, world, final_sizes, owner);
     });
 }
 
@@ -590,6 +662,15 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->scan_mfma_min = (uint32_t)value;
         } else if (n == "fused_scan") {
             h->fused_scan = value != 0;
+        } else if (n == "fused_merge") {
+            h->fused_merge = value != 0;
+        } else if (n == "sgpr_queries") {
+            h->sgpr_queries = value != 0;
+        } else if (n == "scan_window") {
+            require(value >= 0 && value <= 7, "scan_window is 0 (no limit) .. 7");
+            h->quiesce();
+            h->scan_window = (uint32_t)value;
+            h->scan_seq = 0;
         } else if (n == "narrow_blocks") {
             require(value > 0 && value <= 4096, "narrow_blocks out of range");
             h->narrow_blocks = (uint32_t)value;

@@ -283,6 +283,14 @@ struct vdb_ivf {
     uint32_t segs_item_opt = 0;   // segments per wide item (0: one per wave, taken dynamically)
     uint32_t wide_group = 16;     // queries per wide item at most: 16 (4-wave workgroups) or 32 (8-wave)
     bool fused_scan = true;       // narrow items inside the wide scan's grid (option fused_scan; +2-3 %)
+    bool fused_merge = true;      // the four per-batch merges as one launch (option fused_merge)
+    bool sgpr_queries = false;    // wide scan reads its query pairs through SGPRs (option sgpr_queries)
+    // At most this many scans of batches in flight overlap (0: no limit): a batch's scan
+    // waits for the scan issued `scan_window` batches earlier to finish, so the GPU serves
+    // batches closer to issue order (latency spread at several batches in flight).
+    uint32_t scan_window = 0;
+    uint64_t scan_seq = 0;
+    int scan_hist[8] = {};  // slot index of the scans issued, by sequence number
     uint32_t narrow_blocks = 64;  // persistent narrow-scan workgroups beside the wide scan (1/8 shard: +1.5 % vs 512)
 
     // List-cache tier (option list_cache_bytes > 0), the reference's residency model
@@ -344,14 +352,17 @@ struct vdb_ivf {
     // batch's scan). A call takes the next slot; its stream first waits for the
     // slot's previous batch (slot.done), wherever that ran.
     struct SearchSlot {
-        DevBuf<float> qpad{true}, cd{true}, cdelta{true}, part_d{true}, slot_d{true}, carry_d{true};
-        DevBuf<uint64_t> part_i{true}, slot_i{true}, carry_i{true};
+        DevBuf<float> qpad{true}, cd{true}, cdelta{true}, part_d{true}, slot_d{true}, carry_d{true}, carry2_d{true};
+        DevBuf<uint64_t> part_i{true}, slot_i{true}, carry_i{true}, carry2_i{true};
+        uint32_t carry_sel = 0;  // fused merge: the carry buffer the call's next batch reads (ping-pong)
+        const float* q = nullptr;  // the batch's zero-padded queries: qpad, or the caller's rows when dim == dp
         DevBuf<uint32_t> probes{true}, nseg_qp{true}, pbqp{true}, sorted_pair{true}, pbs{true}, counters{true},
             l1base{true}, cand{true}, thr{true};
         DevBuf<uint2> l1_items{true};
         DevBuf<float> l1_d{true};
         DevBuf<uint64_t> l1_i{true};
         DevBuf<vdbk::ScanItem> items{true}, items_w{true};
+        DevBuf<float> qstage{true};  // (sgpr_queries) wide groups' query pairs, [B*P][d4][8] + slack
         DevBuf<uint8_t> xrec{true}, xgat{true};  // multi-GPU: this rank's packed partials, the gathered records
         DevBuf<float> gq{true};            // group member: the call's queries on this device
         DevBuf<uint32_t> greq{true};       // group member: the call's request starts on this device
@@ -359,6 +370,7 @@ struct vdb_ivf {
         hipStream_t gstream = nullptr;  // group member: the stream this slot's searches run on
         hipEvent_t x_ready = nullptr, x_done = nullptr;  // fences around this slot's collectives
         hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
+        hipEvent_t scan_done = nullptr;  // (scan_window) this slot's latest scan has finished
         bool used = false;
     };
     static constexpr int kSlots = 3;
@@ -464,6 +476,7 @@ struct vdb_ivf {
             if (sl.fork) (void)hipEventDestroy(sl.fork);
             if (sl.join) (void)hipEventDestroy(sl.join);
             if (sl.done) (void)hipEventDestroy(sl.done);
+            if (sl.scan_done) (void)hipEventDestroy(sl.scan_done);
             if (sl.side) (void)hipStreamDestroy(sl.side);
             if (sl.gstream) (void)hipStreamDestroy(sl.gstream);
             if (sl.x_ready) (void)hipEventDestroy(sl.x_ready);
@@ -1097,12 +1110,10 @@ struct vdb_ivf {
             at = off[l] + stored[l] * 8 + stored[l] * (uint64_t)dim * 4;
         }
         std::vector<uint8_t> own(nlist, 1);
-        if (shard_file) {  // the stored lists must be exactly the rank's LPT lists
-            std::vector<uint32_t> plan(nlist);
-            vdb_shard_plan(cnt.data(), nlist, hdr[4], plan.data());
+        if (shard_file) {  // a list is this rank's when the file stores its rows (any plan)
             for (uint32_t l = 0; l < nlist; ++l) {
-                own[l] = plan[l] == hdr[3];
-                if (cnt[l] && stored[l] != (own[l] ? cnt[l] : 0)) refuse("shard file lists differ from the LPT plan");
+                if (stored[l] != 0 && stored[l] != cnt[l]) refuse("shard file stores part of a list");
+                own[l] = cnt[l] != 0 && stored[l] == cnt[l];
             }
         }
         HIPCHECK(hipMemcpy2DAsync(cent_rm.p, dp * 4, c.data(), dim * 4, dim * 4, nlist, hipMemcpyHostToDevice, stream));
@@ -1376,11 +1387,17 @@ struct vdb_ivf {
         upload_directory();  // also waits for the stream before tmp buffers go
     }
 
-    void set_shard(uint32_t r, uint32_t w) {
+    // owner: the plan (every list's rank), identical on every rank; null = the LPT plan
+    // of vdb_shard_plan over the current list sizes.
+    void set_shard(uint32_t r, uint32_t w, const uint32_t* owner_in = nullptr) {
         std::vector<uint32_t> owner(nlist);
-        vdb_shard_plan(count.data(), nlist, w, owner.data());
+        if (owner_in) std::copy(owner_in, owner_in + nlist, owner.begin());
+        else vdb_shard_plan(count.data(), nlist, w, owner.data());
         std::vector<uint8_t> new_owned(nlist);
-        for (uint32_t l = 0; l < nlist; ++l) new_owned[l] = owner[l] == r;
+        for (uint32_t l = 0; l < nlist; ++l) {
+            require(owner[l] < w, "shard plan names a rank outside the world");
+            new_owned[l] = owner[l] == r;
+        }
         // Lists this handle no longer scans must have been stored here before.
         for (uint32_t l = 0; l < nlist; ++l)
             require(!new_owned[l] || owned[l] || count[l] == 0, "shard needs a list this handle dropped", VDB_ERR_STATE);
@@ -1411,17 +1428,44 @@ struct vdb_ivf {
     // list sizes (from an assignment pass) fix this handle's lists before any add, so
     // appends store only the owned lists' rows and count the rest. The plan is the same
     // LPT as set_shard, so a later set_shard(r, w) keeps the same lists.
-    void plan_shard(uint32_t r, uint32_t w, const uint64_t* final_sizes) {
+    void plan_shard(uint32_t r, uint32_t w, const uint64_t* final_sizes, const uint32_t* owner_in = nullptr) {
         require(total == 0, "plan_shard needs an empty index (call it between train and add)", VDB_ERR_STATE);
         require(!file_home(), "lists are served from a file (vdb_ivf_open_lists)", VDB_ERR_STATE);
         std::vector<uint32_t> owner(nlist);
-        vdb_shard_plan(final_sizes, nlist, w, owner.data());
+        if (owner_in) std::copy(owner_in, owner_in + nlist, owner.begin());
+        else vdb_shard_plan(final_sizes, nlist, w, owner.data());
         std::vector<uint8_t> new_owned(nlist);
-        for (uint32_t l = 0; l < nlist; ++l) new_owned[l] = owner[l] == r;
+        for (uint32_t l = 0; l < nlist; ++l) {
+            require(owner[l] < w, "shard plan names a rank outside the world");
+            new_owned[l] = owner[l] == r;
+        }
         relayout(count, new_owned);
         rank = r;
         world = w;
         upload_directory();
+    }
+
+    // Probe census for a probe-weighted shard plan: counts[l] += how many of the n device
+    // rows (a query-like sample) probe list l, by the exact probe selection of search.
+    void probe_census(const float* d_rows, uint64_t n, uint32_t nprobe, uint64_t* counts) {
+        const uint32_t P = std::min(nprobe, nlist);
+        if (n == 0 || P == 0) return;
+        quiesce();
+        SearchSlot w;
+        const uint32_t bmax = batch_cap(P);
+        ensure_workspace(w, (uint32_t)std::min<uint64_t>(bmax, n), P, 1);
+        DevBuf<uint32_t> d_counts;
+        HIPCHECK(hipMemsetAsync(d_counts.ensure(nlist), 0, nlist * 4, stream));
+        for (uint64_t b0 = 0; b0 < n; b0 += bmax) {
+            const uint32_t B = (uint32_t)std::min<uint64_t>(bmax, n - b0);
+            coarse_batch(w, d_rows + b0 * dim, B, P, stream);
+            vdbk::launch_histogram(w.probes.p, (uint64_t)B * P, d_counts.p, stream);
+            HIPCHECK(hipGetLastError());
+        }
+        std::vector<uint32_t> h(nlist);
+        HIPCHECK(hipMemcpyAsync(h.data(), d_counts.p, nlist * 4, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        for (uint32_t l = 0; l < nlist; ++l) counts[l] += h[l];
     }
 
     EventSet& next_events() {
@@ -1445,7 +1489,8 @@ struct vdb_ivf {
         const bool grow = w.items_w.cap < max_wide || w.qpad.cap < (size_t)B * dp || w.cd.cap < (size_t)B * nlist ||
                           w.cdelta.cap < (size_t)B * nlist || w.cand.cap < (size_t)B * nlist ||
                           w.probes.cap < BP || w.thr.cap < BP || w.items.cap < max_items || w.part_d.cap < max_items * k ||
-                          w.slot_d.cap < BP * k || w.carry_d.cap < (size_t)P * k || w.l1_items.cap < max_l1 ||
+                          w.slot_d.cap < BP * k || w.carry_d.cap < (size_t)P * k || w.carry2_d.cap < (size_t)P * k ||
+                          w.l1_items.cap < max_l1 ||
                           w.l1_d.cap < max_l1 * k;
         if (!grow) return;
         if (w.used) HIPCHECK(hipEventSynchronize(w.done));
@@ -1472,20 +1517,35 @@ struct vdb_ivf {
         w.slot_i.ensure(BP * k);
         w.carry_d.ensure((size_t)P * k);
         w.carry_i.ensure((size_t)P * k);
+        w.carry2_d.ensure((size_t)P * k);
+        w.carry2_i.ensure((size_t)P * k);
     }
 
     // ---- search: ivf_flat_index.cpp:205-256, one batch of B queries ----
+    // The batch's queries as the kernels read them, zero-padded rows [B][dp]: when dim is
+    // already a multiple of the padding (768) the caller's rows are used in place (they
+    // stay valid until the stream passes the search, as for any asynchronous call), else
+    // a padded copy in w.qpad.
+    void stage_queries(SearchSlot& w, const float* d_q, uint32_t B, hipStream_t s) {
+        if (dim == dp && ((uintptr_t)d_q & 15) == 0) {  // (rows are read as float4)
+            w.q = d_q;
+            return;
+        }
+        vdbk::launch_pad_rows(d_q, B, dim, dp, w.qpad.p, s);
+        w.q = w.qpad.p;
+    }
+
     // Coarse step (select_nprobe_lists, cpp:298-336): padded queries into w.qpad, the
     // first min(nprobe, nlist) lists by (dist, list) into w.probes.
     void coarse_batch(SearchSlot& w, const float* d_q, uint32_t B, uint32_t P, hipStream_t s) {
         const int regs_p = vdbk::topk_regs(P);
-        vdbk::launch_pad_rows(d_q, B, dim, dp, w.qpad.p, s);
+        stage_queries(w, d_q, B, s);
         if (coarse_mode == 1 && metric != 2 && vdbk::rerank_rows(dp, regs_p) > 0) {
-            vdbk::launch_coarse_mfma(metric, cent_rm.p, nlist, dp, w.qpad.p, B, w.cd.p, w.cdelta.p, s);
-            vdbk::launch_select_rerank(metric, regs_p, w.cd.p, w.cdelta.p, cent_rm.p, nlist, dp, w.qpad.p, B, P,
+            vdbk::launch_coarse_mfma(metric, cent_rm.p, nlist, dp, w.q, B, w.cd.p, w.cdelta.p, s);
+            vdbk::launch_select_rerank(metric, regs_p, w.cd.p, w.cdelta.p, cent_rm.p, nlist, dp, w.q, B, P,
                                        w.cand.p, w.probes.p, s);
         } else {
-            vdbk::launch_coarse(metric, cent_il.p, nlist, d4, w.qpad.p, B, w.cd.p, s);
+            vdbk::launch_coarse(metric, cent_il.p, nlist, d4, w.q, B, w.cd.p, s);
             vdbk::launch_select(regs_p, w.cd.p, nlist, B, P, w.probes.p, s);
         }
     }
@@ -1514,13 +1574,25 @@ struct vdb_ivf {
         vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? (int)wide_group : 0, segs_item, w.items.p, w.items_w.p,
                           w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, w.thr.p,
                           mfma_min, s);
+        const bool in_ring = &w >= slots && &w < slots + kSlots;
+        if (scan_window && in_ring && scan_seq >= scan_window) {  // the scan issued scan_window batches ago
+            const SearchSlot& prev = slots[scan_hist[(scan_seq - scan_window) % 8]];
+            if (prev.scan_done) HIPCHECK(hipStreamWaitEvent(s, prev.scan_done, 0));
+        }
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
-        vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.qpad.p, w.items.p, w.items_w.p,
+        vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.q, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
                                 wide_stride, w.counters.p + 4, seg_blocks, segs_item, 0, w.thr.p,
                                 mfma_min, bounded_stats ? stats.p + 5 : nullptr};
         // the bounded items first (the batch's most-probed lists), on the same stream
         if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
+        // SGPR queries: each wide group's pairs staged once per batch for scalar loads
+        const float* qstage = nullptr;
+        if (wide && sgpr_queries && waves == 4 && !mfma_min && vdbk::scan_sq_fits(d4)) {
+            float* st = slot_buf(w, w.qstage, (size_t)BP * d4 * 8 + 64);
+            vdbk::launch_stage_pairs((uint32_t)max_wide, w.items_w.p, w.counters.p, w.sorted_pair.p, w.q, d4, st, s);
+            qstage = st;
+        }
         if (wide && fused_scan) {
             // one persistent grid takes both queues (no side stream, no fork/join)
             // (narrow_blocks counts 4-wave workgroups: as many waves start on the narrow queue)
@@ -1528,7 +1600,7 @@ struct vdb_ivf {
             sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks * 4 / waves, grid_cap / 2));
             const uint64_t want = std::max<uint64_t>(max_wide, (max_items + 3) / 4);
             vdbk::launch_scan_wide(metric, (uint32_t)(scan_blocks ? std::min<uint64_t>(want, scan_blocks) : want), sa, s,
-                                   waves);
+                                   waves, qstage);
         } else if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));
@@ -1536,12 +1608,32 @@ struct vdb_ivf {
             vdbk::launch_scan_narrow(metric, regs_k, std::min<uint32_t>((uint32_t)((max_items + 3) / 4), narrow_blocks), sa,
                                      w.side);
             HIPCHECK(hipEventRecord(w.join, w.side));
-            vdbk::launch_scan_wide(metric, (uint32_t)max_wide, sa, s, waves);
+            vdbk::launch_scan_wide(metric, (uint32_t)max_wide, sa, s, waves, qstage);
             HIPCHECK(hipStreamWaitEvent(s, w.join, 0));
         } else {
             vdbk::launch_scan_narrow(metric, regs_k, (uint32_t)((max_items + 3) / 4), sa, s);
         }
         if (ev) HIPCHECK(hipEventRecord(ev->scan_end, s));
+        if (scan_window && in_ring) {
+            if (!w.scan_done) HIPCHECK(hipEventCreateWithFlags(&w.scan_done, hipEventDisableTiming));
+            HIPCHECK(hipEventRecord(w.scan_done, s));
+            scan_hist[scan_seq % 8] = (int)(&w - slots);
+            ++scan_seq;
+        }
+        if (fused_merge) {
+            // one launch: slot folds, stale sources, unique top-k, the next batch's carry
+            float* cd0 = w.carry_sel ? w.carry2_d.p : w.carry_d.p;
+            uint64_t* ci0 = w.carry_sel ? w.carry2_i.p : w.carry_i.p;
+            float* cd1 = w.carry_sel ? w.carry_d.p : w.carry2_d.p;
+            uint64_t* ci1 = w.carry_sel ? w.carry_i.p : w.carry2_i.p;
+            vdbk::launch_merge_fused(regs_k, w.probes.p, d_count_global.p, w.nseg_qp.p, w.pbqp.p, w.part_d.p, w.part_i.p, B,
+                                     P, k, stale, req_start, b0, cd0, ci0, w.slot_d.p, w.slot_i.p, cd1, ci1, out_d_, out_i_,
+                                     s);
+            if (stale) w.carry_sel ^= 1u;
+            if (ev) HIPCHECK(hipEventRecord(ev->end, s));
+            HIPCHECK(hipGetLastError());
+            return;
+        }
         vdbk::launch_merge_partials(regs_k, (uint32_t)max_l1, w.probes.p, d_count_global.p, w.nseg_qp.p, w.pbqp.p, w.l1base.p,
                                     w.l1_items.p, w.counters.p, w.part_d.p, w.part_i.p, k, w.l1_d.p, w.l1_i.p, s);
         vdbk::launch_slot_merge(regs_k, w.probes.p, d_count_global.p, w.nseg_qp.p, w.pbqp.p, w.l1base.p, w.part_d.p, w.part_i.p,
@@ -1667,7 +1759,7 @@ struct vdb_ivf {
             for (uint32_t l : U[b]) last_use[l] = use_tick;
             EventSet* ev = prof ? &next_events() : nullptr;
             if (ev) HIPCHECK(hipEventRecord(ev->begin, s));
-            vdbk::launch_pad_rows(d_q + (size_t)b0 * dim, B, dim, dp, w.qpad.p, s);
+            stage_queries(w, d_q + (size_t)b0 * dim, B, s);
             HIPCHECK(hipMemcpyAsync(w.probes.p, hp + (size_t)b0 * P, (size_t)B * P * 4, hipMemcpyHostToDevice, s));
             if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
             scan_batch(w, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s, req_start, b0, ev);
@@ -1728,6 +1820,7 @@ struct vdb_ivf {
         }
         if (w.used) HIPCHECK(hipStreamWaitEvent(s, w.done, 0));
         HIPCHECK(hipMemsetAsync(w.carry_i.p, 0xFF, (size_t)P * k * 8, s));
+        w.carry_sel = 0;
         return w;
     }
 

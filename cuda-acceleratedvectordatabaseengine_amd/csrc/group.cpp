@@ -484,15 +484,28 @@ int vdb_ivf_attach_comm(vdb_ivf* h, const void* id, uint32_t rank, uint32_t worl
             if (!c) throw VdbError(VDB_ERR_DEVICE, h->rank_tag() + "ncclCommInitRankConfig returned no communicator");
             h->nccl_settle(r, "communicator init (ncclCommInitRankConfig)");
             h->make_comm_stream();
-            // Every rank must run the same collectives: compare the settings that decide
-            // them (one all-gather, which also proves the communicator end to end).
-            uint64_t mine[4] = {((uint64_t)h->dim << 32) | h->nlist, ((uint64_t)h->metric << 32) | h->batch,
-                                (uint64_t)h->tiered(), (uint64_t)h->stale};
+            // Every rank must run the same collectives and hold a disjoint part of one index:
+            // compare the settings that decide the collectives and the global list sizes,
+            // and check that every non-empty list is stored by exactly one rank (one
+            // all-gather, which also proves the communicator end to end).
+            const uint32_t nw = (h->nlist + 63) / 64;
+            const size_t words = 5 + nw;
+            std::vector<uint64_t> mine(words, 0);
+            uint64_t fnv = 1469598103934665603ull;  // FNV-1a of the global list sizes
+            for (uint32_t l = 0; l < h->nlist; ++l) {
+                fnv = (fnv ^ h->count[l]) * 1099511628211ull;
+                if (h->owned[l] && h->count[l]) mine[5 + l / 64] |= 1ull << (l % 64);
+            }
+            mine[0] = ((uint64_t)h->dim << 32) | h->nlist;
+            mine[1] = ((uint64_t)(uint32_t)h->metric << 32) | h->batch;
+            mine[2] = ((uint64_t)h->tiered() << 1) | (uint64_t)h->stale;
+            mine[3] = fnv;
+            mine[4] = h->total;
             DevBuf<uint64_t> dm, dall;
-            HIPCHECK(hipMemcpyAsync(dm.ensure(4), mine, sizeof(mine), hipMemcpyHostToDevice, h->comm_stream));
-            h->nccl_settle(ncclAllGather(dm.p, dall.ensure(4 * (size_t)world), 4, ncclUint64, c, h->comm_stream),
+            HIPCHECK(hipMemcpyAsync(dm.ensure(words), mine.data(), words * 8, hipMemcpyHostToDevice, h->comm_stream));
+            h->nccl_settle(ncclAllGather(dm.p, dall.ensure(words * world), words, ncclUint64, c, h->comm_stream),
                            "settings all-gather at attach");
-            std::vector<uint64_t> all(4 * (size_t)world);
+            std::vector<uint64_t> all(words * (size_t)world);
             HIPCHECK(hipMemcpyAsync(all.data(), dall.p, all.size() * 8, hipMemcpyDeviceToHost, h->comm_stream));
             const auto t0 = std::chrono::steady_clock::now();
             for (;;) {  // the deadline holds for the first collective too
@@ -507,10 +520,26 @@ int vdb_ivf_attach_comm(vdb_ivf* h, const void* id, uint32_t rank, uint32_t worl
                 std::this_thread::sleep_for(std::chrono::microseconds(200));
             }
             for (uint32_t q = 0; q < world; ++q)
-                require(std::equal(mine, mine + 4, all.data() + 4 * (size_t)q),
+                require(std::equal(mine.begin(), mine.begin() + 5, all.begin() + words * q),
                         h->rank_tag() + "rank " + std::to_string(q) +
-                            " differs in dimension, nlist, metric, batch, list-cache tier or stale_slots",
+                            " differs in dimension, nlist, metric, batch, list-cache tier, stale_slots or list sizes",
                         VDB_ERR_STATE);
+            for (uint32_t wd = 0; wd < nw; ++wd) {
+                uint64_t any = 0, twice = 0;
+                for (uint32_t q = 0; q < world; ++q) {
+                    const uint64_t b = all[words * q + 5 + wd];
+                    twice |= any & b;
+                    any |= b;
+                }
+                uint64_t nonempty = 0;
+                for (uint32_t l = wd * 64; l < std::min(h->nlist, (wd + 1) * 64); ++l)
+                    if (h->count[l]) nonempty |= 1ull << (l % 64);
+                require(!twice && any == nonempty,
+                        h->rank_tag() + "the ranks' shards do not partition the lists (list " +
+                            std::to_string(wd * 64 + __builtin_ctzll(twice ? twice : (any ^ nonempty))) +
+                            (twice ? " stored by two ranks)" : " stored by no rank)"),
+                        VDB_ERR_STATE);
+            }
         } catch (...) {
             if (h->comm) (void)ncclCommAbort(h->comm);
             h->comm = nullptr;

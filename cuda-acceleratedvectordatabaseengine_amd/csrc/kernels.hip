@@ -1078,7 +1078,7 @@ __device__ __forceinline__ void stream_blocks(const float4* __restrict__ base, c
             static_for<0, T>([&](auto u) {
                 constexpr int t = decltype(u)::value;
                 compute(x[t], t0 + t, u);
-                x[t] = load_nt(p + (size_t)(T + t) * 64);
+                if (!(VDB_SCAN_DIAG & 32)) x[t] = load_nt(p + (size_t)(T + t) * 64);  // (DIAGNOSTIC 32: no list reads)
             });
             p += (size_t)T * 64;
         }
@@ -1303,8 +1303,10 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
             for (int p = 0; p < GP; ++p) {
                 const float4 lo = qb[p][0], hi = qb[p][1];
                 pair_terms(p, lo, hi, xlo, xhi, x);
-                qb[p][0] = nxt[2 * p];
-                qb[p][1] = nxt[2 * p + 1];
+                if (!(VDB_SCAN_DIAG & 16)) {  // (DIAGNOSTIC 16: no LDS reads of query pairs in the loop)
+                    qb[p][0] = nxt[2 * p];
+                    qb[p][1] = nxt[2 * p + 1];
+                }
             }
         }
     };
@@ -1574,6 +1576,200 @@ __device__ __forceinline__ void scan_wide_wave_mfma(const ScanArgs& a, const Sca
     }
 }
 
+// ============================================================================
+// SGPR-query wide wave (option sgpr_queries): the arithmetic and the item semantics of
+// scan_wide_wave (exact sums in d order, two queries per packed op, shared thresholds),
+// but the query pairs come from SGPRs instead of LDS. Every wave reads the same
+// (wave-uniform) query values, so a per-lane broadcast read from LDS moves 64x the
+// bytes it uses (16 ds_read_b128 = 64 LDS cycles per tile per wave at 8 pairs); a
+// scalar load moves them once. ivf_stage_pairs writes each wide group's pairs
+// tile-major to qstage ([d4][GP][8 floats] at pair_start * d4 * 8); per tile the wave
+// holds them in ceil(GP / 2) blocks of 16 SGPRs (s_load_dwordx16), each reloaded with
+// the next tile's block right after its last use, so a load has three quarters of a
+// tile of arithmetic to land in. The freed query VGPRs deepen the list stream:
+// T tiles (kSqTiles) in flight per lane instead of 16.
+// ============================================================================
+#ifndef VDB_SQ_TILES
+#define VDB_SQ_TILES 32
+#endif
+constexpr int kSqTiles = VDB_SQ_TILES;
+typedef float v16q __attribute__((ext_vector_type(16)));
+
+template <int H>
+__device__ __forceinline__ f2 pk_sub_bcast_s(f2 q, f2 x) {
+    f2 r;
+    if constexpr (H == 0)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "s"(q), "v"(x));
+    else
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "s"(q), "v"(x));
+    return r;
+}
+template <int H>
+__device__ __forceinline__ f2 pk_mul_bcast_s(f2 q, f2 x) {
+    f2 r;
+    if constexpr (H == 0)
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "s"(q), "v"(x));
+    else
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "s"(q), "v"(x));
+    return r;
+}
+template <int M, int H>
+__device__ __forceinline__ f2 dist_term2_s(f2 acc, f2 q, f2 x) {
+    if constexpr (M == kL2) {
+        const f2 diff = pk_sub_bcast_s<H>(q, x);
+        return acc + diff * diff;
+    } else if constexpr (M == kIP) {
+        return acc + pk_mul_bcast_s<H>(q, x);
+    } else {
+        return acc;
+    }
+}
+
+template <int GP, int M, bool ODD>
+__device__ __forceinline__ void scan_wide_wave_sq(const ScanArgs& a, const ScanItem it, const float* __restrict__ qs,
+                                                  const int np, float* tk_d, uint64_t* tk_i, uint32_t* s_thr,
+                                                  const uint32_t seg) {
+    constexpr int G = 2 * GP;
+    constexpr int NQ = (GP + 1) / 2;  // 16-SGPR blocks (two pairs) per tile
+    const uint32_t d4 = a.d4;
+    const int lane = lane_id();
+    const uint32_t count = a.count[it.list];
+    const uint32_t seg_vectors = a.seg_blocks * 64;
+    const uint64_t b0 = a.block_off[it.list] + (uint64_t)seg * a.seg_blocks;
+    const uint32_t v0 = seg * seg_vectors;
+    const uint32_t nv = min(count - v0, seg_vectors);
+    const uint32_t nb = (nv + 63) >> 6;
+    const int k = (int)a.k;
+
+    for (int e = lane; e < G * k; e += 64) {
+        tk_d[e] = __builtin_inff();
+        tk_i[e] = kNoId;
+    }
+    float kd[G];
+    f2 acc[GP];
+    float acc1 = 0.0f;  // ODD: the single query of the last pair
+#pragma unroll
+    for (int g = 0; g < G; ++g) kd[g] = __builtin_inff();
+#pragma unroll
+    for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
+    auto qsum = [&](int g) -> float {
+        if (ODD && g == 2 * (GP - 1)) return acc1;
+        return (g & 1) ? acc[g >> 1].y : acc[g >> 1].x;
+    };
+    // pair p's four terms of one tile; q8 = (qa.x, qb.x, qa.y, qb.y, qa.z, qb.z, qa.w, qb.w)
+    auto pair_terms = [&](int p, f2 q01, f2 q23, f2 q45, f2 q67, const f2 xlo, const f2 xhi, const float4 x) {
+        if (ODD && p == GP - 1) {  // query 2p alone: the low halves
+            acc1 = dist_term<M>(acc1, q01.x, x.x);
+            acc1 = dist_term<M>(acc1, q23.x, x.y);
+            acc1 = dist_term<M>(acc1, q45.x, x.z);
+            acc1 = dist_term<M>(acc1, q67.x, x.w);
+        } else {
+            acc[p] = dist_term2_s<M, 0>(acc[p], q01, xlo);
+            acc[p] = dist_term2_s<M, 1>(acc[p], q23, xlo);
+            acc[p] = dist_term2_s<M, 0>(acc[p], q45, xhi);
+            acc[p] = dist_term2_s<M, 1>(acc[p], q67, xhi);
+        }
+    };
+    v16q qq[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) qq[j] = *(const v16q*)(qs + (size_t)(2 * j) * 8);
+    auto compute = [&](const float4 x, uint32_t t, auto) {
+        const f2 xlo = {x.x, x.y}, xhi = {x.z, x.w};
+        const float* nxt = qs + (size_t)(t + 1 == d4 ? 0 : t + 1) * GP * 8;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+            const v16q q = qq[j];
+            pair_terms(2 * j, f2{q[0], q[1]}, f2{q[2], q[3]}, f2{q[4], q[5]}, f2{q[6], q[7]}, xlo, xhi, x);
+            if (2 * j + 1 < GP)
+                pair_terms(2 * j + 1, f2{q[8], q[9]}, f2{q[10], q[11]}, f2{q[12], q[13]}, f2{q[14], q[15]}, xlo, xhi,
+                           x);
+            qq[j] = *(const v16q*)(nxt + (size_t)(2 * j) * 8);
+        }
+    };
+    auto finish = [&](uint32_t j, uint64_t id) {
+        const bool valid = j * 64 + lane < nv;
+        float th[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) th[g] = g < np ? fminf(kd[g], ord_dec(s_thr[g])) : kd[g];
+        uint32_t pend = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float dist = dist_finish<M>(qsum(g));
+            if (g < np && __ballot(valid && dist <= th[g])) pend |= 1u << g;
+        }
+        if (VDB_SCAN_DIAG & 1) pend = 0;  // DIAGNOSTIC: no top-k maintenance (results invalid)
+        if (pend) {
+            const uint64_t vid = valid ? id : kNoId;
+            do {
+                const int gs = __builtin_ctz(pend);
+                pend &= pend - 1;
+                float dist = 0.0f, kdg = 0.0f;
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    if (g == gs) {
+                        dist = dist_finish<M>(qsum(g));
+                        kdg = th[g];
+                    }
+                float* sd = tk_d + gs * k;
+                uint64_t* si = tk_i + gs * k;
+                WaveTopK<1> tk;
+                tk.d[0] = lane < k ? sd[lane] : __builtin_inff();
+                tk.id[0] = lane < k ? si[lane] : kNoId;
+                float nkd;
+                uint64_t nki;
+                tk.at(k - 1, nkd, nki);
+                offer_lanes<1>(tk, valid && dist <= kdg, dist, vid, k, nkd, nki);
+                if (lane < k) {
+                    sd[lane] = tk.d[0];
+                    si[lane] = tk.id[0];
+                }
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    if (g == gs) kd[g] = nkd;
+                if (nkd < kdg && lane == 0) atomicMin(&s_thr[gs], ord_enc(nkd));
+            } while (pend);
+        }
+#pragma unroll
+        for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
+        acc1 = 0.0f;
+    };
+    stream_blocks<kSqTiles>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+        if (g < np && lane == 0 && kd[g] < __builtin_inff()) atomicMin(&a.thr[it.pair_start + g], ord_enc(kd[g]));
+    for (int g = 0; g < np; ++g) {
+        const uint32_t part = a.part_base_sorted[it.pair_start + g] + seg;
+        if (lane < k) {
+            a.part_d[(size_t)part * k + lane] = tk_d[g * k + lane];
+            a.part_i[(size_t)part * k + lane] = tk_i[g * k + lane];
+        }
+    }
+}
+
+// Each wide group's query pairs, tile-major, for the SGPR-query scan: one workgroup per
+// group (its first segment range's item), [d4][GP][8 floats] at qstage + pair_start * d4 * 8.
+__global__ __launch_bounds__(256) void ivf_stage_pairs(const ScanItem* __restrict__ items_w,
+                                                      const uint32_t* __restrict__ counters,
+                                                      const uint32_t* __restrict__ sorted_pair,
+                                                      const float* __restrict__ qpad, uint32_t d4,
+                                                      float* __restrict__ qstage) {
+    const uint32_t n = counters[3] + counters[7];
+    for (uint32_t idx = blockIdx.x; idx < n; idx += gridDim.x) {
+        const ScanItem it = items_w[idx];
+        if (it.seg != 0) continue;
+        const int np = (int)it.npairs, gp = (np + 1) / 2;
+        float4* dst = (float4*)(qstage + (size_t)it.pair_start * d4 * 8);
+        for (uint32_t e = threadIdx.x; e < (uint32_t)gp * d4; e += blockDim.x) {
+            const uint32_t t = e / gp, p = e - t * gp;
+            const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
+            const float4 qa = ((const float4*)(qpad + (size_t)(sorted_pair[it.pair_start + ga] >> 16) * d4 * 4))[t];
+            const float4 qb = ((const float4*)(qpad + (size_t)(sorted_pair[it.pair_start + gb] >> 16) * d4 * 4))[t];
+            dst[(t * gp + p) * 2 + 0] = make_float4(qa.x, qb.x, qa.y, qb.y);
+            dst[(t * gp + p) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
+        }
+    }
+}
+
 // One wave-item of a narrow list (<= 4 pairs of one segment).
 template <int R, int M>
 __device__ __forceinline__ void scan_narrow(const ScanArgs& a, const ScanItem it) {
@@ -1629,8 +1825,10 @@ __device__ __forceinline__ void drain_narrow(const ScanArgs& a) {
 //    its half of the queries: the two waves streaming one segment run side by side on
 //    the CU, so the second read is served on-chip, and every wave keeps at most 8 query
 //    pairs in registers (the code path that does not spill).
-template <int M, int W>
-__global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
+// SQ (W = 4): the query pairs come from qstage through SGPRs (scan_wide_wave_sq), not
+// from LDS; qstage is a kernel argument of its own so its loads are scalar.
+template <int M, int W, bool SQ>
+__global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a, const float* __restrict__ qstage) {
     constexpr int GW = 4 * W;  // queries per item at most
     // Dynamic LDS: [d4][gpv][2] float4 of staged query pairs (tile-major), then per wave
     // kWaveQueries x k top-k ids (u64), then the same for distances (f32).
@@ -1671,7 +1869,7 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
         if (threadIdx.x < 2) s_seg[threadIdx.x] = 0;  // visible after the staging barrier below
         if (threadIdx.x < (uint32_t)np) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
         const int gpv = (VDB_SCAN_DIAG & 2) ? 1 : gp;  // (DIAGNOSTIC diag&2: one pair only, results invalid)
-        for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
+        for (uint32_t e = threadIdx.x; !SQ && e < (uint32_t)gpv * d4; e += blockDim.x) {
             const uint32_t t = e / gpv, p = e - t * gpv;
             const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
             const float4 qa = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + ga] >> 16) * d4 * 4))[t];
@@ -1700,6 +1898,20 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
             if (lane_id() == 0) sg = atomicAdd(&s_seg[half], 1u);
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
+            if constexpr (SQ) {
+                const float* qs = qstage + (size_t)it.pair_start * d4 * 8;
+#define VDB_WS(GPN)                                                                                     \
+    case GPN:                                                                                           \
+        if (kOddPairs && (nq & 1)) scan_wide_wave_sq<GPN, M, true>(a, it, qs, nq, tk_d, tk_i, s_thr, sg); \
+        else scan_wide_wave_sq<GPN, M, false>(a, it, qs, nq, tk_d, tk_i, s_thr, sg);                      \
+        break;
+                switch (gw) {
+                    VDB_WS(1) VDB_WS(2) VDB_WS(3) VDB_WS(4) VDB_WS(5) VDB_WS(6) VDB_WS(7)
+                    default: VDB_WS(8)
+                }
+#undef VDB_WS
+                continue;
+            }
 #define VDB_WW(GPN)                                                                       \
     case GPN:                                                                             \
         if (W == 8 && split) scan_wide_wave<GPN, M, true, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg); \
@@ -2089,6 +2301,119 @@ __global__ __launch_bounds__(256) void ivf_merge_ranks(const float* __restrict__
     for (uint32_t r = 0; r < nranks; ++r)
         offer_slot_unique<R>(tk, d + r * d_stride + (size_t)q * k, ids + r * i_stride + (size_t)q * k, k, kd, ki);
     write_final<R>(tk, k, out_d + (size_t)q * k, out_i + (size_t)q * k);
+}
+
+// ============================================================================
+// Fused batch merge (one workgroup of min(16, P) waves per query): the work of ivf_merge_partials,
+// ivf_merge_slots, ivf_merge_query and ivf_carry_slots in ONE launch.
+//  1. Each wave takes probes p = wave, wave + waves, ... and writes the query's EFFECTIVE
+//     slot p into slot_d/i[q][p]: its own list's top-min(k, n_l) folded from all the
+//     segment partials of that (query, probe) pair (search_list_cpu's partial_sort,
+//     cpp:368-377), or, for an empty probed list (quirk A1, cpp:210-233), the same fold
+//     for the nearest earlier query of its request whose probe p is non-empty —
+//     recomputed from that pair's partials, the same bits that query's slot holds —
+//     else the call's carried slot, else nothing.
+//  2. After the workgroup barrier, wave 0 merges the P slots into the unique-id top-k
+//     (merge_results, cpp:474-518).
+//  3. The batch's last query's workgroup writes its effective slots — the last content
+//     of every slot — as the carry of the call's next batch, into the other carry buffer
+//     (ping-pong: other workgroups of this batch may still read the current one).
+// ============================================================================
+template <int R>
+__device__ __forceinline__ void fold_pair_slot(uint32_t i, const uint32_t* __restrict__ probes,
+                                               const uint32_t* __restrict__ count_global,
+                                               const uint32_t* __restrict__ nseg_qp,
+                                               const uint32_t* __restrict__ part_base_qp,
+                                               const float* __restrict__ part_d, const uint64_t* __restrict__ part_i,
+                                               uint32_t k, float* __restrict__ od, uint64_t* __restrict__ oi) {
+    const int lane = lane_id();
+    const uint32_t ns = nseg_qp[i];
+    const size_t base = (size_t)part_base_qp[i] * k;
+    if (ns <= 1) {  // not stored here (or empty): nothing; one segment: its partial is the list's top-k
+        for (uint32_t e = lane; e < k; e += 64) {
+            od[e] = ns ? part_d[base + e] : __builtin_inff();
+            oi[e] = ns ? part_i[base + e] : kNoId;
+        }
+        return;
+    }
+    const int kk = (int)min(k, count_global[probes[i]]);
+    WaveTopK<R> tk;
+    tk.init();
+    float kd = __builtin_inff();
+    uint64_t ki = kNoId;
+    offer_array<R, false>(tk, part_d + base, part_i + base, ns * k, kk, kd, ki);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = r * 64 + lane;
+        if (e < (int)k) {
+            od[e] = e < kk ? tk.d[r] : __builtin_inff();
+            oi[e] = e < kk ? tk.id[r] : kNoId;
+        }
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(1024) void ivf_merge_fused(const uint32_t* __restrict__ probes,
+                                                     const uint32_t* __restrict__ count_global,
+                                                     const uint32_t* __restrict__ nseg_qp,
+                                                     const uint32_t* __restrict__ part_base_qp,
+                                                     const float* __restrict__ part_d,
+                                                     const uint64_t* __restrict__ part_i, uint32_t B, uint32_t P,
+                                                     uint32_t k, int stale, const uint32_t* __restrict__ req_start,
+                                                     uint32_t b0, const float* __restrict__ carry_d,
+                                                     const uint64_t* __restrict__ carry_i, float* __restrict__ slot_d,
+                                                     uint64_t* __restrict__ slot_i, float* __restrict__ carry_nd,
+                                                     uint64_t* __restrict__ carry_ni, float* __restrict__ out_d,
+                                                     uint64_t* __restrict__ out_i) {
+    const uint32_t q = blockIdx.x;
+    const uint32_t wv = wave_index();
+    const int lane = lane_id();
+    // the query's request (coalesced calls; null = one request): stale lookups never cross it
+    const uint32_t qs = req_start ? req_start[b0 + q] : 0u;
+    const uint32_t q_lo = qs > b0 ? qs - b0 : 0u;
+    const bool carry_ok = qs < b0 || b0 == 0;
+    const uint32_t nwaves = blockDim.x >> 6;  // (up to 16: a query's slots fold in parallel)
+    for (uint32_t p = wv; p < P; p += nwaves) {
+        float* od = slot_d + ((size_t)q * P + p) * k;
+        uint64_t* oi = slot_i + ((size_t)q * P + p) * k;
+        uint32_t src = q;
+        bool have = count_global[probes[(size_t)q * P + p]] > 0;
+        if (!have && stale) {
+            for (uint32_t q2 = q; q2 > q_lo;) {
+                --q2;
+                if (count_global[probes[(size_t)q2 * P + p]] > 0) {
+                    src = q2;
+                    have = true;
+                    break;
+                }
+            }
+        }
+        if (have) {
+            fold_pair_slot<R>(src * P + p, probes, count_global, nseg_qp, part_base_qp, part_d, part_i, k, od, oi);
+        } else {
+            const bool from_carry = stale && carry_ok;
+            for (uint32_t e = lane; e < k; e += 64) {
+                od[e] = from_carry ? carry_d[(size_t)p * k + e] : __builtin_inff();
+                oi[e] = from_carry ? carry_i[(size_t)p * k + e] : kNoId;
+            }
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (wv == 0) {
+        WaveTopK<R> tk;
+        tk.init();
+        float kd = __builtin_inff();
+        uint64_t ki = kNoId;
+        offer_array<R, true>(tk, slot_d + (size_t)q * P * k, slot_i + (size_t)q * P * k, P * k, (int)k, kd, ki);
+        write_final<R>(tk, k, out_d + (size_t)q * k, out_i + (size_t)q * k);
+    }
+    if (stale && q + 1 == B) {  // the carry of the call's next batch
+        for (uint32_t e = threadIdx.x; e < P * k; e += blockDim.x) {
+            carry_nd[e] = slot_d[(size_t)q * P * k + e];
+            carry_ni[e] = slot_i[(size_t)q * P * k + e];
+        }
+    }
 }
 
 __global__ void ivf_fill_empty(uint64_t n, float* __restrict__ d, uint64_t* __restrict__ i) {
@@ -2520,14 +2845,16 @@ void launch_scan_bounded(int metric, uint32_t grid_blocks, const ScanArgs& a, hi
     else ivf_scan_bounded<kIP><<<g, 256, lds, s>>>(a);
 }
 
-void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves) {
+void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves,
+                      const float* qstage) {
     if (!grid_blocks) return;
     static const bool raised = [] {
         // wide items stage up to 16 (32) queries in LDS: allow the whole 160 KB of a CU
-        const void* f4[] = {(const void*)ivf_scan_wide<kL2, 4>, (const void*)ivf_scan_wide<kIP, 4>,
-                            (const void*)ivf_scan_wide<kCos, 4>};
-        const void* f8[] = {(const void*)ivf_scan_wide<kL2, 8>, (const void*)ivf_scan_wide<kIP, 8>,
-                            (const void*)ivf_scan_wide<kCos, 8>};
+        const void* f4[] = {(const void*)ivf_scan_wide<kL2, 4, false>, (const void*)ivf_scan_wide<kIP, 4, false>,
+                            (const void*)ivf_scan_wide<kCos, 4, false>, (const void*)ivf_scan_wide<kL2, 4, true>,
+                            (const void*)ivf_scan_wide<kIP, 4, true>, (const void*)ivf_scan_wide<kCos, 4, true>};
+        const void* f8[] = {(const void*)ivf_scan_wide<kL2, 8, false>, (const void*)ivf_scan_wide<kIP, 8, false>,
+                            (const void*)ivf_scan_wide<kCos, 8, false>};
         for (const void* f : f4)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes - wide_static_lds(4)));
         for (const void* f : f8)
@@ -2539,15 +2866,30 @@ void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipSt
     const size_t lds = scan_wide_lds(a.d4, a.k, waves);
     if (waves == 8) {  // one 8-wave workgroup per CU
         const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks / 2);
-        if (metric == kL2) ivf_scan_wide<kL2, 8><<<g, 512, lds, s>>>(a);
-        else if (metric == kIP) ivf_scan_wide<kIP, 8><<<g, 512, lds, s>>>(a);
-        else ivf_scan_wide<kCos, 8><<<g, 512, lds, s>>>(a);
+        if (metric == kL2) ivf_scan_wide<kL2, 8, false><<<g, 512, lds, s>>>(a, nullptr);
+        else if (metric == kIP) ivf_scan_wide<kIP, 8, false><<<g, 512, lds, s>>>(a, nullptr);
+        else ivf_scan_wide<kCos, 8, false><<<g, 512, lds, s>>>(a, nullptr);
         return;
     }
     const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
-    if (metric == kL2) ivf_scan_wide<kL2, 4><<<g, 256, lds, s>>>(a);
-    else if (metric == kIP) ivf_scan_wide<kIP, 4><<<g, 256, lds, s>>>(a);
-    else ivf_scan_wide<kCos, 4><<<g, 256, lds, s>>>(a);
+    if (qstage) {
+        if (metric == kL2) ivf_scan_wide<kL2, 4, true><<<g, 256, lds, s>>>(a, qstage);
+        else if (metric == kIP) ivf_scan_wide<kIP, 4, true><<<g, 256, lds, s>>>(a, qstage);
+        else ivf_scan_wide<kCos, 4, true><<<g, 256, lds, s>>>(a, qstage);
+        return;
+    }
+    if (metric == kL2) ivf_scan_wide<kL2, 4, false><<<g, 256, lds, s>>>(a, nullptr);
+    else if (metric == kIP) ivf_scan_wide<kIP, 4, false><<<g, 256, lds, s>>>(a, nullptr);
+    else ivf_scan_wide<kCos, 4, false><<<g, 256, lds, s>>>(a, nullptr);
+}
+
+bool scan_sq_fits(uint32_t d4) { return d4 % (uint32_t)kSqTiles == 0; }
+
+void launch_stage_pairs(uint32_t grid_items, const ScanItem* items_w, const uint32_t* counters,
+                        const uint32_t* sorted_pair, const float* qpad, uint32_t d4, float* qstage, hipStream_t s) {
+    if (!grid_items) return;
+    ivf_stage_pairs<<<std::min<uint32_t>(grid_items, 2048), 256, 0, s>>>(items_w, counters, sorted_pair, qpad, d4,
+                                                                         qstage);
 }
 
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const uint32_t* nseg_qp,
@@ -2589,6 +2931,24 @@ void launch_carry(const uint32_t* probes, const uint32_t* count_global, uint32_t
                   float* carry_d, uint64_t* carry_i, hipStream_t s) {
     if (!P || !B) return;
     ivf_carry_slots<<<P, 64, 0, s>>>(probes, count_global, B, P, k, slot_d, slot_i, req_start, b0, carry_d, carry_i);
+}
+
+void launch_merge_fused(int regs, const uint32_t* probes, const uint32_t* count_global, const uint32_t* nseg_qp,
+                        const uint32_t* part_base_qp, const float* part_d, const uint64_t* part_i, uint32_t B,
+                        uint32_t P, uint32_t k, int stale, const uint32_t* req_start, uint32_t b0, const float* carry_d,
+                        const uint64_t* carry_i, float* slot_d, uint64_t* slot_i, float* carry_nd, uint64_t* carry_ni,
+                        float* out_d, uint64_t* out_i, hipStream_t s) {
+    if (!B || !P) return;
+    const uint32_t threads = 64 * std::min<uint32_t>(16, P);
+#define VDB_MF(R) ivf_merge_fused<R><<<B, threads, 0, s>>>(probes, count_global, nseg_qp, part_base_qp, part_d, part_i, B, P, k, stale, req_start, b0, carry_d, carry_i, slot_d, slot_i, carry_nd, carry_ni, out_d, out_i)
+    switch (regs) {
+        case 1: VDB_MF(1); break;
+        case 2: VDB_MF(2); break;
+        case 4: VDB_MF(4); break;
+        case 8: VDB_MF(8); break;
+        default: VDB_MF(16); break;
+    }
+#undef VDB_MF
 }
 
 void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint64_t d_stride, uint64_t i_stride,

@@ -28,7 +28,9 @@ constexpr uint32_t kMergeBlocks = VDB_MERGE_BLOCKS;  // level-1 partial merge: w
 constexpr int kTilePipeNarrow = VDB_TILE_PIPE_NARROW;  // the same for narrow items (queries held in SGPRs)
 // Scan timing experiments (a separate build, tools/build_variant.sh; never a runtime option):
 // 1 skip top-k upkeep, 2 one query pair per wave, 4 no insertion on a segment's first block,
-// 8 insertions on its first block only. Every non-zero value makes search results INVALID.
+// 8 insertions on its first block only, 16 no LDS reads of query pairs in the wide loop (tile
+// 0's pairs reused), 32 no list reads in the loop (the first tiles reused). Every non-zero
+// value makes search results INVALID.
 #ifndef VDB_SCAN_DIAG
 #define VDB_SCAN_DIAG 0
 #endif
@@ -121,8 +123,16 @@ struct ScanArgs {
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);
 void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
-// waves 4: items of <= 16 queries, two workgroups per CU; 8: items of <= 32, one per CU
-void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves = 4);
+// waves 4: items of <= 16 queries, two workgroups per CU; 8: items of <= 32, one per CU.
+// qstage (waves 4): the wide groups' query pairs staged by launch_stage_pairs, read
+// through SGPRs instead of LDS (null: LDS staging per item).
+void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves = 4,
+                      const float* qstage = nullptr);
+// The SGPR-query wide scan streams kSqTiles tiles per lane: d4 must be a multiple.
+bool scan_sq_fits(uint32_t d4);
+// Per wide group, its query pairs tile-major ([d4][GP][8] floats at pair_start * d4 * 8).
+void launch_stage_pairs(uint32_t grid_items, const ScanItem* items_w, const uint32_t* counters,
+                        const uint32_t* sorted_pair, const float* qpad, uint32_t d4, float* qstage, hipStream_t s);
 // wide items of >= a.mfma_min queries (L2 / IP): bounded on the matrix cores, exact re-rank
 size_t scan_bounded_lds(uint32_t d4, uint32_t k);
 bool scan_bounded_fits(uint32_t d4, uint32_t k);
@@ -140,6 +150,14 @@ void launch_query_merge(int regs, const uint32_t* probes, const uint32_t* count_
 void launch_carry(const uint32_t* probes, const uint32_t* count_global, uint32_t B, uint32_t P, uint32_t k,
                   const float* slot_d, const uint64_t* slot_i, const uint32_t* req_start, uint32_t b0,
                   float* carry_d, uint64_t* carry_i, hipStream_t s);
+// The four merges above in one launch (one workgroup per query): effective slots (own
+// fold of every segment partial, stale source recomputed, or carry) into slot_d/i, the
+// unique-id top-k into out, and the next batch's carry into carry_nd/ni (ping-pong).
+void launch_merge_fused(int regs, const uint32_t* probes, const uint32_t* count_global, const uint32_t* nseg_qp,
+                        const uint32_t* part_base_qp, const float* part_d, const uint64_t* part_i, uint32_t B,
+                        uint32_t P, uint32_t k, int stale, const uint32_t* req_start, uint32_t b0, const float* carry_d,
+                        const uint64_t* carry_i, float* slot_d, uint64_t* slot_i, float* carry_nd, uint64_t* carry_ni,
+                        float* out_d, uint64_t* out_i, hipStream_t s);
 void launch_rank_merge(int regs, const float* d, const uint64_t* i, uint64_t d_stride, uint64_t i_stride,
                        uint32_t nranks, uint32_t n, uint32_t k, float* out_d, uint64_t* out_i, hipStream_t s);
 void launch_fill_empty(uint64_t n, float* d, uint64_t* i, hipStream_t s);

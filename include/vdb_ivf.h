@@ -161,6 +161,21 @@ int vdb_merge_ranks_packed_device(const void* d_records, uint32_t nranks, uint32
                                   float* d_out_dist, uint64_t* d_out_ids, void* stream);
 /* Host-only: the LPT owner of every list for `world` ranks (no GPU needed). */
 int vdb_shard_plan(const uint64_t* list_sizes, uint32_t nlist, uint32_t world, uint32_t* owner);
+/* Host-only: LPT over each list's expected scan cost per batch of `batch` queries, from a
+ * probe census (probe_counts[l] of n_sample query-like rows probe list l): the list is
+ * streamed once per group of 16 queries that probe it (binomial expectation) plus the
+ * per-query distance arithmetic. Balances the ranks' scan time where list popularity, not
+ * only list size, differs. Identical on every rank for the same inputs. */
+int vdb_shard_plan_probe_weighted(const uint64_t* list_sizes, const uint64_t* probe_counts, uint64_t n_sample,
+                                  uint32_t batch, uint32_t nlist, uint32_t world, uint32_t* owner);
+/* counts[l] = how many of the n device rows d_rows (n x dim) probe list l with `nprobe`
+ * (the exact probe selection of search; nlist entries written). */
+int vdb_ivf_probe_census(vdb_ivf* index, const float* d_rows, uint64_t n, uint32_t nprobe, uint64_t* counts);
+/* set_shard / plan_shard with an explicit plan (owner[l] = rank of list l, the same array
+ * on every rank), e.g. from vdb_shard_plan_probe_weighted. */
+int vdb_ivf_set_shard_owners(vdb_ivf* index, uint32_t rank, uint32_t world, const uint32_t* owner);
+int vdb_ivf_plan_shard_owners(vdb_ivf* index, uint32_t rank, uint32_t world, const uint64_t* final_sizes,
+                              const uint32_t* owner);
 
 /* ---- Multi-GPU inside the engine (RCCL over xGMI) ----
  * One process per GPU: rank 0 draws a communicator id (vdb_comm_unique_id) and shares it
@@ -181,7 +196,8 @@ int vdb_ivf_detach_comm(vdb_ivf* index);
 /* The communicator's deadline (option "comm_timeout_ms", default 120000): init is
  * non-blocking and polled, so a rank that never joins makes vdb_ivf_attach_comm fail with
  * VDB_ERR_DEVICE naming this rank; at attach every rank's dimension, nlist, metric, batch,
- * tier setting and stale_slots are compared. Each exchange's completion is watched; one
+ * tier setting, stale_slots and list sizes are compared, and the ranks' stored lists must
+ * partition the non-empty lists (VDB_ERR_STATE otherwise). Each exchange's completion is watched; one
  * still pending after the deadline marks the communicator failed (later searches fail with
  * the message). vdb_ivf_comm_status returns VDB_OK, or VDB_ERR_DEVICE with that message,
  * and the exchanges issued / completed so far (either pointer may be NULL): a caller

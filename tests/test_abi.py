@@ -97,3 +97,22 @@ def test_product_never_imports_the_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
                 text = open(os.path.join(dirpath, f), errors="ignore").read()
                 assert "import oracle" not in text and "cpu_ref" not in text and "oracle_" not in text, f
+
+
+def test_probe_weighted_plan_balances_popular_lists():
+    """vdb_shard_plan_probe_weighted: the same lists and sizes, but one list probed by
+    every query: the size-only LPT puts it with as many vectors as the others, the
+    probe-weighted LPT gives its rank fewer vectors. Deterministic; every list owned."""
+    sizes = np.array([1000, 1000, 1000, 1000, 500, 500, 500, 500], dtype=np.uint64)
+    counts = np.array([64000, 10, 10, 10, 10, 10, 10, 10], dtype=np.uint64)  # list 0: a hub
+    lpt = vdb.shard_plan(sizes, 2)
+    w = vdb.shard_plan_probe_weighted(sizes, counts, 64000, 64, 2)
+    assert np.array_equal(w, vdb.shard_plan_probe_weighted(sizes, counts, 64000, 64, 2))
+    assert set(w.tolist()) == {0, 1} and set(lpt.tolist()) == {0, 1}
+    vec = lambda o, r: int(sizes[o == r].sum())
+    assert vec(lpt, lpt[0]) == vec(lpt, 1 - lpt[0])          # sizes balanced, hub ignored
+    assert vec(w, w[0]) < vec(w, 1 - w[0])                    # the hub's rank holds fewer vectors
+    # uniform popularity: the weighted plan balances sizes like the LPT
+    uni = np.full(8, 640, dtype=np.uint64)
+    wu = vdb.shard_plan_probe_weighted(sizes, uni, 64000, 64, 2)
+    assert vec(wu, 0) == vec(wu, 1)

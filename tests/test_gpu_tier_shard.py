@@ -345,3 +345,97 @@ def test_exchange_watchdog_reports_a_stalled_exchange():
     assert r["err"] and "rank 0 of 1" in r["err"] and "exchange" in r["err"], r
     assert 1.0 < r["watchdog_s"] < 15, r
     assert r["released_ok"] and r["after_raised"] and r["after_detach_ok"], r
+
+
+def test_probe_census_and_weighted_plan_shards():
+    """vdb_ivf_probe_census equals the oracle's probe histogram (select_nprobe on the same
+    rows); shards cut by the probe-weighted plan (explicit owners) merge to the oracle's
+    full answer."""
+    import torch
+    X, Q, ids, o, blocks, need = fixture()
+    dev = torch.device("cuda", 0)
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST, max_gpu_memory=0))
+    g.centroids = o.centroids
+    g.add(X, ids)
+    rows = torch.from_numpy(X[:3000]).to(dev)
+    counts = g.probe_census(rows.data_ptr(), 3000, NPROBE)
+    ref = np.zeros(NLIST, dtype=np.uint64)
+    for x in X[:3000]:
+        ref[o.select_nprobe(x, NPROBE)] += 1
+    assert np.array_equal(counts, ref)
+    sizes = g.list_sizes()
+    world = 3
+    owners = vdb.shard_plan_probe_weighted(sizes, counts, 3000, 64, world)
+    n = len(Q)
+    rb = vdb.rank_record_bytes(n, K)
+    recs = torch.empty(world * rb, dtype=torch.uint8, device=dev)
+    q = torch.from_numpy(Q).to(dev)
+    for r in range(world):
+        h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST, max_gpu_memory=0))
+        h.centroids = o.centroids
+        h.add(X, ids)
+        h.set_shard(r, world, owners=owners)
+        assert np.array_equal(h.list_owners() == r, owners == r)
+        s = torch.cuda.Stream(dev)
+        rec = recs[r * rb:]
+        h.search_device(q.data_ptr(), n, NPROBE, K, rec.data_ptr(), rec.data_ptr() + vdb.rank_record_ids_offset(n, K),
+                        s.cuda_stream)
+        torch.cuda.synchronize()
+    od = torch.empty((n, K), dtype=torch.float32, device=dev)
+    oi = torch.empty((n, K), dtype=torch.int64, device=dev)
+    vdb.merge_ranks_packed_device(recs.data_ptr(), world, n, K, od.data_ptr(), oi.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), *o.search(Q, NPROBE, K))
+
+
+def test_queries_read_in_place_and_misaligned():
+    """dim a multiple of 64 (the padded width): the kernels read the caller's query rows in
+    place (no padding copy); a pointer that is not 16-byte aligned falls back to the
+    padded copy. Both equal the oracle, fused and unfused merges alike."""
+    import torch
+    X, Q, ids, o, blocks, need = fixture()
+    Dr, Ir = o.search(Q, NPROBE, K)
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST, max_gpu_memory=0))
+    g.centroids = o.centroids
+    g.add(X, ids)
+    dev = torch.device("cuda", 0)
+    n = len(Q)
+    buf = torch.zeros(n * D + 1, dtype=torch.float32, device=dev)
+    od = torch.empty((n, K), dtype=torch.float32, device=dev)
+    oi = torch.empty((n, K), dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+    for fm in (1, 0):
+        g.set_option("fused_merge", fm)
+        for off in (0, 1):  # 16-byte aligned rows, then rows 4 bytes off
+            buf[off:off + n * D] = torch.from_numpy(Q.reshape(-1)).to(dev)
+            torch.cuda.synchronize()
+            g.search_device(buf.data_ptr() + 4 * off, n, NPROBE, K, od.data_ptr(), oi.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), Dr, Ir)
+
+
+@pytest.mark.parametrize("k", [10, 64])
+def test_sgpr_query_wide_scan_hub_lists(k):
+    """The SGPR-query wide scan (option sgpr_queries: each wide group's query pairs staged
+    once per batch and read by scalar loads instead of LDS) on hub lists probed by every
+    query, odd and even query groups, both merges: bit-identical to the oracle."""
+    rng = np.random.default_rng(11)
+    dim = 128  # d4 = 32: a whole number of the SGPR scan's 32-tile rounds
+    X = rng.standard_normal((30000, dim)).astype(np.float32)
+    Q = rng.standard_normal((131, dim)).astype(np.float32)
+    ids = rng.permutation(30000).astype(np.uint64)
+    C = np.zeros((6, dim), np.float32)  # centroid 0 at the origin takes most vectors
+    C[1:] = 3.0 * rng.standard_normal((5, dim)).astype(np.float32)
+    o = oracle.OracleIndex(dim, 6, 0)
+    o.centroids = C
+    o.add(X, ids)
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, 6, max_gpu_memory=0))
+    g.centroids = C
+    g.add(X, ids)
+    g.set_option("sgpr_queries", 1)
+    for batch in (64, 131, 7):  # 7: groups of 7 queries (an odd last pair)
+        g.set_batch(batch)
+        for fm in (1, 0):
+            g.set_option("fused_merge", fm)
+            assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))

@@ -2,7 +2,7 @@
 # One GPU-box session (run via gpurun from the repo root): parity tests, the default
 # bench line, the kernel-trace summary of the bench command, PMC passes.
 #   usage: bash tools/gpu_session.sh <tag> [steps, comma-separated:
-#          tests,smoke,bench,multi,grpc,prof,pmc]  [extra bench args...]
+#          tests,smoke,bench,multi,ranks3,ranks4,grpc,prof,pmc]  [extra bench args...]
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 TAG=${1:-run}
@@ -49,6 +49,67 @@ if has multi; then
     run multi 600 python -u bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu --prof-steps 4
     grep '^{' "$O/multi.log" > "$O/multi.json"
     cat "$O/multi.json"
+fi
+if has ranks3; then
+    # every rank's shard of the 8-GPU headline (LPT plan), timed in turn: per-rank balance
+    run ranks3 900 python -u bench.py --cfg cfg3 --emulate-rank all --emulate-shard 8 --inflight 3 --no-cpu
+    grep '^{' "$O/ranks3.log" > "$O/ranks3.json"
+    cut -c 1-600 "$O/ranks3.json"
+fi
+if has ranks4; then
+    run ranks4 1100 python -u bench.py --cfg cfg4 --emulate-rank all --emulate-shard 8 --inflight 3 --no-cpu
+    grep '^{' "$O/ranks4.log" > "$O/ranks4.json"
+    cut -c 1-600 "$O/ranks4.json"
+fi
+if has ranks3w; then
+    run ranks3w 900 python -u bench.py --cfg cfg3 --emulate-rank all --emulate-shard 8 --inflight 3 --no-cpu --plan weighted
+    grep '^{' "$O/ranks3w.log" > "$O/ranks3w.json"
+    cut -c 1-300 "$O/ranks3w.json"
+fi
+if has ranks4w; then
+    run ranks4w 1100 python -u bench.py --cfg cfg4 --emulate-rank all --emulate-shard 8 --inflight 3 --no-cpu --plan weighted
+    grep '^{' "$O/ranks4w.log" > "$O/ranks4w.json"
+    cut -c 1-300 "$O/ranks4w.json"
+fi
+if has emu8; then
+    # rank 0 of 8 cut from the whole headline index by set_shard (round 2's rehearsal line)
+    run emu8 600 python -u bench.py --emulate-shard 8 --inflight 3 --no-cpu
+    grep '^{' "$O/emu8.log" > "$O/emu8.json"
+    cut -c 1-300 "$O/emu8.json"
+fi
+if has emu8ab; then
+    # A/B of one engine option on the 1/8-shard rehearsal line, same box: $AB_OPT=0 vs default
+    run emu8a 600 python -u bench.py --emulate-shard 8 --inflight 3 --no-cpu --opt "$AB_OPT=0"
+    run emu8b 600 python -u bench.py --emulate-shard 8 --inflight 3 --no-cpu
+    run emu8c 600 python -u bench.py --emulate-shard 8 --inflight 3 --no-cpu --opt "$AB_OPT=0"
+    run emu8d 600 python -u bench.py --emulate-shard 8 --inflight 3 --no-cpu
+    for x in a b c d; do grep '^{' "$O/emu8$x.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$x', d['value'], d['ms_per_step'], d['p99_ms_one_in_flight'], r['scan_ms_per_launch'], r['search_ms_per_batch'], d['engine_options'])"; done
+fi
+if has diag4; then
+    # cfg4 shard scan under result-invalidating diagnostic builds (_variants/, tools/build_variant.sh):
+    # where the scan's time goes (LDS query reads, list reads)
+    run diag4_base 600 python -u tools/knob_sweep.py cfg4 ""
+    for v in ${DIAG_VARIANTS:-nolds nomem nolds_nomem}; do
+        export VDB_IVF_LIB=$R/_variants/$v/libvdb_ivf.so
+        run diag4_$v 600 python -u tools/knob_sweep.py cfg4 ""
+        unset VDB_IVF_LIB
+    done
+    for f in "$O"/diag4_*.log; do echo "$(basename $f) $(grep '^{' $f | tail -1)"; done
+fi
+if has sweep; then
+    # one build, several option sets: tools/knob_sweep.py $SWEEP_WL $SWEEP_SETS (scan ms, wall ms per batch)
+    for wl in ${SWEEP_WL:-cfg3}; do
+        run sweep_$wl 900 python -u tools/knob_sweep.py $wl $SWEEP_SETS
+        grep '^{' "$O/sweep_$wl.log"
+    done
+fi
+if has swin; then
+    # scan_window A/B at 3 batches in flight (throughput, p99, mean latency): 1/8 shard and cfg4 shard
+    run swin_a 600 python -u bench.py --emulate-shard 8 --inflight 3 --no-cpu
+    run swin_b 600 python -u bench.py --emulate-shard 8 --inflight 3 --no-cpu --opt scan_window=2
+    run swin_c 900 python -u bench.py --cfg cfg4 --emulate-shard 8 --inflight 3 --no-cpu --steps 60 --prof-steps 10
+    run swin_d 900 python -u bench.py --cfg cfg4 --emulate-shard 8 --inflight 3 --no-cpu --steps 60 --prof-steps 10 --opt scan_window=2
+    for x in a b c d; do grep '^{' "$O/swin_$x.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$x', d['config']['workload'], d['value'], d['ms_per_step'], 'p99', d['p99_ms'], 'mean', d['latency_mean_ms'], d['engine_options'])"; done
 fi
 if has grpc; then
     run grpc 600 python -u tools/grpc_load.py
