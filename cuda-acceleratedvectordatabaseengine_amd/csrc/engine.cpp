@@ -664,8 +664,6 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->fused_scan = value != 0;
         } else if (n == "fused_merge") {
             h->fused_merge = value != 0;
-        } else if (n == "sgpr_queries") {
-            h->sgpr_queries = value != 0;
         } else if (n == "scan_window") {
             require(value >= 0 && value <= 7, "scan_window is 0 (no limit) .. 7");
             h->quiesce();

@@ -284,7 +284,6 @@ struct vdb_ivf {
     uint32_t wide_group = 16;     // queries per wide item at most: 16 (4-wave workgroups) or 32 (8-wave)
     bool fused_scan = true;       // narrow items inside the wide scan's grid (option fused_scan; +2-3 %)
     bool fused_merge = true;      // the four per-batch merges as one launch (option fused_merge)
-    bool sgpr_queries = false;    // wide scan reads its query pairs through SGPRs (option sgpr_queries)
     // At most this many scans of batches in flight overlap (0: no limit): a batch's scan
     // waits for the scan issued `scan_window` batches earlier to finish, so the GPU serves
     // batches closer to issue order (latency spread at several batches in flight).
@@ -362,7 +361,6 @@ struct vdb_ivf {
         DevBuf<float> l1_d{true};
         DevBuf<uint64_t> l1_i{true};
         DevBuf<vdbk::ScanItem> items{true}, items_w{true};
-        DevBuf<float> qstage{true};  // (sgpr_queries) wide groups' query pairs, [B*P][d4][8] + slack
         DevBuf<uint8_t> xrec{true}, xgat{true};  // multi-GPU: this rank's packed partials, the gathered records
         DevBuf<float> gq{true};            // group member: the call's queries on this device
         DevBuf<uint32_t> greq{true};       // group member: the call's request starts on this device
@@ -1565,7 +1563,8 @@ struct vdb_ivf {
         const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
         const uint64_t max_wide = max_items / 4 + BP + 1;
         const int waves = wide_group == 32 ? 8 : 4;  // workgroup shape of the wide scan
-        const bool wide = regs_k == 1 && wide_scan && vdbk::scan_wide_fits(d4, k, waves);
+        // (Cosine: every CPU-path distance is 0.0f, A5; its lists scan as narrow items only)
+        const bool wide = regs_k == 1 && wide_scan && metric != 2 && vdbk::scan_wide_fits(d4, k, waves);
         // segments per item: one per wave (more adds tail latency, no throughput)
         const uint32_t segs_item = segs_item_opt ? segs_item_opt : (uint32_t)waves;
         // wide items of many queries: bounded on the matrix cores (L2 / IP, 16-query items)
@@ -1586,13 +1585,6 @@ struct vdb_ivf {
                                 mfma_min, bounded_stats ? stats.p + 5 : nullptr};
         // the bounded items first (the batch's most-probed lists), on the same stream
         if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
-        // SGPR queries: each wide group's pairs staged once per batch for scalar loads
-        const float* qstage = nullptr;
-        if (wide && sgpr_queries && waves == 4 && !mfma_min && vdbk::scan_sq_fits(d4)) {
-            float* st = slot_buf(w, w.qstage, (size_t)BP * d4 * 8 + 64);
-            vdbk::launch_stage_pairs((uint32_t)max_wide, w.items_w.p, w.counters.p, w.sorted_pair.p, w.q, d4, st, s);
-            qstage = st;
-        }
         if (wide && fused_scan) {
             // one persistent grid takes both queues (no side stream, no fork/join)
             // (narrow_blocks counts 4-wave workgroups: as many waves start on the narrow queue)
@@ -1600,7 +1592,7 @@ struct vdb_ivf {
             sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks * 4 / waves, grid_cap / 2));
             const uint64_t want = std::max<uint64_t>(max_wide, (max_items + 3) / 4);
             vdbk::launch_scan_wide(metric, (uint32_t)(scan_blocks ? std::min<uint64_t>(want, scan_blocks) : want), sa, s,
-                                   waves, qstage);
+                                   waves);
         } else if (wide) {
             // narrow items on the side stream fill the CUs the wide items leave idle
             HIPCHECK(hipEventRecord(w.fork, s));
@@ -1608,7 +1600,7 @@ struct vdb_ivf {
             vdbk::launch_scan_narrow(metric, regs_k, std::min<uint32_t>((uint32_t)((max_items + 3) / 4), narrow_blocks), sa,
                                      w.side);
             HIPCHECK(hipEventRecord(w.join, w.side));
-            vdbk::launch_scan_wide(metric, (uint32_t)max_wide, sa, s, waves, qstage);
+            vdbk::launch_scan_wide(metric, (uint32_t)max_wide, sa, s, waves);
             HIPCHECK(hipStreamWaitEvent(s, w.join, 0));
         } else {
             vdbk::launch_scan_narrow(metric, regs_k, (uint32_t)((max_items + 3) / 4), sa, s);

@@ -1576,200 +1576,6 @@ __device__ __forceinline__ void scan_wide_wave_mfma(const ScanArgs& a, const Sca
     }
 }
 
-// ============================================================================
-// SGPR-query wide wave (option sgpr_queries): the arithmetic and the item semantics of
-// scan_wide_wave (exact sums in d order, two queries per packed op, shared thresholds),
-// but the query pairs come from SGPRs instead of LDS. Every wave reads the same
-// (wave-uniform) query values, so a per-lane broadcast read from LDS moves 64x the
-// bytes it uses (16 ds_read_b128 = 64 LDS cycles per tile per wave at 8 pairs); a
-// scalar load moves them once. ivf_stage_pairs writes each wide group's pairs
-// tile-major to qstage ([d4][GP][8 floats] at pair_start * d4 * 8); per tile the wave
-// holds them in ceil(GP / 2) blocks of 16 SGPRs (s_load_dwordx16), each reloaded with
-// the next tile's block right after its last use, so a load has three quarters of a
-// tile of arithmetic to land in. The freed query VGPRs deepen the list stream:
-// T tiles (kSqTiles) in flight per lane instead of 16.
-// ============================================================================
-#ifndef VDB_SQ_TILES
-#define VDB_SQ_TILES 32
-#endif
-constexpr int kSqTiles = VDB_SQ_TILES;
-typedef float v16q __attribute__((ext_vector_type(16)));
-
-template <int H>
-__device__ __forceinline__ f2 pk_sub_bcast_s(f2 q, f2 x) {
-    f2 r;
-    if constexpr (H == 0)
-        asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "s"(q), "v"(x));
-    else
-        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "s"(q), "v"(x));
-    return r;
-}
-template <int H>
-__device__ __forceinline__ f2 pk_mul_bcast_s(f2 q, f2 x) {
-    f2 r;
-    if constexpr (H == 0)
-        asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "s"(q), "v"(x));
-    else
-        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "s"(q), "v"(x));
-    return r;
-}
-template <int M, int H>
-__device__ __forceinline__ f2 dist_term2_s(f2 acc, f2 q, f2 x) {
-    if constexpr (M == kL2) {
-        const f2 diff = pk_sub_bcast_s<H>(q, x);
-        return acc + diff * diff;
-    } else if constexpr (M == kIP) {
-        return acc + pk_mul_bcast_s<H>(q, x);
-    } else {
-        return acc;
-    }
-}
-
-template <int GP, int M, bool ODD>
-__device__ __forceinline__ void scan_wide_wave_sq(const ScanArgs& a, const ScanItem it, const float* __restrict__ qs,
-                                                  const int np, float* tk_d, uint64_t* tk_i, uint32_t* s_thr,
-                                                  const uint32_t seg) {
-    constexpr int G = 2 * GP;
-    constexpr int NQ = (GP + 1) / 2;  // 16-SGPR blocks (two pairs) per tile
-    const uint32_t d4 = a.d4;
-    const int lane = lane_id();
-    const uint32_t count = a.count[it.list];
-    const uint32_t seg_vectors = a.seg_blocks * 64;
-    const uint64_t b0 = a.block_off[it.list] + (uint64_t)seg * a.seg_blocks;
-    const uint32_t v0 = seg * seg_vectors;
-    const uint32_t nv = min(count - v0, seg_vectors);
-    const uint32_t nb = (nv + 63) >> 6;
-    const int k = (int)a.k;
-
-    for (int e = lane; e < G * k; e += 64) {
-        tk_d[e] = __builtin_inff();
-        tk_i[e] = kNoId;
-    }
-    float kd[G];
-    f2 acc[GP];
-    float acc1 = 0.0f;  // ODD: the single query of the last pair
-#pragma unroll
-    for (int g = 0; g < G; ++g) kd[g] = __builtin_inff();
-#pragma unroll
-    for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
-    auto qsum = [&](int g) -> float {
-        if (ODD && g == 2 * (GP - 1)) return acc1;
-        return (g & 1) ? acc[g >> 1].y : acc[g >> 1].x;
-    };
-    // pair p's four terms of one tile; q8 = (qa.x, qb.x, qa.y, qb.y, qa.z, qb.z, qa.w, qb.w)
-    auto pair_terms = [&](int p, f2 q01, f2 q23, f2 q45, f2 q67, const f2 xlo, const f2 xhi, const float4 x) {
-        if (ODD && p == GP - 1) {  // query 2p alone: the low halves
-            acc1 = dist_term<M>(acc1, q01.x, x.x);
-            acc1 = dist_term<M>(acc1, q23.x, x.y);
-            acc1 = dist_term<M>(acc1, q45.x, x.z);
-            acc1 = dist_term<M>(acc1, q67.x, x.w);
-        } else {
-            acc[p] = dist_term2_s<M, 0>(acc[p], q01, xlo);
-            acc[p] = dist_term2_s<M, 1>(acc[p], q23, xlo);
-            acc[p] = dist_term2_s<M, 0>(acc[p], q45, xhi);
-            acc[p] = dist_term2_s<M, 1>(acc[p], q67, xhi);
-        }
-    };
-    v16q qq[NQ];
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) qq[j] = *(const v16q*)(qs + (size_t)(2 * j) * 8);
-    auto compute = [&](const float4 x, uint32_t t, auto) {
-        const f2 xlo = {x.x, x.y}, xhi = {x.z, x.w};
-        const float* nxt = qs + (size_t)(t + 1 == d4 ? 0 : t + 1) * GP * 8;
-#pragma unroll
-        for (int j = 0; j < NQ; ++j) {
-            const v16q q = qq[j];
-            pair_terms(2 * j, f2{q[0], q[1]}, f2{q[2], q[3]}, f2{q[4], q[5]}, f2{q[6], q[7]}, xlo, xhi, x);
-            if (2 * j + 1 < GP)
-                pair_terms(2 * j + 1, f2{q[8], q[9]}, f2{q[10], q[11]}, f2{q[12], q[13]}, f2{q[14], q[15]}, xlo, xhi,
-                           x);
-            qq[j] = *(const v16q*)(nxt + (size_t)(2 * j) * 8);
-        }
-    };
-    auto finish = [&](uint32_t j, uint64_t id) {
-        const bool valid = j * 64 + lane < nv;
-        float th[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) th[g] = g < np ? fminf(kd[g], ord_dec(s_thr[g])) : kd[g];
-        uint32_t pend = 0;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float dist = dist_finish<M>(qsum(g));
-            if (g < np && __ballot(valid && dist <= th[g])) pend |= 1u << g;
-        }
-        if (VDB_SCAN_DIAG & 1) pend = 0;  // DIAGNOSTIC: no top-k maintenance (results invalid)
-        if (pend) {
-            const uint64_t vid = valid ? id : kNoId;
-            do {
-                const int gs = __builtin_ctz(pend);
-                pend &= pend - 1;
-                float dist = 0.0f, kdg = 0.0f;
-#pragma unroll
-                for (int g = 0; g < G; ++g)
-                    if (g == gs) {
-                        dist = dist_finish<M>(qsum(g));
-                        kdg = th[g];
-                    }
-                float* sd = tk_d + gs * k;
-                uint64_t* si = tk_i + gs * k;
-                WaveTopK<1> tk;
-                tk.d[0] = lane < k ? sd[lane] : __builtin_inff();
-                tk.id[0] = lane < k ? si[lane] : kNoId;
-                float nkd;
-                uint64_t nki;
-                tk.at(k - 1, nkd, nki);
-                offer_lanes<1>(tk, valid && dist <= kdg, dist, vid, k, nkd, nki);
-                if (lane < k) {
-                    sd[lane] = tk.d[0];
-                    si[lane] = tk.id[0];
-                }
-#pragma unroll
-                for (int g = 0; g < G; ++g)
-                    if (g == gs) kd[g] = nkd;
-                if (nkd < kdg && lane == 0) atomicMin(&s_thr[gs], ord_enc(nkd));
-            } while (pend);
-        }
-#pragma unroll
-        for (int p = 0; p < GP; ++p) acc[p] = f2{0.0f, 0.0f};
-        acc1 = 0.0f;
-    };
-    stream_blocks<kSqTiles>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-        if (g < np && lane == 0 && kd[g] < __builtin_inff()) atomicMin(&a.thr[it.pair_start + g], ord_enc(kd[g]));
-    for (int g = 0; g < np; ++g) {
-        const uint32_t part = a.part_base_sorted[it.pair_start + g] + seg;
-        if (lane < k) {
-            a.part_d[(size_t)part * k + lane] = tk_d[g * k + lane];
-            a.part_i[(size_t)part * k + lane] = tk_i[g * k + lane];
-        }
-    }
-}
-
-// Each wide group's query pairs, tile-major, for the SGPR-query scan: one workgroup per
-// group (its first segment range's item), [d4][GP][8 floats] at qstage + pair_start * d4 * 8.
-__global__ __launch_bounds__(256) void ivf_stage_pairs(const ScanItem* __restrict__ items_w,
-                                                      const uint32_t* __restrict__ counters,
-                                                      const uint32_t* __restrict__ sorted_pair,
-                                                      const float* __restrict__ qpad, uint32_t d4,
-                                                      float* __restrict__ qstage) {
-    const uint32_t n = counters[3] + counters[7];
-    for (uint32_t idx = blockIdx.x; idx < n; idx += gridDim.x) {
-        const ScanItem it = items_w[idx];
-        if (it.seg != 0) continue;
-        const int np = (int)it.npairs, gp = (np + 1) / 2;
-        float4* dst = (float4*)(qstage + (size_t)it.pair_start * d4 * 8);
-        for (uint32_t e = threadIdx.x; e < (uint32_t)gp * d4; e += blockDim.x) {
-            const uint32_t t = e / gp, p = e - t * gp;
-            const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
-            const float4 qa = ((const float4*)(qpad + (size_t)(sorted_pair[it.pair_start + ga] >> 16) * d4 * 4))[t];
-            const float4 qb = ((const float4*)(qpad + (size_t)(sorted_pair[it.pair_start + gb] >> 16) * d4 * 4))[t];
-            dst[(t * gp + p) * 2 + 0] = make_float4(qa.x, qb.x, qa.y, qb.y);
-            dst[(t * gp + p) * 2 + 1] = make_float4(qa.z, qb.z, qa.w, qb.w);
-        }
-    }
-}
-
 // One wave-item of a narrow list (<= 4 pairs of one segment).
 template <int R, int M>
 __device__ __forceinline__ void scan_narrow(const ScanArgs& a, const ScanItem it) {
@@ -1825,10 +1631,8 @@ __device__ __forceinline__ void drain_narrow(const ScanArgs& a) {
 //    its half of the queries: the two waves streaming one segment run side by side on
 //    the CU, so the second read is served on-chip, and every wave keeps at most 8 query
 //    pairs in registers (the code path that does not spill).
-// SQ (W = 4): the query pairs come from qstage through SGPRs (scan_wide_wave_sq), not
-// from LDS; qstage is a kernel argument of its own so its loads are scalar.
-template <int M, int W, bool SQ>
-__global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a, const float* __restrict__ qstage) {
+template <int M, int W>
+__global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
     constexpr int GW = 4 * W;  // queries per item at most
     // Dynamic LDS: [d4][gpv][2] float4 of staged query pairs (tile-major), then per wave
     // kWaveQueries x k top-k ids (u64), then the same for distances (f32).
@@ -1869,7 +1673,7 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a, c
         if (threadIdx.x < 2) s_seg[threadIdx.x] = 0;  // visible after the staging barrier below
         if (threadIdx.x < (uint32_t)np) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
         const int gpv = (VDB_SCAN_DIAG & 2) ? 1 : gp;  // (DIAGNOSTIC diag&2: one pair only, results invalid)
-        for (uint32_t e = threadIdx.x; !SQ && e < (uint32_t)gpv * d4; e += blockDim.x) {
+        for (uint32_t e = threadIdx.x; e < (uint32_t)gpv * d4; e += blockDim.x) {
             const uint32_t t = e / gpv, p = e - t * gpv;
             const int ga = min((int)(2 * p), np - 1), gb = min((int)(2 * p + 1), np - 1);
             const float4 qa = ((const float4*)(a.qpad + (size_t)(a.sorted_pair[it.pair_start + ga] >> 16) * d4 * 4))[t];
@@ -1898,20 +1702,6 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a, c
             if (lane_id() == 0) sg = atomicAdd(&s_seg[half], 1u);
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
-            if constexpr (SQ) {
-                const float* qs = qstage + (size_t)it.pair_start * d4 * 8;
-#define VDB_WS(GPN)                                                                                     \
-    case GPN:                                                                                           \
-        if (kOddPairs && (nq & 1)) scan_wide_wave_sq<GPN, M, true>(a, it, qs, nq, tk_d, tk_i, s_thr, sg); \
-        else scan_wide_wave_sq<GPN, M, false>(a, it, qs, nq, tk_d, tk_i, s_thr, sg);                      \
-        break;
-                switch (gw) {
-                    VDB_WS(1) VDB_WS(2) VDB_WS(3) VDB_WS(4) VDB_WS(5) VDB_WS(6) VDB_WS(7)
-                    default: VDB_WS(8)
-                }
-#undef VDB_WS
-                continue;
-            }
 #define VDB_WW(GPN)                                                                       \
     case GPN:                                                                             \
         if (W == 8 && split) scan_wide_wave<GPN, M, true, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg); \
@@ -2845,16 +2635,12 @@ void launch_scan_bounded(int metric, uint32_t grid_blocks, const ScanArgs& a, hi
     else ivf_scan_bounded<kIP><<<g, 256, lds, s>>>(a);
 }
 
-void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves,
-                      const float* qstage) {
+void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves) {
     if (!grid_blocks) return;
     static const bool raised = [] {
         // wide items stage up to 16 (32) queries in LDS: allow the whole 160 KB of a CU
-        const void* f4[] = {(const void*)ivf_scan_wide<kL2, 4, false>, (const void*)ivf_scan_wide<kIP, 4, false>,
-                            (const void*)ivf_scan_wide<kCos, 4, false>, (const void*)ivf_scan_wide<kL2, 4, true>,
-                            (const void*)ivf_scan_wide<kIP, 4, true>, (const void*)ivf_scan_wide<kCos, 4, true>};
-        const void* f8[] = {(const void*)ivf_scan_wide<kL2, 8, false>, (const void*)ivf_scan_wide<kIP, 8, false>,
-                            (const void*)ivf_scan_wide<kCos, 8, false>};
+        const void* f4[] = {(const void*)ivf_scan_wide<kL2, 4>, (const void*)ivf_scan_wide<kIP, 4>};
+        const void* f8[] = {(const void*)ivf_scan_wide<kL2, 8>, (const void*)ivf_scan_wide<kIP, 8>};
         for (const void* f : f4)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes - wide_static_lds(4)));
         for (const void* f : f8)
@@ -2866,30 +2652,13 @@ void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipSt
     const size_t lds = scan_wide_lds(a.d4, a.k, waves);
     if (waves == 8) {  // one 8-wave workgroup per CU
         const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks / 2);
-        if (metric == kL2) ivf_scan_wide<kL2, 8, false><<<g, 512, lds, s>>>(a, nullptr);
-        else if (metric == kIP) ivf_scan_wide<kIP, 8, false><<<g, 512, lds, s>>>(a, nullptr);
-        else ivf_scan_wide<kCos, 8, false><<<g, 512, lds, s>>>(a, nullptr);
+        if (metric == kL2) ivf_scan_wide<kL2, 8><<<g, 512, lds, s>>>(a);
+        else ivf_scan_wide<kIP, 8><<<g, 512, lds, s>>>(a);
         return;
     }
     const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
-    if (qstage) {
-        if (metric == kL2) ivf_scan_wide<kL2, 4, true><<<g, 256, lds, s>>>(a, qstage);
-        else if (metric == kIP) ivf_scan_wide<kIP, 4, true><<<g, 256, lds, s>>>(a, qstage);
-        else ivf_scan_wide<kCos, 4, true><<<g, 256, lds, s>>>(a, qstage);
-        return;
-    }
-    if (metric == kL2) ivf_scan_wide<kL2, 4, false><<<g, 256, lds, s>>>(a, nullptr);
-    else if (metric == kIP) ivf_scan_wide<kIP, 4, false><<<g, 256, lds, s>>>(a, nullptr);
-    else ivf_scan_wide<kCos, 4, false><<<g, 256, lds, s>>>(a, nullptr);
-}
-
-bool scan_sq_fits(uint32_t d4) { return d4 % (uint32_t)kSqTiles == 0; }
-
-void launch_stage_pairs(uint32_t grid_items, const ScanItem* items_w, const uint32_t* counters,
-                        const uint32_t* sorted_pair, const float* qpad, uint32_t d4, float* qstage, hipStream_t s) {
-    if (!grid_items) return;
-    ivf_stage_pairs<<<std::min<uint32_t>(grid_items, 2048), 256, 0, s>>>(items_w, counters, sorted_pair, qpad, d4,
-                                                                         qstage);
+    if (metric == kL2) ivf_scan_wide<kL2, 4><<<g, 256, lds, s>>>(a);
+    else ivf_scan_wide<kIP, 4><<<g, 256, lds, s>>>(a);
 }
 
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const uint32_t* nseg_qp,

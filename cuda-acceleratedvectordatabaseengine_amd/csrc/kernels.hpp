@@ -123,16 +123,9 @@ struct ScanArgs {
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);
 void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
+// L2 / IP only (Cosine, whose CPU-path distance is always 0.0f, scans narrow items).
 // waves 4: items of <= 16 queries, two workgroups per CU; 8: items of <= 32, one per CU.
-// qstage (waves 4): the wide groups' query pairs staged by launch_stage_pairs, read
-// through SGPRs instead of LDS (null: LDS staging per item).
-void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves = 4,
-                      const float* qstage = nullptr);
-// The SGPR-query wide scan streams kSqTiles tiles per lane: d4 must be a multiple.
-bool scan_sq_fits(uint32_t d4);
-// Per wide group, its query pairs tile-major ([d4][GP][8] floats at pair_start * d4 * 8).
-void launch_stage_pairs(uint32_t grid_items, const ScanItem* items_w, const uint32_t* counters,
-                        const uint32_t* sorted_pair, const float* qpad, uint32_t d4, float* qstage, hipStream_t s);
+void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s, int waves = 4);
 // wide items of >= a.mfma_min queries (L2 / IP): bounded on the matrix cores, exact re-rank
 size_t scan_bounded_lds(uint32_t d4, uint32_t k);
 bool scan_bounded_fits(uint32_t d4, uint32_t k);

@@ -414,28 +414,3 @@ def test_queries_read_in_place_and_misaligned():
             torch.cuda.synchronize()
             assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), Dr, Ir)
 
-
-@pytest.mark.parametrize("k", [10, 64])
-def test_sgpr_query_wide_scan_hub_lists(k):
-    """The SGPR-query wide scan (option sgpr_queries: each wide group's query pairs staged
-    once per batch and read by scalar loads instead of LDS) on hub lists probed by every
-    query, odd and even query groups, both merges: bit-identical to the oracle."""
-    rng = np.random.default_rng(11)
-    dim = 128  # d4 = 32: a whole number of the SGPR scan's 32-tile rounds
-    X = rng.standard_normal((30000, dim)).astype(np.float32)
-    Q = rng.standard_normal((131, dim)).astype(np.float32)
-    ids = rng.permutation(30000).astype(np.uint64)
-    C = np.zeros((6, dim), np.float32)  # centroid 0 at the origin takes most vectors
-    C[1:] = 3.0 * rng.standard_normal((5, dim)).astype(np.float32)
-    o = oracle.OracleIndex(dim, 6, 0)
-    o.centroids = C
-    o.add(X, ids)
-    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, 6, max_gpu_memory=0))
-    g.centroids = C
-    g.add(X, ids)
-    g.set_option("sgpr_queries", 1)
-    for batch in (64, 131, 7):  # 7: groups of 7 queries (an odd last pair)
-        g.set_batch(batch)
-        for fm in (1, 0):
-            g.set_option("fused_merge", fm)
-            assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))

@@ -103,6 +103,20 @@ if has sweep; then
         grep '^{' "$O/sweep_$wl.log"
     done
 fi
+if has libab; then
+    # A/B of two libraries on the same box: the in-tree build vs _variants/$AB_LIB (tools/build_variant.sh),
+    # knob_sweep timing (scan ms, wall ms per batch) per workload, alternating A B A B
+    for wl in ${AB_WL:-cfg3}; do
+        for rep in 1 2; do
+            run ab_${wl}_A$rep 900 python -u tools/knob_sweep.py $wl ""
+            export VDB_IVF_LIB=$R/_variants/$AB_LIB/libvdb_ivf.so
+            run ab_${wl}_B$rep 900 python -u tools/knob_sweep.py $wl ""
+            unset VDB_IVF_LIB
+            [ "$wl" = cfg4 ] && break
+        done
+    done
+    for f in "$O"/ab_*.log; do echo "$(basename $f .log) $(grep '^{' $f | tail -1 | cut -c1-160)"; done
+fi
 if has swin; then
     # scan_window A/B at 3 batches in flight (throughput, p99, mean latency): 1/8 shard and cfg4 shard
     run swin_a 600 python -u bench.py --emulate-shard 8 --inflight 3 --no-cpu

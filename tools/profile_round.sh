@@ -9,6 +9,8 @@
 #   trace    rocprofv3 --kernel-trace --stats of the headline bench at 1 and 2 batches in
 #            flight, and of the mixture bench
 #   shard    the cfg4 rank-0-of-8 shard line (sharded 100M build), with its kernel trace
+#   emu8     rank 0 of 8 of the headline index at 3 in flight (the 8-GPU per-GPU work)
+#   tier5    the cfg4 rank-0 shard served from a shard file through a smaller HBM cache (cfg5 shape)
 #   usage: bash tools/profile_round.sh <tag> [steps, comma-separated]
 set -o pipefail
 TAG=${1:-round}
@@ -70,6 +72,22 @@ fi
 if has shard; then
     run shard 600 python3 -u bench.py $CFG4 --shard-check 4 --traffic-json "$TJ"
     grep '^{' "$O/shard.log" > "$O/shard.json" && cut -c 1-400 "$O/shard.json"
+fi
+if has emu8; then
+    # rank 0 of 8 cut from the headline index (the per-GPU work of the 8-GPU headline), 3 in flight
+    run emu8 600 python3 -u bench.py --emulate-shard 8 --inflight 3 --no-cpu --traffic-json "$TJ"
+    grep '^{' "$O/emu8.log" > "$O/emu8.json" && cut -c 1-300 "$O/emu8.json"
+fi
+if has emu8trace; then
+    run trace_emu8 600 rocprofv3 --kernel-trace --stats -d "$O/trace_emu8" -o k -f csv -- python3 bench.py --emulate-shard 8 --steps 40 --warmup 4 --no-cpu --inflight 1 --prof-steps 4
+    find "$O/trace_emu8" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_emu8.csv" \;
+    head -14 "$O/kernel_stats_emu8.csv" | cut -c 1-160
+fi
+if has tier5; then
+    # configs[4]'s per-GPU shape: the cfg4 rank-0 shard (37 GB) served from a shard file through an
+    # HBM cache smaller than the shard (io_uring + O_DIRECT, next-use eviction, prefetch)
+    run tier5 1000 python3 -u bench.py $CFG4 --steps 20 --warmup 2 --prof-steps 4 --tier-cache-gib ${TIER_GIB:-24} --tier-call 512 --tier-calls ${TIER_CALLS:-4}
+    grep '^{' "$O/tier5.log" > "$O/tier5.json" && python3 -c "import json; d=json.load(open('$O/tier5.json')); print(json.dumps(d.get('tier')))"
 fi
 if has shardtrace; then
     run trace_cfg4 600 rocprofv3 --kernel-trace --stats -d "$O/trace_cfg4" -o k -f csv -- python3 bench.py $CFG4 --steps 20 --warmup 2 --inflight 1
