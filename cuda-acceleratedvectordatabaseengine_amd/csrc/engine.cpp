@@ -660,6 +660,11 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "scan_mfma_min") {
             require(value >= 0 && value <= 16, "scan_mfma_min is 0 (never) .. 16");
             h->scan_mfma_min = (uint32_t)value;
+        } else if (n == "screen") {
+            h->set_device();
+            h->quiesce();
+            h->screen_opt = value != 0;
+            h->screen_update();
         } else if (n == "fused_scan") {
             h->fused_scan = value != 0;
         } else if (n == "fused_merge") {
@@ -682,6 +687,8 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->set_device();
             h->max_gpu_memory = (uint64_t)value;
             h->apply_memory_cap(h->count);
+            h->quiesce();
+            h->screen_update();  // the screen's extra bytes count against the cap too
         } else if (n == "bounded_stats") {
             h->bounded_stats = value != 0;  // statistics only: results never change
         } else if (n == "comm_timeout_ms") {

@@ -292,6 +292,21 @@ struct vdb_ivf {
     int scan_hist[8] = {};  // slot index of the scans issued, by sequence number
     uint32_t narrow_blocks = 64;  // persistent narrow-scan workgroups beside the wide scan (1/8 shard: +1.5 % vs 512)
 
+    // Screened scan (screen.hip, option "screen", on by default): every (query, vector)
+    // distance is bounded on the matrix cores from a bf16 shadow of the lists and computed
+    // exactly (the reference's sequential fp32 sum) only where it can reach the list's
+    // top-k; results are bit-identical to the exact scan. Built from the arena whenever
+    // the lists change (upload_directory): the shadow in MFMA operand order (half the
+    // arena's bytes), the fp32 rows in slot order for the exact re-checks, per-slot norms.
+    // Not built for the tier (lists not all in HBM), for Cosine, or when the extra 1.5x of
+    // the list bytes does not fit (Config::max_gpu_memory, or a failed allocation).
+    bool screen_opt = true;
+    bool screen_ready = false;
+    DevBuf<uint4> screen_sh;
+    DevBuf<float> screen_rows;
+    DevBuf<float4> screen_meta;
+    DevBuf<uint32_t> screen_blist;  // the list of every arena block (residuals against its centroid)
+
     // List-cache tier (option list_cache_bytes > 0), the reference's residency model
     // (load_list_to_gpu on first touch under a byte cap, evict_list_from_gpu,
     // ivf_flat_index.cpp:387-471) for indexes larger than HBM: the arena then lives in
@@ -361,6 +376,8 @@ struct vdb_ivf {
         DevBuf<float> l1_d{true};
         DevBuf<uint64_t> l1_i{true};
         DevBuf<vdbk::ScanItem> items{true}, items_w{true};
+        DevBuf<uint16_t> qres{true};  // screened scan: per (query, probe) bf16 A rows [B * P][dp]
+        DevBuf<float4> pst{true};     // ... and their norms
         DevBuf<uint8_t> xrec{true}, xgat{true};  // multi-GPU: this rank's packed partials, the gathered records
         DevBuf<float> gq{true};            // group member: the call's queries on this device
         DevBuf<uint32_t> greq{true};       // group member: the call's request starts on this device
@@ -715,6 +732,44 @@ struct vdb_ivf {
         nseg_prefix.assign(nlist + 1, 0);
         for (uint32_t j = 0; j < nlist; ++j) nseg_prefix[j + 1] = nseg_prefix[j] + sorted[j];
         HIPCHECK(hipStreamSynchronize(stream));  // host vectors above are stack-owned
+        screen_update();
+    }
+
+    // (Re)build the screened scan's data from the arena (quiesced by the caller), or drop it.
+    void screen_update() {
+        screen_ready = false;
+        const bool want = screen_opt && metric != 2 && !tiered() && !arena.host && arena_blocks > 0;
+        const uint64_t extra = arena_blocks * 64 * ((uint64_t)dp * 6 + 16);  // shadow + rows + norms
+        if (!want || (max_gpu_memory && arena_blocks * 64 * ((uint64_t)dp * 4 + 8) + extra > max_gpu_memory)) {
+            screen_sh.release();
+            screen_rows.release();
+            screen_meta.release();
+            screen_blist.release();
+            return;
+        }
+        std::vector<uint32_t> blist(arena_blocks, 0);
+        for (uint32_t l = 0; l < nlist; ++l)
+            if (owned[l])
+                for (uint64_t b = 0; b < list_blocks(l); ++b) blist[block_off[l] + b] = l;
+        try {
+            screen_sh.ensure(vdbk::screen_shadow_u4(arena_blocks, d4));
+            screen_rows.ensure((size_t)arena_blocks * 64 * dp);
+            screen_meta.ensure((size_t)arena_blocks * 64);
+            screen_blist.ensure(arena_blocks);
+        } catch (const VdbError&) {  // no room for it: the exact scan serves
+            (void)hipGetLastError();
+            screen_sh.release();
+            screen_rows.release();
+            screen_meta.release();
+            screen_blist.release();
+            return;
+        }
+        HIPCHECK(hipMemcpyAsync(screen_blist.p, blist.data(), arena_blocks * 4, hipMemcpyHostToDevice, stream));
+        vdbk::launch_screen_build(arena.p, arena_blocks, d4, screen_blist.p, cent_rm.p, screen_sh.p, screen_rows.p,
+                                  screen_meta.p, stream);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipStreamSynchronize(stream));
+        screen_ready = true;
     }
 
     // Rebuild the arena so list l holds `keep[l]` of its current blocks at new
@@ -1231,6 +1286,7 @@ struct vdb_ivf {
         quiesce();
         vdbk::launch_interleave(cent_rm.p, nlist, dp, cent_il.p, stream);
         HIPCHECK(hipGetLastError());
+        if (arena_blocks) screen_update();  // the shadow holds residuals against the centroids
     }
 
     // assign_to_lists (cpp:259-295): exact argmin with ties to the lowest centroid. For
@@ -1568,9 +1624,14 @@ struct vdb_ivf {
         // segments per item: one per wave (more adds tail latency, no throughput)
         const uint32_t segs_item = segs_item_opt ? segs_item_opt : (uint32_t)waves;
         // wide items of many queries: bounded on the matrix cores (L2 / IP, 16-query items)
-        const uint32_t mfma_min = wide && waves == 4 && metric != 2 && !(VDB_SCAN_DIAG & 2) && vdbk::scan_bounded_fits(d4, k)
+        // the screened scan (default): its items are the exact scan's 16-query wide items
+        // and narrow items
+        const bool screened = screen_ready && !tiered() && regs_k == 1 && metric != 2 && vdbk::scan_screen_fits(k, dp);
+        const uint32_t mfma_min = !screened && wide && waves == 4 && metric != 2 && !(VDB_SCAN_DIAG & 2) &&
+                                          vdbk::scan_bounded_fits(d4, k)
                                       ? scan_mfma_min : 0u;
-        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, wide ? (int)wide_group : 0, segs_item, w.items.p, w.items_w.p,
+        const int plan_wide = screened ? vdbk::kWideGroup : (wide ? (int)wide_group : 0);
+        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, plan_wide, screened ? 4u : segs_item, w.items.p, w.items_w.p,
                           w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, w.thr.p,
                           mfma_min, s);
         const bool in_ring = &w >= slots && &w < slots + kSlots;
@@ -1585,7 +1646,21 @@ struct vdb_ivf {
                                 mfma_min, bounded_stats ? stats.p + 5 : nullptr};
         // the bounded items first (the batch's most-probed lists), on the same stream
         if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
-        if (wide && fused_scan) {
+        if (screened) {
+            vdbk::launch_screen_pairs(metric, w.q, B, P, w.probes.p, cent_rm.p, dp, slot_buf(w, w.qres, (size_t)BP * dp),
+                                      slot_buf(w, w.pst, BP), s);
+            sa.shadow = screen_sh.p;
+            sa.rows = screen_rows.p;
+            sa.meta = screen_meta.p;
+            sa.qres = w.qres.p;
+            sa.pst = w.pst.p;
+            sa.dp = dp;
+            sa.P = P;
+            sa.segs_item = 4;
+            sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks, vdbk::kPersistentBlocks / 2));
+            const uint64_t want = std::max<uint64_t>(max_wide, (max_items + 3) / 4);
+            vdbk::launch_scan_screen(metric, (uint32_t)(scan_blocks ? std::min<uint64_t>(want, scan_blocks) : want), sa, s);
+        } else if (wide && fused_scan) {
             // one persistent grid takes both queues (no side stream, no fork/join)
             // (narrow_blocks counts 4-wave workgroups: as many waves start on the narrow queue)
             const uint32_t grid_cap = waves == 8 ? vdbk::kPersistentBlocks / 2 : vdbk::kPersistentBlocks;

@@ -17,42 +17,11 @@
 #include <type_traits>
 
 #include "kernels.hpp"
+#include "scan_common.hpp"
 #include "wave_topk.hpp"
 
 
 namespace vdbk {
-
-enum { kL2 = 0, kIP = 1, kCos = 2 };
-
-template <int M>
-__device__ __forceinline__ float dist_term(float acc, float a, float b) {
-    if constexpr (M == kL2) {
-        const float diff = a - b;
-        return acc + diff * diff;
-    } else if constexpr (M == kIP) {
-        return acc + a * b;
-    } else {
-        return acc;  // Cosine: the CPU path never assigns a distance (cpp:351-362)
-    }
-}
-template <int M>
-__device__ __forceinline__ float dist_finish(float acc) {
-    if constexpr (M == kIP) return -acc;
-    return acc;
-}
-
-template <int M>
-__device__ __forceinline__ float acc4(float acc, const float4 q, const float4 x) {
-    acc = dist_term<M>(acc, q.x, x.x);
-    acc = dist_term<M>(acc, q.y, x.y);
-    acc = dist_term<M>(acc, q.z, x.z);
-    acc = dist_term<M>(acc, q.w, x.w);
-    return acc;
-}
-
-__device__ __forceinline__ uint32_t wave_index() {
-    return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-}
 
 // Grid-stride helpers. An HSA dispatch packet holds the grid size in work-items as
 // 32 bits, so every element-wise launch caps its grid (launch_grid) and strides.
@@ -113,14 +82,6 @@ __device__ __forceinline__ float nan_last(float d) { return d == d ? d : __built
 
 // Order-preserving float <-> uint32 map (a < b as floats <=> enc(a) < enc(b) as
 // unsigned), so shared thresholds can be lowered with integer atomic minimum.
-__device__ __forceinline__ uint32_t ord_enc(float f) {
-    const uint32_t b = __float_as_uint(f);
-    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
-__device__ __forceinline__ float ord_dec(uint32_t u) {
-    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
-}
-constexpr uint32_t kThrInf = 0xFF800000u;  // ord_enc(+inf)
 
 
 // ============================================================================
@@ -1053,15 +1014,6 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
 // the segment, which the arena's slack block keeps in bounds.
 //   compute(x, t): consume tile t (0 <= t < d4) of the current block
 //   finish(j, id): block j done; id = this lane's id slot in block j
-
-// List data is read once per batch: non-temporal loads (nt) keep it from displacing
-// reusable lines and stream measurably faster on gfx950 (tools/stream_probe.hip:
-// 6.8 vs 6.25 TB/s for this access pattern).
-typedef float v4f_nt __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 load_nt(const float4* p) {
-    const v4f_nt v = __builtin_nontemporal_load((const v4f_nt*)p);
-    return make_float4(v.x, v.y, v.z, v.w);
-}
 
 template <int T, class Compute, class Finish>
 __device__ __forceinline__ void stream_blocks(const float4* __restrict__ base, const uint64_t* __restrict__ ids,

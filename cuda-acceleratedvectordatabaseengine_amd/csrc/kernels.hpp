@@ -119,6 +119,16 @@ struct ScanArgs {
     uint32_t mfma_min;     // wide items of >= this many queries run the bounded (MFMA) waves (0: never)
     unsigned long long* mstats;  // bounded-scan statistics (option bounded_stats; null by default):
                                  // [0] exact re-ranks, [1] bounded blocks
+    // Screened scan (screen.hip): the lists' bf16 residual shadow in MFMA B-operand order,
+    // their fp32 rows in slot order (exact re-checks) and per-slot norms; per (query, probe)
+    // pair (q * P + p) the bf16 A rows [B * P][dp] and their norms.
+    const uint4* __restrict__ shadow = nullptr;
+    const float* __restrict__ rows = nullptr;
+    const float4* __restrict__ meta = nullptr;
+    const uint16_t* __restrict__ qres = nullptr;
+    const float4* __restrict__ pst = nullptr;
+    uint32_t dp = 0;
+    uint32_t P = 0;
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);
@@ -130,6 +140,14 @@ void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipSt
 size_t scan_bounded_lds(uint32_t d4, uint32_t k);
 bool scan_bounded_fits(uint32_t d4, uint32_t k);
 void launch_scan_bounded(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
+// ---- screened scan (screen.hip): L2 / IP, k <= 64, lists in HBM ----
+bool scan_screen_fits(uint32_t k, uint32_t dp);
+size_t screen_shadow_u4(uint64_t blocks, uint32_t d4);  // shadow size (uint4) incl. the prefetch slack
+void launch_screen_build(const float4* arena, uint64_t blocks, uint32_t d4, const uint32_t* block_list,
+                         const float* cent_rm, uint4* shadow, float* rows, float4* meta, hipStream_t s);
+void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, const uint32_t* probes,
+                         const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, hipStream_t s);
+void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                        const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,

@@ -1,0 +1,515 @@
+// screen.hip — the screened fine scan (search_list_cpu, ivf_flat_index.cpp:339-384), the
+// default scan for L2 / IP with k <= 64 on lists held in HBM.
+//
+// Every (query, list vector) distance is first SCREENED on the matrix cores from a bf16
+// shadow of the lists, and the reference's exact sequential fp32 sum is computed only
+// for the pairs that can still reach the list's top-k. Results are bit-identical to the
+// exact scan (kernels.hip ivf_scan_wide / ivf_scan_narrow):
+//  * Shadow: each list block of 64 vectors is also stored as bf16 RESIDUALS b' = bf16(x - c)
+//    against the list's centroid c, in the B-operand order of v_mfma_f32_16x16x32_bf16:
+//    per k-step s (32 dims) and vector tile vt (16 vectors), lane l holds vector
+//    16 vt + (l & 15), dims 32 s + 8 (l >> 4) .. + 8 — one 1 KiB wave-load per MFMA operand,
+//    half the bytes of the fp32 stream. Residuals keep the bound proportional to the spread
+//    of the list rather than to |x|, so clustered data screens as well as iid data.
+//  * Screen: A = per (query, probed list) bf16 rows a' (L2: a = q - c; IP: a = q), so D lane l
+//    holds <a', b'> for vector v = 16 vt + (l & 15) and queries g = 4 (l >> 4) + r.
+//      L2: |q - x|^2 = |a|^2 + |b|^2 - 2 <a, b>,  approx = |a|^2 + |b|^2 - 2 <a', b'>
+//      IP: -<q, x> = -(<q, c> + <q, b>),           approx = -(<q, c> + <q', b'>)
+//    With e = b - b', f = a - a' (measured per vector / pair in double, rounded up),
+//      |<a, b> - <a', b'>| <= (|a| + |f|) |e| + |f| (|b| + |e|) + |f| |e|   (Cauchy-Schwarz)
+//    and the MFMA's f32 accumulation, the reference's own rounding (its sequential fp32 sum
+//    is within 2 (n + 4) u of the real value relative to (|a| + |b|)^2, resp. |q| |x|), the
+//    float rounding of the norms and of approx are all below (12 dp + 64) u S^2 (S: the sum
+//    of every norm involved, u = 2^-24). delta is padded further (x 1.001, + 1e-6 |approx|,
+//    + 1e-30) for its own rounding and for subnormals.
+//  * A pair is a candidate unless approx - delta > th, th = min(the wave's own k-th, the
+//    list-wide shared k-th, the block bound below): a pair above th is strictly worse than
+//    k vectors of the same list and cannot be in the list's multiset top-k (the exact
+//    scan's pruning rule). NaN / inf anywhere makes the test false, so such pairs are always
+//    re-checked; vectors, centroids or queries with a non-finite or huge (> 2^50) value carry
+//    |e| or |f| = inf.
+//  * Candidates are compacted into a per-wave LDS ring and recomputed exactly in rounds
+//    of 64 (one lane per pair: the reference's d = 0..D-1 sum over the fp32 row, from a
+//    row-major copy of the lists in slot order), then offered to the query's top-k exactly
+//    as the exact scan does (ties always kept). Every k-th reached is published to the
+//    list-wide thresholds at once, and every block re-reads them.
+// Items, partials and merges are the exact scan's (kernels.hip).
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+
+#include "kernels.hpp"
+#include "scan_common.hpp"
+#include "wave_topk.hpp"
+
+namespace vdbk {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr float kScreenHuge = 1125899906842624.0f;  // 2^50: larger magnitudes are never screened
+constexpr int kRing = 512;                          // candidate ring entries per wave
+#ifndef VDB_SCREEN_EXACT_PIPE
+#define VDB_SCREEN_EXACT_PIPE 4
+#endif
+constexpr int kExactPipe = VDB_SCREEN_EXACT_PIPE;   // float4 of a row in flight per lane (exact re-check)
+// Timing experiment (a separate build, never an option): 1 drops the candidates instead
+// of re-checking them (the screen stream alone; results INVALID).
+#ifndef VDB_SCREEN_DIAG
+#define VDB_SCREEN_DIAG 0
+#endif
+
+// Nearest bf16, ties to even; +0 for |f| < 2^-126 (no bf16 subnormals reach the matrix
+// cores, and |e| accounts for the flush). Non-finite inputs are flagged by the caller.
+__device__ __forceinline__ uint32_t bf16_bits(float f) {
+    const uint32_t b = __float_as_uint(f);
+    const uint32_t ex = b & 0x7F800000u;
+    if (ex == 0) return 0u;
+    if (ex == 0x7F800000u) return 0x7FC0u;
+    return (b + 0x7FFFu + ((b >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf16_val(uint32_t h) { return __uint_as_float(h << 16); }
+
+__device__ __forceinline__ uint4 pack_bf16x8(const float4 lo, const float4 hi) {
+    uint4 r;
+    r.x = bf16_bits(lo.x) | (bf16_bits(lo.y) << 16);
+    r.y = bf16_bits(lo.z) | (bf16_bits(lo.w) << 16);
+    r.z = bf16_bits(hi.x) | (bf16_bits(hi.y) << 16);
+    r.w = bf16_bits(hi.z) | (bf16_bits(hi.w) << 16);
+    return r;
+}
+
+// x - c rounded to float (the value the shadow's bf16 rounds), from the exact double difference
+__device__ __forceinline__ float4 resid(const float4 x, const float4 c) {
+    return make_float4((float)((double)x.x - c.x), (float)((double)x.y - c.y), (float)((double)x.z - c.z),
+                       (float)((double)x.w - c.w));
+}
+
+// ---- build: the residual shadow, the row-major fp32 copy and the per-slot norms
+// {|b|^2, |b| up, |b - b'| up, |x| up} of every arena block (one wave per block of 64
+// vectors; lane = vector; block_list: the list each block belongs to).
+__device__ __forceinline__ float ru(double v) { return __double2float_ru(v * (1.0 + 0x1p-30)); }
+
+__global__ __launch_bounds__(256) void ivf_screen_build(const float4* __restrict__ arena, uint64_t blocks,
+                                                        uint32_t d4, const uint32_t* __restrict__ block_list,
+                                                        const float* __restrict__ cent_rm, uint4* __restrict__ shadow,
+                                                        float* __restrict__ rows, float4* __restrict__ meta) {
+    const int lane = lane_id();
+    const uint32_t dp = d4 * 4, ks = dp / 32;
+    for (uint64_t b = (uint64_t)blockIdx.x * 4 + wave_index(); b < blocks; b += (uint64_t)gridDim.x * 4) {
+        const float4* blk = arena + b * d4 * 64;
+        const float4* cen = (const float4*)(cent_rm + (size_t)block_list[b] * dp);
+        const uint64_t slot = b * 64 + lane;
+        float4* row = (float4*)(rows + slot * dp);
+        double x2 = 0.0, b2 = 0.0, e2 = 0.0;
+        bool huge = false;
+        for (uint32_t t = 0; t < d4; ++t) {
+            const float4 x = blk[(size_t)t * 64 + lane];
+            const float4 c = cen[t];
+            row[t] = x;
+            const float xv[4] = {x.x, x.y, x.z, x.w}, cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double bd = (double)xv[i] - (double)cv[i];
+                const double ed = bd - (double)bf16_val(bf16_bits((float)bd));
+                huge |= !(fabs(bd) <= (double)kScreenHuge) || !(fabsf(xv[i]) <= kScreenHuge);
+                x2 += (double)xv[i] * xv[i];
+                b2 += bd * bd;
+                e2 += ed * ed;
+            }
+        }
+        meta[slot] = huge ? make_float4(__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff())
+                          : make_float4((float)b2, ru(sqrt(b2)), ru(sqrt(e2)), ru(sqrt(x2)));
+        uint4* sh = shadow + b * (uint64_t)d4 * 32;
+        const int vv = lane & 15, h = lane >> 4;
+        for (uint32_t s = 0; s < ks; ++s) {
+            const float4 c0 = cen[8 * s + 2 * h], c1 = cen[8 * s + 2 * h + 1];
+            for (int vt = 0; vt < 4; ++vt) {
+                const float4 lo = blk[(size_t)(8 * s + 2 * h) * 64 + 16 * vt + vv];
+                const float4 hi = blk[(size_t)(8 * s + 2 * h + 1) * 64 + 16 * vt + vv];
+                sh[((size_t)s * 4 + vt) * 64 + lane] = pack_bf16x8(resid(lo, c0), resid(hi, c1));
+            }
+        }
+    }
+}
+
+// ---- per batch: per (query, probe) pair i = q * P + p the MFMA A row a' (bf16, [BP][dp]) and
+// its norms pst[i]: L2 (a = q - c): {|a|^2, |a| up, |a - a'| up, 0}; IP (a = q):
+// {<q, c>, |q| up, |q - q'| up, |c| up}. One wave per pair; flagged (inf) when q, c or a
+// holds a non-finite or huge value.
+template <int M>
+__global__ __launch_bounds__(256) void ivf_screen_pairs(const float* __restrict__ q, uint32_t BP, uint32_t P,
+                                                        const uint32_t* __restrict__ probes,
+                                                        const float* __restrict__ cent_rm, uint32_t dp,
+                                                        uint16_t* __restrict__ qres, float4* __restrict__ pst) {
+    const int lane = lane_id();
+    for (uint32_t i = blockIdx.x * 4 + wave_index(); i < BP; i += gridDim.x * 4) {
+        const float* qr = q + (size_t)(i / P) * dp;
+        const float* cr = cent_rm + (size_t)probes[i] * dp;
+        double a2 = 0.0, f2 = 0.0, c2 = 0.0, qc = 0.0;
+        bool huge = false;
+        for (uint32_t d = lane; d < dp; d += 64) {
+            const float qv = qr[d], cv = cr[d];
+            const double ad = M == kL2 ? (double)qv - (double)cv : (double)qv;
+            const uint32_t h = bf16_bits((float)ad);
+            qres[(size_t)i * dp + d] = (uint16_t)h;
+            const double fd = ad - (double)bf16_val(h);
+            huge |= !(fabs(ad) <= (double)kScreenHuge) || !(fabsf(qv) <= kScreenHuge) || !(fabsf(cv) <= kScreenHuge);
+            a2 += ad * ad;
+            f2 += fd * fd;
+            c2 += (double)cv * cv;
+            qc += (double)qv * cv;
+        }
+        for (int m = 32; m >= 1; m >>= 1) {
+            a2 += __shfl_xor(a2, m);
+            f2 += __shfl_xor(f2, m);
+            c2 += __shfl_xor(c2, m);
+            qc += __shfl_xor(qc, m);
+        }
+        huge = __ballot(huge) != 0;
+        if (lane == 0) {
+            const float inf = __builtin_inff();
+            if (huge) pst[i] = make_float4(inf, inf, inf, inf);
+            else if (M == kL2) pst[i] = make_float4((float)a2, ru(sqrt(a2)), ru(sqrt(f2)), 0.0f);
+            else pst[i] = make_float4((float)qc, ru(sqrt(a2)), ru(sqrt(f2)), ru(sqrt(c2)));
+        }
+    }
+}
+
+// Bitonic sort of x over each 16-lane row (DPP exchanges), then the row's c-th smallest
+// (1 <= c <= 16) in every lane of the row. Every lane of the wave must be active.
+__device__ __forceinline__ float row_sorted_at(float x, int c) {
+    const int l = lane_id() & 15;
+#define VDB_ROW_STEP(SIZE, STRIDE)                                           \
+    {                                                                        \
+        const float y = xor_f<STRIDE>(x);                                    \
+        const bool keep_min = ((l & SIZE) == 0) == ((l & STRIDE) == 0);      \
+        x = keep_min ? fminf(x, y) : fmaxf(x, y);                            \
+    }
+    VDB_ROW_STEP(2, 1)
+    VDB_ROW_STEP(4, 2) VDB_ROW_STEP(4, 1)
+    VDB_ROW_STEP(8, 4) VDB_ROW_STEP(8, 2) VDB_ROW_STEP(8, 1)
+    VDB_ROW_STEP(16, 8) VDB_ROW_STEP(16, 4) VDB_ROW_STEP(16, 2) VDB_ROW_STEP(16, 1)
+#undef VDB_ROW_STEP
+    return __shfl(x, (lane_id() & ~15) + c - 1);
+}
+
+__device__ __forceinline__ uint4 ld_nt_u4(const uint4* p) {
+    const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ bf16x8 as_bf16x8(const uint4 v) {
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// One wave: segment `seg` of list it.list against the nq (<= 16) queries of the item
+// starting at sorted pair it.pair_start + q0. tk_d / tk_i: this wave's per-query top-k
+// lists (16 x k, LDS); kdl: its per-query k-th distances; s_thr: the shared k-th of the
+// item's queries (LDS, lowered with atomicMin); ring: the candidate ring (kRing).
+template <int M, int KD>
+__device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
+                                               const uint32_t seg, float* tk_d, uint64_t* tk_i, float* kdl,
+                                               uint32_t* s_thr, uint32_t* ring) {
+    const int lane = lane_id();
+    const uint32_t dp = a.dp, ks = dp >> 5, d4 = a.d4;
+    const uint32_t count = a.count[it.list];
+    const uint32_t seg_vectors = a.seg_blocks * 64;
+    const uint64_t b0 = a.block_off[it.list] + (uint64_t)seg * a.seg_blocks;
+    const uint32_t v0 = seg * seg_vectors;
+    const uint32_t nv = min(count - v0, seg_vectors);
+    const uint32_t nb = (nv + 63) >> 6;
+    const int k = (int)a.k;
+    const uint32_t* pairs = a.sorted_pair + it.pair_start + q0;
+    const float c2 = (float)(12 * dp + 64) * 0x1p-24f;
+
+    for (int e = lane; e < 16 * k; e += 64) {
+        tk_d[e] = __builtin_inff();
+        tk_i[e] = kNoId;
+    }
+    if (lane < 16) kdl[lane] = __builtin_inff();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+
+    // (query, probe) pair index of the item's query g: the A rows and norms are per pair
+    auto pair_of = [&](int g) -> uint32_t {
+        const uint32_t pr = pairs[g];
+        return (pr >> 16) * a.P + (pr & 0xFFFFu);
+    };
+    // the MFMA A row of this lane: query (lane & 15), its dims 8 (lane >> 4) .. + 8 of each k-step
+    const int ga = min(lane & 15, nq - 1);
+    const uint4* qa_row = (const uint4*)(a.qres + (size_t)pair_of(ga) * dp) + (lane >> 4);
+    // the D rows of this lane: queries 4 (lane >> 4) + r
+    float4 pst[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pst[r] = a.pst[pair_of(min(4 * (lane >> 4) + r, nq - 1))];
+
+    uint32_t head = 0, tail = 0;  // wave-uniform ring cursors
+
+    // Exact re-check of up to 64 ring entries (one per lane), then the top-k offers.
+    auto exact_round = [&](uint32_t n) {
+        const bool act = lane < (int)n;
+        const uint32_t ent = ring[(head + (act ? (uint32_t)lane : 0u)) & (kRing - 1)];
+        head += n;
+        if (a.mstats && lane == 0) atomicAdd(&a.mstats[0], (unsigned long long)n);
+        const int g = (int)(ent >> 16);
+        const uint32_t v = ent & 0xFFFFu;
+        const uint64_t slot = (b0 + (v >> 6)) * 64 + (v & 63);
+        const float4* xr = (const float4*)(a.rows + slot * dp);
+        const float4* qr = (const float4*)(a.qpad + (size_t)(pairs[g] >> 16) * dp);
+        float acc = 0.0f;
+        float4 xb[kExactPipe], qb[kExactPipe];
+#pragma unroll
+        for (int i = 0; i < kExactPipe; ++i) {
+            xb[i] = xr[i];
+            qb[i] = qr[i];
+        }
+        for (uint32_t t0 = 0; t0 < d4; t0 += kExactPipe) {
+#pragma unroll
+            for (int i = 0; i < kExactPipe; ++i) {
+                acc = acc4<M>(acc, qb[i], xb[i]);
+                if (t0 + kExactPipe < d4) {
+                    xb[i] = xr[t0 + kExactPipe + i];
+                    qb[i] = qr[t0 + kExactPipe + i];
+                }
+            }
+        }
+        const float dist = dist_finish<M>(acc);
+        const uint64_t vid = a.ids[slot];
+        uint32_t present = 0;
+        for (int gq = 0; gq < nq; ++gq)
+            if (__ballot(act && g == gq)) present |= 1u << gq;
+        while (present) {
+            const int gs = __builtin_ctz(present);
+            present &= present - 1;
+            const float kdg = fminf(kdl[gs], ord_dec(s_thr[gs]));
+            float* sd = tk_d + gs * k;
+            uint64_t* si = tk_i + gs * k;
+            WaveTopK<1> tk;
+            tk.d[0] = lane < k ? sd[lane] : __builtin_inff();
+            tk.id[0] = lane < k ? si[lane] : kNoId;
+            float nkd;
+            uint64_t nki;
+            tk.at(k - 1, nkd, nki);
+            offer_lanes<1>(tk, act && g == gs && dist <= kdg, dist, vid, k, nkd, nki);
+            if (lane < k) {
+                sd[lane] = tk.d[0];
+                si[lane] = tk.id[0];
+            }
+            if (lane == 0) kdl[gs] = nkd;
+            if (nkd < kdg && lane == 0) {
+                atomicMin(&s_thr[gs], ord_enc(nkd));
+                atomicMin(&a.thr[it.pair_start + q0 + gs], ord_enc(nkd));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
+    };
+
+    // the screen: stream the segment's shadow blocks through the matrix cores, KD k-steps
+    // (4 x 1 KiB each) in flight; the pipeline runs KD steps past the segment (slack)
+    const uint4* sp = a.shadow + b0 * (uint64_t)dp * 8 + lane;
+    uint4 xa[KD][4], qa[KD];
+#pragma unroll
+    for (int u = 0; u < KD; ++u) {
+#pragma unroll
+        for (int vt = 0; vt < 4; ++vt) xa[u][vt] = ld_nt_u4(sp + (size_t)(u * 4 + vt) * 64);
+        qa[u] = qa_row[4 * (u % ks)];
+    }
+    for (uint32_t j = 0; j < nb; ++j) {
+        f32x4 acc[4];
+#pragma unroll
+        for (int vt = 0; vt < 4; ++vt) acc[vt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (uint32_t s0 = 0; s0 < ks; s0 += KD) {
+            static_for<0, KD>([&](auto uu) {
+                constexpr int u = decltype(uu)::value;
+                const bf16x8 A = as_bf16x8(qa[u]);
+#pragma unroll
+                for (int vt = 0; vt < 4; ++vt)
+                    acc[vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, as_bf16x8(xa[u][vt]), acc[vt], 0, 0, 0);
+                const uint64_t nxt = (uint64_t)j * ks + s0 + u + KD;
+#pragma unroll
+                for (int vt = 0; vt < 4; ++vt) xa[u][vt] = ld_nt_u4(sp + (nxt * 4 + vt) * 64);
+                qa[u] = qa_row[4 * ((s0 + u + KD) % ks)];
+            });
+        }
+        // Bounds of the block's 64 x 16 pairs: lower bounds replace the dot products in acc;
+        // per query, the lane's largest upper bound over its 4 vectors (invalid / NaN: inf).
+        float mx[4] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+#pragma unroll
+        for (int vt = 0; vt < 4; ++vt) {
+            const float4 mt = a.meta[(b0 + j) * 64 + 16 * vt + (lane & 15)];
+            const bool valid = j * 64 + 16 * vt + (lane & 15) < nv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float dot = acc[vt][r];
+                const float4 ps = pst[r];
+                const float approx = M == kL2 ? (ps.x + mt.x) - 2.0f * dot : -(ps.x + dot);
+                const float S = M == kL2 ? ps.y + mt.y + ps.z + mt.z : ps.y + mt.w + ps.w + mt.y + ps.z + mt.z;
+                float del = (ps.y + ps.z) * mt.z + ps.z * (mt.y + mt.z) + ps.z * mt.z;
+                if (M == kL2) del = 2.0f * del;
+                del = (del + c2 * (S * S)) * 1.001f + 1e-6f * fabsf(approx) + 1e-30f;
+                const float ub = approx + del;
+                acc[vt][r] = approx - del;
+                mx[r] = fmaxf(mx[r], valid && ub == ub ? ub : __builtin_inff());
+            }
+        }
+        // Block bound per query: the ceil(k/4)-th smallest of those lane maxima over the
+        // query's 16 lanes (one DPP row) — at least k vectors of this segment have exact
+        // distances at or below it, so a pair whose lower bound exceeds it is strictly worse
+        // than k vectors of the list.
+        float tb[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int g = min(4 * (lane >> 4) + r, nq - 1);
+            tb[r] = fminf(row_sorted_at(mx[r], (k + 3) >> 2), ord_dec(a.thr[it.pair_start + q0 + g]));
+        }
+#pragma unroll
+        for (int vt = 0; vt < 4; ++vt) {
+            const uint32_t v = j * 64 + 16 * vt + (lane & 15);
+            const bool valid = v < nv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int g = 4 * (lane >> 4) + r;
+                // (re-read per tile: the exact rounds of the previous tile lower them)
+                const float th = g < nq ? fminf(tb[r], fminf(kdl[g], ord_dec(s_thr[g]))) : -__builtin_inff();
+                const bool cand = valid && g < nq && !(acc[vt][r] > th);
+                const uint64_t m = __ballot(cand);
+                if (cand) {
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    ring[(tail + below) & (kRing - 1)] = ((uint32_t)g << 16) | v;
+                }
+                tail += (uint32_t)__popcll(m);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            // full rounds as they fill; the segment's last tile drains the ring
+            const uint32_t need = (j + 1 == nb && vt == 3) ? 1u : 64u;
+            if (VDB_SCREEN_DIAG & 1) head = tail;
+            while (tail - head >= need) exact_round(min(64u, tail - head));
+        }
+    }
+    if (a.mstats && lane == 0) atomicAdd(&a.mstats[1], (unsigned long long)nb);
+    // the segment's k-th distances lower the list-wide thresholds; its top-k is one partial
+    for (int g = 0; g < nq; ++g) {
+        const float kg = kdl[g];
+        if (lane == 0 && kg < __builtin_inff()) atomicMin(&a.thr[it.pair_start + q0 + g], ord_enc(kg));
+        const uint32_t part = a.part_base_sorted[it.pair_start + q0 + g] + seg;
+        if (lane < k) {
+            a.part_d[(size_t)part * k + lane] = tk_d[g * k + lane];
+            a.part_i[(size_t)part * k + lane] = tk_i[g * k + lane];
+        }
+    }
+}
+
+// Per-wave dynamic LDS: tk_i [16 k] u64 | tk_d [16 k] f32 | kdl [16] f32 | s_thr [16] u32 | ring [kRing] u32.
+__host__ __device__ constexpr size_t screen_wave_lds(uint32_t k) { return (size_t)16 * k * 12 + 64 + 64 + kRing * 4; }
+
+// ivf_scan_screen: persistent grid (two 4-wave workgroups per CU) over the plan's queues,
+// like ivf_scan_wide: wide items (a list's segments x <= 16 queries; the 4 waves take the
+// segments dynamically and share the item's thresholds), then narrow items (one wave each:
+// one segment x <= 4 queries). The last a.fused workgroups start on the narrow queue.
+template <int M, int KD>
+__global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t slds[];
+    const uint32_t wv = wave_index();
+    char* base = (char*)slds + (size_t)wv * screen_wave_lds(a.k);
+    uint64_t* tk_i = (uint64_t*)base;
+    float* tk_d = (float*)(base + (size_t)16 * a.k * 8);
+    float* kdl = tk_d + 16 * a.k;
+    uint32_t* s_thr_w = (uint32_t*)(kdl + 16);
+    uint32_t* ring = s_thr_w + 16;
+    __shared__ uint32_t s_next, s_seg;
+    __shared__ uint32_t s_thr[16];
+    const int lane = lane_id();
+
+    auto drain_narrow = [&]() {
+        const uint32_t n_narrow = a.counters[0];
+        for (;;) {
+            uint32_t idx = 0;
+            if (lane == 0) idx = atomicAdd(&a.work[0], 1u);
+            idx = __builtin_amdgcn_readfirstlane(idx);
+            if (idx >= n_narrow) break;
+            ScanItem it = a.items[idx];
+            it.list = __builtin_amdgcn_readfirstlane(it.list);
+            it.seg = __builtin_amdgcn_readfirstlane(it.seg);
+            it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
+            it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
+            if (lane < (int)it.npairs) s_thr_w[lane] = a.thr[it.pair_start + lane];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            screen_segment<M, KD>(a, it, 0, (int)it.npairs, it.seg, tk_d, tk_i, kdl, s_thr_w, ring);
+        }
+    };
+
+    const uint32_t n_wide = a.counters[3];
+    uint32_t stride = a.wide_stride;
+    if (stride > 1 && n_wide % stride == 0) stride = stride == 40009u ? 40013u : 40009u;
+    if (a.fused && blockIdx.x + a.fused >= gridDim.x) drain_narrow();
+    for (;;) {
+        if (threadIdx.x == 0) s_next = atomicAdd(&a.work[1], 1u);
+        __syncthreads();
+        const uint32_t b = s_next;
+        if (b >= n_wide) break;
+        const uint32_t item = stride > 1 ? (uint32_t)(((uint64_t)b * stride) % n_wide) : b;
+        ScanItem it = a.items_w[item];
+        it.list = __builtin_amdgcn_readfirstlane(it.list);
+        it.seg = __builtin_amdgcn_readfirstlane(it.seg);
+        it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
+        it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
+        const int nq = (int)it.npairs;
+        if (threadIdx.x == 0) s_seg = 0;
+        if (threadIdx.x < (uint32_t)nq) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
+        __syncthreads();
+        const uint32_t seg_vectors = a.seg_blocks * 64;
+        const uint32_t nseg = (a.count[it.list] + seg_vectors - 1) / seg_vectors;
+        const uint32_t seg0 = it.seg * a.segs_item, seg1 = min(nseg, seg0 + a.segs_item);
+        for (;;) {
+            uint32_t sg = 0;
+            if (lane == 0) sg = atomicAdd(&s_seg, 1u);
+            sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
+            if (sg >= seg1) break;
+            screen_segment<M, KD>(a, it, 0, nq, sg, tk_d, tk_i, kdl, s_thr, ring);
+        }
+        __syncthreads();  // s_thr / s_seg are reset by the next item
+    }
+    if (a.fused) drain_narrow();
+}
+
+bool scan_screen_fits(uint32_t k, uint32_t dp) {
+    return k >= 1 && k <= 64 && dp % 64 == 0 && 4 * screen_wave_lds(k) + 128 <= kLdsBytes / 2;
+}
+
+size_t screen_shadow_u4(uint64_t blocks, uint32_t d4) { return (size_t)(blocks + 2) * d4 * 32; }
+
+void launch_screen_build(const float4* arena, uint64_t blocks, uint32_t d4, const uint32_t* block_list,
+                         const float* cent_rm, uint4* shadow, float* rows, float4* meta, hipStream_t s) {
+    if (!blocks) return;
+    const uint32_t g = (uint32_t)std::min<uint64_t>((blocks + 3) / 4, 8192);
+    ivf_screen_build<<<g, 256, 0, s>>>(arena, blocks, d4, block_list, cent_rm, shadow, rows, meta);
+}
+
+void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, const uint32_t* probes,
+                         const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, hipStream_t s) {
+    const uint32_t BP = B * P;
+    if (!BP) return;
+    const uint32_t g = std::min<uint32_t>((BP + 3) / 4, 2048);
+    if (metric == kL2) ivf_screen_pairs<kL2><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst);
+    else ivf_screen_pairs<kIP><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst);
+}
+
+void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
+    if (!grid_blocks) return;
+    const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
+    const size_t lds = 4 * screen_wave_lds(a.k);
+    const bool kd4 = (a.dp / 32) % 4 == 0;
+    if (metric == kL2) {
+        if (kd4) ivf_scan_screen<kL2, 4><<<g, 256, lds, s>>>(a);
+        else ivf_scan_screen<kL2, 2><<<g, 256, lds, s>>>(a);
+    } else {
+        if (kd4) ivf_scan_screen<kIP, 4><<<g, 256, lds, s>>>(a);
+        else ivf_scan_screen<kIP, 2><<<g, 256, lds, s>>>(a);
+    }
+}
+
+}  // namespace vdbk

@@ -82,8 +82,8 @@ typedef struct vdb_ivf_profile {
     uint64_t work_items;       /* sum over batches of scan work items */
     uint64_t scan_bytes;       /* algorithmic bytes read by ivf_scan: 4 * dim * scan_vectors */
     uint64_t pair_vectors;     /* sum over batches and (query, probe) pairs of n_l: distances computed */
-    uint64_t exact_reranks;    /* bounded scan: (query, vector) distances recomputed exactly (option bounded_stats) */
-    uint64_t bounded_blocks;   /* bounded scan: 64-vector blocks bounded on the matrix cores (option bounded_stats) */
+    uint64_t exact_reranks;    /* screened / bounded scan: (query, vector) distances recomputed exactly (option bounded_stats) */
+    uint64_t bounded_blocks;   /* screened / bounded scan: 64-vector blocks bounded on the matrix cores (option bounded_stats) */
     uint64_t computed_vectors; /* query slots the scan streams per vector: pair_vectors plus one per
                                   odd wide group (its last query runs alone, on scalar ops) */
     double local_merge_ms;     /* summed per-batch merges after the scan (segment, slot, query top-k) */
@@ -289,11 +289,14 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * 64/128/256/512/1024: list vectors per scan segment), "coalesce" (0/1), "coalesce_max_queries",
  * "coalesce_window_us" (0: no waiting; calls arriving while the device is busy batch up),
  * "fused_scan" (1, default: one persistent scan grid takes both the wide and the narrow
- * items; 0: narrow items on a second stream), "list_cache_bytes" (0 = every list HBM-resident; > 0 = the list-cache tier above with an
+ * items; 0: narrow items on a second stream), "screen" (1, default: the screened scan — bf16
+ * matrix-core distance bounds from a shadow of the lists, exact fp32 sums only for pairs that can
+ * reach a list's top-k; L2/IP, k <= 64, lists in HBM; costs 1.5x the list bytes of extra HBM;
+ * 0: the exact VALU scan of every pair), "list_cache_bytes" (0 = every list HBM-resident; > 0 = the list-cache tier above with an
  * HBM cache of that many bytes; a search whose single query probes more fails with
  * VDB_ERR_OUT_OF_MEMORY, a batch probing more is split; setting it replaces the
  * max_gpu_memory cap), "max_gpu_memory" (the Config cap, applied at once), "bounded_stats"
- * (0/1: count the opt-in bounded scan's re-ranks in vdb_ivf_profile). Timing experiments
+ * (0/1: count the screened / bounded scan's exact re-checks and blocks in vdb_ivf_profile). Timing experiments
  * that change results exist only as separate builds (VDB_SCAN_DIAG), never as options. */
 int vdb_ivf_set_option(vdb_ivf* index, const char* name, int64_t value);
 /* Host-API coalescing counters: device batches run and search() calls they served. */

@@ -75,6 +75,7 @@ def search_all(g, Q, nprobe, k, batch):
 def test_bounded_hub_lists(metric, k):
     X, ids, lists, C, Q = hub_data(48, seed=3 + k)
     g, o = lists_pair(X, ids, lists, C, metric)
+    g.set_option("screen", 0)  # (the bounded scan serves only with the screen off)
     nprobe = 3 if metric == 0 else 6  # IP: every list (the origin centroid ties at 0)
     Dr, Ir = o.search(Q, nprobe, k)
     for mm in (1, 8, 0):  # every wide item bounded / items of >= 8 queries / never (the default)
@@ -90,6 +91,7 @@ def test_bounded_hub_lists(metric, k):
 def test_bounded_path_is_taken_and_prunes():
     X, ids, lists, C, Q = hub_data(64, seed=5)
     g, o = lists_pair(X, ids, lists, C, 0)
+    g.set_option("screen", 0)  # (the bounded scan serves only with the screen off)
     g.set_option("scan_mfma_min", 1)
     g.set_option("bounded_stats", 1)  # statistics only: results stay valid
     g.profile_reset()
@@ -117,6 +119,7 @@ def test_bounded_cancellation_every_pair_a_candidate(metric):
     ids = np.arange(12000, dtype=np.uint64)
     C = np.stack([c, -c]).astype(np.float32)
     g, o = lists_pair(X, ids, lists, C, metric)
+    g.set_option("screen", 0)  # (the bounded scan serves only with the screen off)
     Dr, Ir = o.search(Q, 2, 10)
     g.set_option("scan_mfma_min", 1)
     g.set_option("bounded_stats", 1)
@@ -146,6 +149,7 @@ def test_bounded_ties_duplicates_nonfinite():
     C = np.zeros((2, dim), np.float32)
     C[1] = 5.0
     g, o = lists_pair(X, ids, lists, C, 0)
+    g.set_option("screen", 0)  # (the bounded scan serves only with the screen off)
     Q = np.concatenate([base[:48] + 1e-3 * rng.standard_normal((48, dim)).astype(np.float32),
                         rng.standard_normal((40, dim)).astype(np.float32)])
     for k in (5, 10, 40):
@@ -160,6 +164,7 @@ def test_bounded_ties_duplicates_nonfinite():
 def test_bounded_odd_dimensions(dim):
     X, ids, lists, C, Q = hub_data(dim, seed=dim, n_hub=12000, n_other=800)
     g, o = lists_pair(X, ids, lists, C, 0)
+    g.set_option("screen", 0)  # (the bounded scan serves only with the screen off)
     g.set_option("scan_mfma_min", 1)
     assert_same(*search_all(g, Q, 3, 10, 130), *o.search(Q, 3, 10))
     g.set_option("scan_mfma_min", 0)

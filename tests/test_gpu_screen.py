@@ -1,0 +1,163 @@
+"""GPU parity of the screened scan (screen.hip, the default scan for L2 / IP, k <= 64):
+every (query, vector) distance is bounded on the matrix cores from a bf16 shadow of the
+lists and recomputed with the reference's sequential fp32 sum (search_list_cpu,
+ivf_flat_index.cpp:347-370) only where it can reach the list's top-k. Results must stay
+bit-identical to the oracle whatever the screen prunes, so these cases stress it: hub
+lists probed by every query, both metrics, k up to the screen's 64 and just past it (the
+exact scan then serves), a cancellation regime where the bound is wider than the whole
+distance spread, ties, duplicate ids, infinite / overflowing / huge / subnormal values,
+odd dimensions (both operand pipelines), incremental adds (the shadow is rebuilt), the
+residency cap, and the screen against the exact scan on a trained index.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import load_vdb
+from test_gpu_bounded import assert_same, hub_data, lists_pair, search_all
+
+vdb = load_vdb()
+pytestmark = pytest.mark.gpu
+
+
+def screen_stats(g, Q, nprobe, k, batch):
+    g.set_option("bounded_stats", 1)  # statistics only: results stay valid
+    g.profile_reset()
+    D, I = search_all(g, Q, nprobe, k, batch)
+    p = g.profile_read()
+    g.set_option("bounded_stats", 0)
+    return D, I, p
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("k", [1, 10, 16, 17, 64, 65])
+def test_screen_hub_lists(metric, k):
+    X, ids, lists, C, Q = hub_data(48, seed=30 + k)
+    g, o = lists_pair(X, ids, lists, C, metric)
+    nprobe = 3 if metric == 0 else 6
+    Dr, Ir = o.search(Q, nprobe, k)
+    for batch in (64, 130):
+        for seg in (0, 64, 1024):
+            g.set_option("seg_vectors", seg)
+            assert_same(*search_all(g, Q, nprobe, k, batch), Dr, Ir)
+    g.set_option("screen", 0)
+    assert_same(*search_all(g, Q, nprobe, k, 130), Dr, Ir)
+
+
+def test_screen_is_taken_and_prunes():
+    X, ids, lists, C, Q = hub_data(64, seed=5)
+    g, o = lists_pair(X, ids, lists, C, 0)
+    D, I, p = screen_stats(g, Q, 3, 10, 130)
+    print("screen stats", p)
+    assert_same(D, I, *o.search(Q, 3, 10))
+    assert p["bounded_blocks"] > 0, p
+    # every query scans the 30000-vector hub list: iid data prunes most pairs, even with the
+    # 64-vector segments this small index gets (each segment pays its own first block)
+    assert 0 < p["exact_reranks"] < 0.3 * p["pair_vectors"], p
+    g.set_option("screen", 0)
+    D, I, p = screen_stats(g, Q, 3, 10, 130)
+    assert p["bounded_blocks"] == 0 and p["exact_reranks"] == 0, p
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_screen_cancellation_every_pair_a_candidate(metric):
+    """Vectors and queries in a tiny ball far from the origin: |q|, |x| ~ 100 while the
+    distances are ~ 1e-2, so the screen's bound exceeds the whole distance spread and
+    every pair goes through the exact re-check."""
+    rng = np.random.default_rng(11)
+    dim = 40
+    c = (100.0 / np.sqrt(dim)) * np.ones(dim, np.float32)
+    X = (c + 0.01 * rng.standard_normal((12000, dim))).astype(np.float32)
+    Q = (c + 0.01 * rng.standard_normal((96, dim))).astype(np.float32)
+    lists = (rng.random(12000) >= 0.8).astype(np.int64)
+    ids = np.arange(12000, dtype=np.uint64)
+    C = np.stack([c, -c]).astype(np.float32)
+    g, o = lists_pair(X, ids, lists, C, metric)
+    Dr, Ir = o.search(Q, 2, 10)
+    D, I, p = screen_stats(g, Q, 2, 10, 96)
+    assert_same(D, I, Dr, Ir)
+    if metric == 0:
+        assert p["exact_reranks"] > 0.5 * p["pair_vectors"], p
+
+
+def test_screen_ties_duplicates_nonfinite_huge_subnormal():
+    rng = np.random.default_rng(17)
+    dim = 32
+    base = rng.standard_normal((3000, dim)).astype(np.float32)
+    X = np.concatenate([base, base, base[:500]])           # exact duplicate vectors: equal distances
+    ids = np.concatenate([np.arange(3000), np.arange(3000) + 10000, np.arange(500)]).astype(np.uint64)
+    # (no NaN: the reference ranks with std::partial_sort on (dist, id) pairs, and a NaN
+    # key breaks its strict weak order, so where it lands is undefined behaviour)
+    X[17, 3] = np.inf
+    X[31, :] = -np.inf
+    X[40, 5] = 3.0e38                                      # finite, overflows when squared
+    X[41, 7] = 2.0e15                                      # above the screen's 2^50 limit
+    X[42, :] = 1.0e-39                                     # subnormal coordinates (flushed in the shadow)
+    X[43, 0] = 1.0e-40
+    X[44, :8] = 1.5e-38
+    lists = np.zeros(len(X), np.int64)
+    lists[rng.random(len(X)) < 0.1] = 1
+    C = np.zeros((2, dim), np.float32)
+    C[1] = 5.0
+    g, o = lists_pair(X, ids, lists, C, 0)
+    Q = np.concatenate([base[:48] + 1e-3 * rng.standard_normal((48, dim)).astype(np.float32),
+                        rng.standard_normal((40, dim)).astype(np.float32),
+                        np.full((1, dim), 1e-39, np.float32),         # a subnormal query
+                        np.zeros((1, dim), np.float32)])               # the zero query
+    Q[60, 2] = 1.0e20                                                  # a huge query coordinate
+    for k in (5, 10, 40):
+        Dr, Ir = o.search(Q, 2, k)
+        assert_same(*search_all(g, Q, 2, k, 90), Dr, Ir)
+        assert_same(*search_all(g, Q, 2, k, 7), Dr, Ir)
+
+
+@pytest.mark.parametrize("dim", [1, 3, 67, 130, 256])
+@pytest.mark.parametrize("metric", [0, 1])
+def test_screen_odd_dimensions(dim, metric):
+    X, ids, lists, C, Q = hub_data(dim, seed=dim + 7, n_hub=12000, n_other=800)
+    g, o = lists_pair(X, ids, lists, C, metric)
+    nprobe = 3 if metric == 0 else 6
+    assert_same(*search_all(g, Q, nprobe, 10, 130), *o.search(Q, nprobe, 10))
+
+
+def test_screen_rebuilt_after_incremental_adds_and_under_the_cap():
+    X, Q, ids = oracle.reference_test_data(20000, 120, 64)
+    nlist, nprobe, k = 32, 8, 10
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(64, nlist, vdb.Metric.L2, device=0))
+    o = oracle.OracleIndex(64, nlist, 0)
+    g.train(X[:5000])
+    o.train(X[:5000])
+    for a, b in ((0, 7000), (7000, 7001), (7001, 20000)):
+        g.add(X[a:b], ids[a:b])
+        o.add(X[a:b], ids[a:b])
+        D, I, p = screen_stats(g, Q, nprobe, k, 64)
+        assert_same(D, I, *o.search(Q, nprobe, k))
+        assert p["bounded_blocks"] > 0, p
+    # a residency cap that holds the lists but not the screen's 1.5x extra: exact scan
+    g.set_option("max_gpu_memory", int(20000 * (64 * 4 + 8) * 1.2))
+    D, I, p = screen_stats(g, Q, nprobe, k, 64)
+    assert_same(D, I, *o.search(Q, nprobe, k))
+    assert p["bounded_blocks"] == 0, p
+    g.set_option("max_gpu_memory", 0)
+    D, I, p = screen_stats(g, Q, nprobe, k, 64)
+    assert_same(D, I, *o.search(Q, nprobe, k))
+    assert p["bounded_blocks"] > 0, p
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_screen_equals_exact_scan_on_trained_index(metric):
+    """gpu_vs_cpu_test's shape with stale slots: screened and exact scans, and the oracle."""
+    X, Q, ids = oracle.reference_test_data(30000, 300, 96)
+    nlist = 64
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(96, nlist, vdb.Metric(metric), device=0))
+    o = oracle.OracleIndex(96, nlist, metric)
+    g.train(X[:8000])
+    o.train(X[:8000])
+    g.add(X, ids)
+    o.add(X, ids)
+    for nprobe, k in ((1, 10), (8, 10), (16, 64), (64, 3)):
+        Dr, Ir = o.search(Q, nprobe, k)
+        g.set_option("screen", 1)
+        assert_same(*search_all(g, Q, nprobe, k, 100), Dr, Ir)
+        g.set_option("screen", 0)
+        assert_same(*search_all(g, Q, nprobe, k, 100), Dr, Ir)

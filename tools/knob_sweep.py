@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 DEFAULTS = {"seg_vectors": 0, "segs_per_item": 0, "wide_stride": 1, "fused_scan": 1, "narrow_blocks": 64,
-            "wide_group": 16, "fused_merge": 1, "scan_window": 0}
+            "wide_group": 16, "fused_merge": 1, "scan_window": 0, "screen": 1, "bounded_stats": 0}
 
 
 def main():
@@ -55,6 +55,7 @@ def main():
                 idx.search_device(q[j * B:].data_ptr(), B, args.nprobe, 10, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
             torch.cuda.synchronize()
             idx.profile_enable(True)
+            idx.set_option("bounded_stats", 1)  # statistics only
             idx.profile_reset()
             t0 = time.perf_counter()
             for j in range(steps):
@@ -69,7 +70,8 @@ def main():
                               "search_ms": round(p["total_ms"] / n, 3), "wall_ms": round(wall, 3),
                               "alg_GB": round(alg / 1e9, 2),
                               "pairs_M": round(p["pair_vectors"] / max(p["batches"], 1) / 1e6, 2),
-                              "computed_M": round(p["computed_vectors"] / max(p["batches"], 1) / 1e6, 2), "frac": round(alg / (p["scan_ms"] / n * 1e-3) / 8e12, 4)}),
+                              "computed_M": round(p["computed_vectors"] / max(p["batches"], 1) / 1e6, 2), "frac": round(alg / (p["scan_ms"] / n * 1e-3) / 8e12, 4),
+                              "rechecks_M": round(p["exact_reranks"] / max(p["batches"], 1) / 1e6, 3)}),
                   flush=True)
             for n_, _ in opts:  # back to defaults
                 idx.set_option(n_, DEFAULTS[n_])
