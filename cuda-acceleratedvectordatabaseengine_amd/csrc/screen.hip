@@ -180,6 +180,47 @@ __global__ __launch_bounds__(256) void ivf_screen_pairs(const float* __restrict_
     }
 }
 
+// One compare-exchange stage of a bitonic sort of 64 values held as u[v] in the 16 lanes of
+// a DPP row: element e = 4 (lane & 15) + v (strides 1, 2 within a lane, 4 .. 32 across lanes).
+template <int SIZE, int STRIDE>
+__device__ __forceinline__ void bitonic64_step(float (&u)[4], int l) {
+    if constexpr (STRIDE < 4) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            if (v & STRIDE) continue;
+            const int w = v | STRIDE;
+            const bool asc = ((4 * l + v) & SIZE) == 0;
+            const float lo = fminf(u[v], u[w]), hi = fmaxf(u[v], u[w]);
+            u[v] = asc ? lo : hi;
+            u[w] = asc ? hi : lo;
+        }
+    } else {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const float p = xor_f<STRIDE / 4>(u[v]);
+            const int e = 4 * l + v;
+            const bool keep_min = ((e & SIZE) == 0) == ((e & STRIDE) == 0);
+            u[v] = keep_min ? fminf(u[v], p) : fmaxf(u[v], p);
+        }
+    }
+}
+// The kk-th smallest (1 <= kk <= 64) of the 64 values u[0..3] x 16 lanes of each DPP row, in
+// every lane of the row (u is sorted in place). Every lane of the wave must be active.
+__device__ __forceinline__ float block_kth(float (&u)[4], int kk) {
+    const int l = lane_id() & 15;
+    bitonic64_step<2, 1>(u, l);
+    bitonic64_step<4, 2>(u, l), bitonic64_step<4, 1>(u, l);
+    bitonic64_step<8, 4>(u, l), bitonic64_step<8, 2>(u, l), bitonic64_step<8, 1>(u, l);
+    bitonic64_step<16, 8>(u, l), bitonic64_step<16, 4>(u, l), bitonic64_step<16, 2>(u, l), bitonic64_step<16, 1>(u, l);
+    bitonic64_step<32, 16>(u, l), bitonic64_step<32, 8>(u, l), bitonic64_step<32, 4>(u, l);
+    bitonic64_step<32, 2>(u, l), bitonic64_step<32, 1>(u, l);
+    bitonic64_step<64, 32>(u, l), bitonic64_step<64, 16>(u, l), bitonic64_step<64, 8>(u, l);
+    bitonic64_step<64, 4>(u, l), bitonic64_step<64, 2>(u, l), bitonic64_step<64, 1>(u, l);
+    const int e = kk - 1, v = e & 3;
+    const float x = v == 0 ? u[0] : v == 1 ? u[1] : v == 2 ? u[2] : u[3];
+    return __shfl(x, (lane_id() & ~15) + (e >> 2));
+}
+
 // Bitonic sort of x over each 16-lane row (DPP exchanges), then the row's c-th smallest
 // (1 <= c <= 16) in every lane of the row. Every lane of the wave must be active.
 __device__ __forceinline__ float row_sorted_at(float x, int c) {
@@ -241,10 +282,11 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
     // the MFMA A row of this lane: query (lane & 15), its dims 8 (lane >> 4) .. + 8 of each k-step
     const int ga = min(lane & 15, nq - 1);
     const uint4* qa_row = (const uint4*)(a.qres + (size_t)pair_of(ga) * dp) + (lane >> 4);
-    // the D rows of this lane: queries 4 (lane >> 4) + r
-    float4 pst[4];
+    // the D rows of this lane: queries 4 (lane >> 4) + r (their norms are re-read per block:
+    // L1 hits, and no registers held across the stream)
+    const float4* pst_r[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) pst[r] = a.pst[pair_of(min(4 * (lane >> 4) + r, nq - 1))];
+    for (int r = 0; r < 4; ++r) pst_r[r] = a.pst + pair_of(min(4 * (lane >> 4) + r, nq - 1));
 
     uint32_t head = 0, tail = 0;  // wave-uniform ring cursors
 
@@ -301,7 +343,8 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
             if (lane == 0) kdl[gs] = nkd;
             if (nkd < kdg && lane == 0) {
                 atomicMin(&s_thr[gs], ord_enc(nkd));
-                atomicMin(&a.thr[it.pair_start + q0 + gs], ord_enc(nkd));
+                uint32_t* gt = a.thr + it.pair_start + q0 + gs;
+                if (nkd < ord_dec(*gt)) atomicMin(gt, ord_enc(nkd));
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         }
@@ -334,9 +377,12 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
                 qa[u] = qa_row[4 * ((s0 + u + KD) % ks)];
             });
         }
-        // Bounds of the block's 64 x 16 pairs: lower bounds replace the dot products in acc;
-        // per query, the lane's largest upper bound over its 4 vectors (invalid / NaN: inf).
-        float mx[4] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+        // Bounds of the block's 64 x 16 pairs: lower bounds replace the dot products in acc,
+        // upper bounds go to ubv (invalid vectors and NaN: +inf).
+        float ubv[4][4];
+        float4 pst[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pst[r] = *pst_r[r];
 #pragma unroll
         for (int vt = 0; vt < 4; ++vt) {
             const float4 mt = a.meta[(b0 + j) * 64 + 16 * vt + (lane & 15)];
@@ -352,18 +398,28 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
                 del = (del + c2 * (S * S)) * 1.001f + 1e-6f * fabsf(approx) + 1e-30f;
                 const float ub = approx + del;
                 acc[vt][r] = approx - del;
-                mx[r] = fmaxf(mx[r], valid && ub == ub ? ub : __builtin_inff());
+                ubv[r][vt] = valid && ub == ub ? ub : __builtin_inff();
             }
         }
-        // Block bound per query: the ceil(k/4)-th smallest of those lane maxima over the
-        // query's 16 lanes (one DPP row) — at least k vectors of this segment have exact
-        // distances at or below it, so a pair whose lower bound exceeds it is strictly worse
-        // than k vectors of the list.
+        // Block bound per query: the k-th smallest upper bound of the block's 64 vectors (a
+        // bitonic sort over the query's 16 lanes x 4 registers). k vectors of the list have
+        // exact distances at or below it, so it is a valid shared threshold: published to the
+        // item's and the list-wide thresholds at once, so that every segment of the list that
+        // starts later (or reads them at its next block) prunes against it.
+        // (Published only where it improves on the current list-wide value: a hub list's
+        // blocks would otherwise serialise on the same few addresses.)
         float tb[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int g = min(4 * (lane >> 4) + r, nq - 1);
-            tb[r] = fminf(row_sorted_at(mx[r], (k + 3) >> 2), ord_dec(a.thr[it.pair_start + q0 + g]));
+            const int g = 4 * (lane >> 4) + r;
+            const uint32_t* gt = a.thr + it.pair_start + q0 + min(g, nq - 1);
+            const float cur = fminf(ord_dec(*gt), ord_dec(s_thr[min(g, nq - 1)]));
+            const float t = block_kth(ubv[r], k);
+            if ((lane & 15) == 0 && g < nq && t < cur) {
+                atomicMin(&s_thr[g], ord_enc(t));
+                atomicMin((uint32_t*)gt, ord_enc(t));
+            }
+            tb[r] = fminf(t, cur);
         }
 #pragma unroll
         for (int vt = 0; vt < 4; ++vt) {

@@ -61,9 +61,11 @@ def test_screen_is_taken_and_prunes():
 
 @pytest.mark.parametrize("metric", [0, 1])
 def test_screen_cancellation_every_pair_a_candidate(metric):
-    """Vectors and queries in a tiny ball far from the origin: |q|, |x| ~ 100 while the
-    distances are ~ 1e-2, so the screen's bound exceeds the whole distance spread and
-    every pair goes through the exact re-check."""
+    """Vectors and queries in a tiny ball far from the origin (|q|, |x| ~ 100, distances
+    ~ 1e-2) stored in lists whose centroids are far from the ball: the residuals are as
+    large as the vectors, so the screen's bound exceeds the whole distance spread and
+    every pair goes through the exact re-check. (With centroids at the ball the residual
+    shadow screens this data well: the second half.)"""
     rng = np.random.default_rng(11)
     dim = 40
     c = (100.0 / np.sqrt(dim)) * np.ones(dim, np.float32)
@@ -71,13 +73,20 @@ def test_screen_cancellation_every_pair_a_candidate(metric):
     Q = (c + 0.01 * rng.standard_normal((96, dim))).astype(np.float32)
     lists = (rng.random(12000) >= 0.8).astype(np.int64)
     ids = np.arange(12000, dtype=np.uint64)
-    C = np.stack([c, -c]).astype(np.float32)
+    C = np.stack([np.zeros_like(c), -c]).astype(np.float32)
     g, o = lists_pair(X, ids, lists, C, metric)
     Dr, Ir = o.search(Q, 2, 10)
     D, I, p = screen_stats(g, Q, 2, 10, 96)
     assert_same(D, I, Dr, Ir)
     if metric == 0:
         assert p["exact_reranks"] > 0.5 * p["pair_vectors"], p
+    C = np.stack([c, c + 0.05]).astype(np.float32)
+    g, o = lists_pair(X, ids, lists, C, metric)
+    Dr, Ir = o.search(Q, 2, 10)
+    D, I, p = screen_stats(g, Q, 2, 10, 96)
+    assert_same(D, I, Dr, Ir)
+    if metric == 0:
+        assert p["exact_reranks"] < 0.5 * p["pair_vectors"], p
 
 
 def test_screen_ties_duplicates_nonfinite_huge_subnormal():
