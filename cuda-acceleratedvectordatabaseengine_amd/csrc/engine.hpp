@@ -302,6 +302,7 @@ struct vdb_ivf {
     // the list bytes does not fit (Config::max_gpu_memory, or a failed allocation).
     bool screen_opt = true;
     bool screen_ready = false;
+    uint32_t screen_segs_auto = 4;  // segments per screened wide item (upload_directory; option segs_per_item)
     DevBuf<uint4> screen_sh;
     DevBuf<float> screen_rows;
     DevBuf<float4> screen_meta;
@@ -727,6 +728,20 @@ struct vdb_ivf {
         HIPCHECK(hipMemcpyAsync(d_count_local.ensure(nlist), cl.data(), nlist * 4, hipMemcpyHostToDevice, stream));
         HIPCHECK(hipMemcpyAsync(d_count_global.ensure(nlist), cg.data(), nlist * 4, hipMemcpyHostToDevice, stream));
         HIPCHECK(hipMemcpyAsync(d_nseg.ensure(nlist), ns.data(), nlist * 4, hipMemcpyHostToDevice, stream));
+        // Screened items: a wave carries its top-k across the segments it takes from one item,
+        // so items of long lists take more segments (its thresholds tighten over more
+        // vectors); short lists keep 4 for parallelism. By the size-weighted mean segment
+        // count of the stored lists (measured: iid 10M x 768, 40 per list: 8; the 1/8 shard
+        // of 100M x 768, ~200: 16; the mixture, 5: 4).
+        {
+            double wsum = 0.0, wseg = 0.0;
+            for (uint32_t l = 0; l < nlist; ++l) {
+                wsum += cl[l];
+                wseg += (double)cl[l] * ns[l];
+            }
+            const double mean_seg = wsum > 0 ? wseg / wsum : 0.0;
+            screen_segs_auto = mean_seg < 16.0 ? 4u : (mean_seg < 96.0 ? 8u : 16u);
+        }
         std::vector<uint32_t> sorted(ns);
         std::sort(sorted.begin(), sorted.end(), std::greater<uint32_t>());
         nseg_prefix.assign(nlist + 1, 0);
@@ -1631,7 +1646,10 @@ struct vdb_ivf {
                                           vdbk::scan_bounded_fits(d4, k)
                                       ? scan_mfma_min : 0u;
         const int plan_wide = screened ? vdbk::kWideGroup : (wide ? (int)wide_group : 0);
-        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, plan_wide, screened ? 4u : segs_item, w.items.p, w.items_w.p,
+        // (screened items: segs_per_item segments, default 4; a wave's top-k carries across
+        // the segments it takes from one item)
+        const uint32_t segs_screen = segs_item_opt ? segs_item_opt : screen_segs_auto;
+        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, plan_wide, screened ? segs_screen : segs_item, w.items.p, w.items_w.p,
                           w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, w.thr.p,
                           mfma_min, s);
         const bool in_ring = &w >= slots && &w < slots + kSlots;
@@ -1656,7 +1674,7 @@ struct vdb_ivf {
             sa.pst = w.pst.p;
             sa.dp = dp;
             sa.P = P;
-            sa.segs_item = 4;
+            sa.segs_item = segs_screen;
             sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks, vdbk::kPersistentBlocks / 2));
             const uint64_t want = std::max<uint64_t>(max_wide, (max_items + 3) / 4);
             vdbk::launch_scan_screen(metric, (uint32_t)(scan_blocks ? std::min<uint64_t>(want, scan_blocks) : want), sa, s);

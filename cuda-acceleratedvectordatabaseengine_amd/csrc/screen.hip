@@ -249,12 +249,14 @@ __device__ __forceinline__ bf16x8 as_bf16x8(const uint4 v) {
 
 // One wave: segment `seg` of list it.list against the nq (<= 16) queries of the item
 // starting at sorted pair it.pair_start + q0. tk_d / tk_i: this wave's per-query top-k
-// lists (16 x k, LDS); kdl: its per-query k-th distances; s_thr: the shared k-th of the
-// item's queries (LDS, lowered with atomicMin); ring: the candidate ring (kRing).
+// lists (16 x k, LDS), reset when `fresh` (else they carry the wave's earlier segments of
+// the same item, so its thresholds keep improving); kdl: its per-query k-th distances;
+// s_thr: the shared k-th of the item's queries (LDS, lowered with atomicMin); ring: the
+// candidate ring (kRing). The caller writes the partials (screen_partials).
 template <int M, int KD>
 __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
                                                const uint32_t seg, float* tk_d, uint64_t* tk_i, float* kdl,
-                                               uint32_t* s_thr, uint32_t* ring) {
+                                               uint32_t* s_thr, uint32_t* ring, const bool fresh) {
     const int lane = lane_id();
     const uint32_t dp = a.dp, ks = dp >> 5, d4 = a.d4;
     const uint32_t count = a.count[it.list];
@@ -265,14 +267,22 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
     const uint32_t nb = (nv + 63) >> 6;
     const int k = (int)a.k;
     const uint32_t* pairs = a.sorted_pair + it.pair_start + q0;
-    const float c2 = (float)(12 * dp + 64) * 0x1p-24f;
+    // rounding coefficients of the bound (u = 2^-24, 1 % margin): the MFMA's f32 sum of dp
+    // exact bf16 products (4 (dp + 4) u, a 4x margin over sequential accumulation), the
+    // reference's sequential sum ((dp + 2) u relative to its terms), the norms' and approx's
+    // own roundings
+    const float cm = (float)(4 * dp + 16) * 0x1.02p-24f;
+    const float cr = (float)(dp + 2) * 0x1.02p-24f;
+    const float cu = 0x1.02p-23f;
 
-    for (int e = lane; e < 16 * k; e += 64) {
-        tk_d[e] = __builtin_inff();
-        tk_i[e] = kNoId;
+    if (fresh) {
+        for (int e = lane; e < 16 * k; e += 64) {
+            tk_d[e] = __builtin_inff();
+            tk_i[e] = kNoId;
+        }
+        if (lane < 16) kdl[lane] = __builtin_inff();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
-    if (lane < 16) kdl[lane] = __builtin_inff();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 
     // (query, probe) pair index of the item's query g: the A rows and norms are per pair
     auto pair_of = [&](int g) -> uint32_t {
@@ -392,10 +402,21 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
                 const float dot = acc[vt][r];
                 const float4 ps = pst[r];
                 const float approx = M == kL2 ? (ps.x + mt.x) - 2.0f * dot : -(ps.x + dot);
-                const float S = M == kL2 ? ps.y + mt.y + ps.z + mt.z : ps.y + mt.w + ps.w + mt.y + ps.z + mt.z;
-                float del = (ps.y + ps.z) * mt.z + ps.z * (mt.y + mt.z) + ps.z * mt.z;
-                if (M == kL2) del = 2.0f * del;
-                del = (del + c2 * (S * S)) * 1.001f + 1e-6f * fabsf(approx) + 1e-30f;
+                // Cauchy-Schwarz term of <a, b> - <a', b'>, and the MFMA's accumulation bound
+                const float an = ps.y + ps.z, bn = mt.y + mt.z;
+                const float cs = an * mt.z + ps.z * bn + ps.z * mt.z;
+                float del;
+                if (M == kL2) {
+                    // |approx - |a - b|^2| <= rest; the reference's sum is within cr |a - b|^2
+                    // <= cr (|approx| + rest) of the real value
+                    const float rest = 2.0f * (cs + cm * (an * bn)) + cu * (ps.x + mt.x + fabsf(approx));
+                    del = rest + cr * (fabsf(approx) + rest);
+                } else {
+                    // IP: -(<q, c> + <q', b'>); the reference's sum is within cr |q| |x| (mt.w),
+                    // <q, c> rounded to float within u |q| |c| (ps.w)
+                    del = cs + cm * (an * bn) + cr * (ps.y * mt.w) + cu * (ps.y * ps.w + an * bn + fabsf(approx));
+                }
+                del = del * 1.001f + 1e-30f;
                 const float ub = approx + del;
                 acc[vt][r] = approx - del;
                 ubv[r][vt] = valid && ub == ub ? ub : __builtin_inff();
@@ -447,14 +468,22 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
         }
     }
     if (a.mstats && lane == 0) atomicAdd(&a.mstats[1], (unsigned long long)nb);
-    // the segment's k-th distances lower the list-wide thresholds; its top-k is one partial
+}
+
+// The partials of segment `seg` for the item's nq queries: the wave's top-k lists (`keep`),
+// or empty (inf, no id) for a segment whose vectors live on in the wave's lists and reach
+// the merge through a later segment's partial. Every vector the wave scanned is in exactly
+// one partial, so the merge's multiset top-min(k, n_l) of the union is the list's.
+__device__ __forceinline__ void screen_partials(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
+                                                const uint32_t seg, const float* tk_d, const uint64_t* tk_i,
+                                                const bool keep) {
+    const int lane = lane_id();
+    const int k = (int)a.k;
     for (int g = 0; g < nq; ++g) {
-        const float kg = kdl[g];
-        if (lane == 0 && kg < __builtin_inff()) atomicMin(&a.thr[it.pair_start + q0 + g], ord_enc(kg));
         const uint32_t part = a.part_base_sorted[it.pair_start + q0 + g] + seg;
         if (lane < k) {
-            a.part_d[(size_t)part * k + lane] = tk_d[g * k + lane];
-            a.part_i[(size_t)part * k + lane] = tk_i[g * k + lane];
+            a.part_d[(size_t)part * k + lane] = keep ? tk_d[g * k + lane] : __builtin_inff();
+            a.part_i[(size_t)part * k + lane] = keep ? tk_i[g * k + lane] : kNoId;
         }
     }
 }
@@ -494,7 +523,8 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
             it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
             if (lane < (int)it.npairs) s_thr_w[lane] = a.thr[it.pair_start + lane];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            screen_segment<M, KD>(a, it, 0, (int)it.npairs, it.seg, tk_d, tk_i, kdl, s_thr_w, ring);
+            screen_segment<M, KD>(a, it, 0, (int)it.npairs, it.seg, tk_d, tk_i, kdl, s_thr_w, ring, true);
+            screen_partials(a, it, 0, (int)it.npairs, it.seg, tk_d, tk_i, true);
         }
     };
 
@@ -520,13 +550,19 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
         const uint32_t seg_vectors = a.seg_blocks * 64;
         const uint32_t nseg = (a.count[it.list] + seg_vectors - 1) / seg_vectors;
         const uint32_t seg0 = it.seg * a.segs_item, seg1 = min(nseg, seg0 + a.segs_item);
+        // A wave keeps its top-k lists across the segments it takes from the item; each
+        // segment it moves on from gets empty partials, its last one the lists.
+        uint32_t prev = ~0u;
         for (;;) {
             uint32_t sg = 0;
             if (lane == 0) sg = atomicAdd(&s_seg, 1u);
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
-            screen_segment<M, KD>(a, it, 0, nq, sg, tk_d, tk_i, kdl, s_thr, ring);
+            if (prev != ~0u) screen_partials(a, it, 0, nq, prev, tk_d, tk_i, false);
+            screen_segment<M, KD>(a, it, 0, nq, sg, tk_d, tk_i, kdl, s_thr, ring, prev == ~0u);
+            prev = sg;
         }
+        if (prev != ~0u) screen_partials(a, it, 0, nq, prev, tk_d, tk_i, true);
         __syncthreads();  // s_thr / s_seg are reset by the next item
     }
     if (a.fused) drain_narrow();

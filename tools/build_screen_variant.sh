@@ -10,7 +10,7 @@ P=$R/cuda-acceleratedvectordatabaseengine_amd
 O=$R/_variants/$N
 mkdir -p "$O"
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wall -I$R/include"
-/opt/rocm/bin/hipcc $F "$@" -c "$P/csrc/screen.hip" -I"$P/csrc" -o "$O/screen.o"
+/opt/rocm/bin/hipcc $F "$@" -c "${SRC:-$P/csrc/screen.hip}" -I"$P/csrc" -o "$O/screen.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libvdb_ivf.so" "$P/build/kernels.o" "$O/screen.o" \
     "$P/build/engine.o" "$P/build/group.o" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f "$O/screen.o"
