@@ -694,6 +694,7 @@ def timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, che
 
     device_wait(args, world, idx, streams, rank)
     idx.profile_enable(True)
+    idx.set_option("bounded_stats", 1)  # the screen's re-check count (roofline bytes); never changes results
     idx.profile_reset()
     s_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.prof_steps)]
     e_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.prof_steps)]
@@ -704,6 +705,7 @@ def timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, che
     device_wait(args, world, idx, streams, rank)
     prof = idx.profile_read()
     idx.profile_enable(False)
+    idx.set_option("bounded_stats", 0)
     step_ms_single = [a.elapsed_time(b) for a, b in zip(s_ev, e_ev)]
     p99_single = percentile(step_ms_single, 0.99)
     mine = rank_breakdown(rank, prof, elapsed * 1e3 / max(args.steps, 1), step_ms_single)
@@ -853,7 +855,19 @@ def run(vdb, args, device, rank, world):
 
     launches = max(prof["scan_launches"], 1)
     scan_ms = prof["scan_ms"] / launches
-    bytes_per_launch = prof["scan_bytes"] / max(prof["batches"], 1)
+    batches = max(prof["batches"], 1)
+    fp32_bytes = prof["scan_bytes"] / batches  # 4 D per vector of the batch's distinct probed lists
+    # The screened scan (default) streams the lists' bf16 residual shadow (2 dp B per vector)
+    # and 16 B of norms, and reads the fp32 row (4 dp B) of every re-checked pair: its
+    # algorithmic bytes. The exact scan reads the fp32 lists once per batch.
+    screened = prof.get("bounded_blocks", 0) > 0
+    dp = -(-args.dim // 64) * 64
+    if screened:
+        vecs = prof["scan_vectors"] / batches
+        rechecks = prof["exact_reranks"] / batches
+        bytes_per_launch = vecs * (2 * dp + 16) + rechecks * 4 * dp
+    else:
+        bytes_per_launch = fp32_bytes
     achieved = bytes_per_launch / (scan_ms * 1e-3) / 1e9 if scan_ms > 0 else 0.0
     key = f"{args.nvec}x{args.dim}/{args.nlist}/{args.nprobe}/{B}/{k}/N{world}"
     if args.data != "iid":
@@ -899,7 +913,12 @@ def run(vdb, args, device, rank, world):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "ivf_scan",
+            "kernel": "ivf_scan_screen" if screened else "ivf_scan_wide",
+            "bytes_model": ("screened: 2 dp B bf16 shadow + 16 B norms per vector of the distinct probed lists "
+                            "+ 4 dp B per exactly re-checked (query, vector) pair" if screened else
+                            "exact: 4 D B per vector of the distinct probed lists"),
+            "fp32_list_bytes_per_batch": int(fp32_bytes),
+            "fp32_equivalent_GBps": round(fp32_bytes / (scan_ms * 1e-3) / 1e9, 1) if scan_ms > 0 else None,
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
