@@ -302,6 +302,7 @@ struct vdb_ivf {
     // the list bytes does not fit (Config::max_gpu_memory, or a failed allocation).
     bool screen_opt = true;
     bool screen_ready = false;
+    bool screen_stale = false;  // lists or centroids changed since the last build
     uint32_t screen_segs_auto = 4;  // segments per screened wide item (upload_directory; option segs_per_item)
     DevBuf<uint4> screen_sh;
     DevBuf<float> screen_rows;
@@ -747,11 +748,15 @@ struct vdb_ivf {
         nseg_prefix.assign(nlist + 1, 0);
         for (uint32_t j = 0; j < nlist; ++j) nseg_prefix[j + 1] = nseg_prefix[j] + sorted[j];
         HIPCHECK(hipStreamSynchronize(stream));  // host vectors above are stack-owned
-        screen_update();
+        screen_stale = true;  // rebuilt by the next search (a bulk add appends in many calls)
     }
 
-    // (Re)build the screened scan's data from the arena (quiesced by the caller), or drop it.
+    // (Re)build the screened scan's data from the arena, or drop it. Called by the first
+    // search after the lists or centroids change (every search issued before the change
+    // was quiesced by it, and none since has read the data) and by the options that
+    // decide whether it exists.
     void screen_update() {
+        screen_stale = false;
         screen_ready = false;
         const bool want = screen_opt && metric != 2 && !tiered() && !arena.host && arena_blocks > 0;
         const uint64_t extra = arena_blocks * 64 * ((uint64_t)dp * 6 + 16);  // shadow + rows + norms
@@ -1301,7 +1306,7 @@ struct vdb_ivf {
         quiesce();
         vdbk::launch_interleave(cent_rm.p, nlist, dp, cent_il.p, stream);
         HIPCHECK(hipGetLastError());
-        if (arena_blocks) screen_update();  // the shadow holds residuals against the centroids
+        screen_stale = true;  // the shadow holds residuals against the centroids
     }
 
     // assign_to_lists (cpp:259-295): exact argmin with ties to the lowest centroid. For
@@ -1641,6 +1646,7 @@ struct vdb_ivf {
         // wide items of many queries: bounded on the matrix cores (L2 / IP, 16-query items)
         // the screened scan (default): its items are the exact scan's 16-query wide items
         // and narrow items
+        if (screen_stale) screen_update();
         const bool screened = screen_ready && !tiered() && regs_k == 1 && metric != 2 && vdbk::scan_screen_fits(k, dp);
         const uint32_t mfma_min = !screened && wide && waves == 4 && metric != 2 && !(VDB_SCAN_DIAG & 2) &&
                                           vdbk::scan_bounded_fits(d4, k)
