@@ -82,23 +82,22 @@ def test_cfg3_10m_x_768_nlist4096_nprobe32_two_batches_in_flight():
     assert np.all(np.isfinite(D)) and np.all(D >= 0) and np.all(I < n)
 
 
-@pytest.mark.timeout(900)
-def test_cfg4_all_8_shards_and_final_merge_100m_x_768_nlist16384_nprobe64():
-    """configs[3] whole: "100M x 768, nlist 16384, nprobe 64, lists sharded across 8 GPUs
-    with the top-k merge". One exact assignment pass over the 100M rows; then, one shard
-    at a time on this GPU, every rank r of the LPT plan (plan_shard + append of its rows):
-    its partial results for the queries (one search call, written as its packed rank
-    record) against oracle_search_shard over only that shard's probed lists (host memory
-    freed before the next shard). Finally the 8 GPU records are merged on the device
-    (vdb_merge_ranks_packed_device, the merge every rank runs after the all-gather) and
-    compared with the oracle's merge of its 8 partials: the final cfg4 answer."""
+CFG4 = dict(n=100_000_000, dim=768, nlist=16384, nprobe=64, k=10, world=8, chunk=10_000_000, nq=4)
+_cfg4 = {}
+
+
+def _cfg4_setup():
+    """One exact assignment pass over the 100M rows (shared by the two cfg4 tests)."""
+    if _cfg4:
+        return _cfg4
     import torch
-    n, dim, nlist, nprobe, k, world, chunk, nq = 100_000_000, 768, 16384, 64, 10, 8, 10_000_000, 4
+    c = CFG4
+    n, dim, nlist, chunk, nq = c["n"], c["dim"], c["nlist"], c["chunk"], c["nq"]
     dev = torch.device("cuda", 0)
-    with torch.cuda.stream(torch.cuda.Stream(dev)):
-        s = torch.cuda.current_stream().cuda_stream
+    st = torch.cuda.Stream(dev)
+    with torch.cuda.stream(st):
+        s = st.cuda_stream
         data = torch.empty((chunk, dim), dtype=torch.float32, device=dev)
-        rid = torch.empty(chunk, dtype=torch.int64, device=dev)
         asg = torch.empty(n, dtype=torch.int32, device=dev)
         g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, max_gpu_memory=0))
         vdb.gen_normal_device(data.data_ptr(), 100_000 * dim, seed=12345, offset=0, stream=s)
@@ -114,64 +113,106 @@ def test_cfg4_all_8_shards_and_final_merge_100m_x_768_nlist16384_nprobe64():
         q = torch.empty((nq, dim), dtype=torch.float32, device=dev)
         vdb.gen_normal_device(q.data_ptr(), nq * dim, seed=12346, stream=s)
         torch.cuda.synchronize()
-        Q = q.cpu().numpy()
-        rb = vdb.rank_record_bytes(nq, k)
-        ids_off = vdb.rank_record_ids_offset(nq, k)
-        records = torch.empty(world * rb, dtype=torch.uint8, device=dev)
-        plan = vdb.shard_plan(sizes, world)
+    o = oracle.OracleIndex(dim, nlist, 0)
+    o.centroids = cent
+    Q = q.cpu().numpy()
+    _cfg4.update(dev=dev, stream=st, data=data, asg=asg, sizes=sizes, cent=cent, q=q, Q=Q,
+                 plan=vdb.shard_plan(sizes, c["world"]),
+                 probed={int(l) for qv in Q for l in o.select_nprobe(qv, c["nprobe"])},
+                 records=torch.empty(c["world"] * vdb.rank_record_bytes(nq, c["k"]), dtype=torch.uint8, device=dev),
+                 oD=np.empty((c["world"], nq, c["k"]), dtype=np.float32),
+                 oI=np.empty((c["world"], nq, c["k"]), dtype=np.uint64), done=set(), scanned={})
+    return _cfg4
+
+
+def _cfg4_rank(r):
+    """Rank r of the LPT plan built on this GPU (plan_shard + append of its rows), its packed
+    rank record for the queries against oracle_search_shard over only its probed lists."""
+    import torch
+    c, e = CFG4, _cfg4_setup()
+    if r in e["done"]:
+        return
+    n, dim, nlist, nprobe, k, world, chunk, nq = (c[x] for x in ("n", "dim", "nlist", "nprobe", "k", "world",
+                                                                  "chunk", "nq"))
+    dev, data, asg, sizes, cent = e["dev"], e["data"], e["asg"], e["sizes"], e["cent"]
+    rb, ids_off = vdb.rank_record_bytes(nq, k), vdb.rank_record_ids_offset(nq, k)
+    with torch.cuda.stream(e["stream"]):
+        s = e["stream"].cuda_stream
+        rid = torch.empty(chunk, dtype=torch.int64, device=dev)
+        g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, max_gpu_memory=0))
+        g.centroids = cent
+        g.plan_shard(r, world, sizes)
+        for a in range(0, n, chunk):  # pass 2: rank r appends its LPT lists only
+            vdb.gen_normal_device(data.data_ptr(), chunk * dim, seed=12345, offset=a * dim, stream=s)
+            torch.arange(a, a + chunk, dtype=torch.int64, device=dev, out=rid)
+            torch.cuda.synchronize()
+            g.add_to_lists_device(data.data_ptr(), rid.data_ptr(), asg[a:].data_ptr(), chunk)
+        assert np.array_equal(g.list_sizes(), sizes)
+        owned = e["plan"] == r
+        assert np.array_equal(g.list_owners() == r, owned)
+        rec = e["records"][r * rb:]
+        g.search_device(e["q"].data_ptr(), nq, nprobe, k, rec.data_ptr(), rec.data_ptr() + ids_off, s)
+        torch.cuda.synchronize()
+        Dg = rec[:nq * k * 4].cpu().numpy().view(np.float32).reshape(nq, k)
+        Ig = rec[ids_off:ids_off + nq * k * 8].cpu().numpy().view(np.uint64).reshape(nq, k)
         o = oracle.OracleIndex(dim, nlist, 0)
         o.centroids = cent
-        probed = {int(l) for qv in Q for l in o.select_nprobe(qv, nprobe)}
+        loaded = 0
+        for l in range(nlist):
+            if l in e["probed"] and owned[l] and sizes[l]:
+                v, i = o.list_buffers(l, int(sizes[l]))
+                g.get_list_into(l, v, i)
+                loaded += int(sizes[l])
+            else:
+                o.set_list_count(l, int(sizes[l]))
+        Dr, Ir = o.search_shard(e["Q"], nprobe, k, owned.astype(np.uint8), threads=THREADS)
         del o
-        oD = np.empty((world, nq, k), dtype=np.float32)
-        oI = np.empty((world, nq, k), dtype=np.uint64)
-        scanned = []
-        for r in range(world):
-            g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, max_gpu_memory=0))
-            g.centroids = cent
-            g.plan_shard(r, world, sizes)
-            for a in range(0, n, chunk):  # pass 2: rank r appends its LPT lists only
-                vdb.gen_normal_device(data.data_ptr(), chunk * dim, seed=12345, offset=a * dim, stream=s)
-                torch.arange(a, a + chunk, dtype=torch.int64, device=dev, out=rid)
-                torch.cuda.synchronize()
-                g.add_to_lists_device(data.data_ptr(), rid.data_ptr(), asg[a:].data_ptr(), chunk)
-            assert np.array_equal(g.list_sizes(), sizes)
-            owned = plan == r
-            assert np.array_equal(g.list_owners() == r, owned)
-            rec = records[r * rb:]
-            g.search_device(q.data_ptr(), nq, nprobe, k, rec.data_ptr(), rec.data_ptr() + ids_off, s)
-            torch.cuda.synchronize()
-            Dg = rec[:nq * k * 4].cpu().numpy().view(np.float32).reshape(nq, k)
-            Ig = rec[ids_off:ids_off + nq * k * 8].cpu().numpy().view(np.uint64).reshape(nq, k)
-            o = oracle.OracleIndex(dim, nlist, 0)
-            o.centroids = cent
-            loaded = 0
-            for l in range(nlist):
-                if l in probed and owned[l] and sizes[l]:
-                    v, i = o.list_buffers(l, int(sizes[l]))
-                    g.get_list_into(l, v, i)
-                    loaded += int(sizes[l])
-                else:
-                    o.set_list_count(l, int(sizes[l]))
-            Dr, Ir = o.search_shard(Q, nprobe, k, owned.astype(np.uint8), threads=THREADS)
-            del o
-            g.close()
-            torch.cuda.empty_cache()
-            assert np.array_equal(Ig, Ir), f"rank {r}: ids differ"
-            assert np.array_equal(bits(Dg), bits(Dr)), f"rank {r}: distance bits differ"
-            oD[r], oI[r] = Dr, Ir
-            scanned.append(loaded)
-        del data, rid, asg
+        g.close()
         torch.cuda.empty_cache()
-        od = torch.empty((nq, k), dtype=torch.float32, device=dev)
-        oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
-        vdb.merge_ranks_packed_device(records.data_ptr(), world, nq, k, od.data_ptr(), oi.data_ptr(), s)
+    assert np.array_equal(Ig, Ir), f"rank {r}: ids differ"
+    assert np.array_equal(bits(Dg), bits(Dr)), f"rank {r}: distance bits differ"
+    e["oD"][r], e["oI"][r] = Dr, Ir
+    e["scanned"][r] = loaded
+    e["done"].add(r)
+
+
+@pytest.mark.timeout(900)
+def test_cfg4_shards_0_to_3_100m_x_768_nlist16384_nprobe64():
+    """configs[3] ("100M x 768, nlist 16384, nprobe 64, lists sharded across 8 GPUs with the
+    top-k merge"), first half: one exact assignment pass over the 100M rows, then ranks 0-3
+    of the LPT plan built one at a time on this GPU, each one's partial results against
+    oracle_search_shard over only that shard's probed lists (host memory freed before the
+    next shard)."""
+    for r in range(4):
+        _cfg4_rank(r)
+
+
+@pytest.mark.timeout(900)
+def test_cfg4_shards_4_to_7_and_final_merge_100m_x_768_nlist16384_nprobe64():
+    """configs[3], second half: ranks 4-7 (and any the first test did not run), then the 8
+    GPU records merged on the device (vdb_merge_ranks_packed_device, the merge every rank
+    runs after the all-gather) against the oracle's merge of its 8 partials: the final
+    cfg4 answer."""
+    import torch
+    c = CFG4
+    for r in range(c["world"]):
+        _cfg4_rank(r)
+    e = _cfg4
+    nq, k, world = c["nq"], c["k"], c["world"]
+    with torch.cuda.stream(e["stream"]):
+        od = torch.empty((nq, k), dtype=torch.float32, device=e["dev"])
+        oi = torch.empty((nq, k), dtype=torch.int64, device=e["dev"])
+        vdb.merge_ranks_packed_device(e["records"].data_ptr(), world, nq, k, od.data_ptr(), oi.data_ptr(),
+                                      e["stream"].cuda_stream)
         torch.cuda.synchronize()
         D, I = od.cpu().numpy(), oi.cpu().numpy().view(np.uint64)
-    Df, If = oracle.merge_ranks(oD, oI, k)
+    Df, If = oracle.merge_ranks(e["oD"], e["oI"], k)
+    sizes, scanned = e["sizes"], e["scanned"]
+    _cfg4.clear()  # (releases the 100M-row assignment and the records)
+    torch.cuda.empty_cache()
     assert np.array_equal(I, If), "final (merged) ids differ"
     assert np.array_equal(bits(D), bits(Df)), "final (merged) distance bits differ"
-    assert int(sizes.sum()) == n
-    assert sum(1 for x in scanned if x) >= 2, "the probed lists should span several shards"
+    assert int(sizes.sum()) == c["n"]
+    assert sum(1 for x in scanned.values() if x) >= 2, "the probed lists should span several shards"
     # gpu_vs_cpu_test.cpp:209-219 validity rules on the final answer
-    assert np.all(np.isfinite(D)) and np.all(D >= 0) and np.all(I < n)
+    assert np.all(np.isfinite(D)) and np.all(D >= 0) and np.all(I < c["n"])

@@ -29,6 +29,7 @@ def build_id():
     spec = importlib.util.spec_from_file_location("vdb_amd", os.path.join(pkg, "__init__.py"),
                                                   submodule_search_locations=[pkg])
     mod = importlib.util.module_from_spec(spec)
+    sys.modules["vdb_amd"] = mod  # (dataclasses resolve their module by name)
     spec.loader.exec_module(mod)
     return mod.build_id()
 
