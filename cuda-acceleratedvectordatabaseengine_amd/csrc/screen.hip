@@ -256,7 +256,8 @@ __device__ __forceinline__ bf16x8 as_bf16x8(const uint4 v) {
 template <int M, int KD>
 __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
                                                const uint32_t seg, float* tk_d, uint64_t* tk_i, float* kdl,
-                                               uint32_t* s_thr, uint32_t* ring, const bool fresh) {
+                                               uint32_t* s_thr, uint32_t* ring, const bool fresh,
+                                               uint32_t* locks) {
     const int lane = lane_id();
     const uint32_t dp = a.dp, ks = dp >> 5, d4 = a.d4;
     const uint32_t count = a.count[it.list];
@@ -336,6 +337,11 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
         while (present) {
             const int gs = __builtin_ctz(present);
             present &= present - 1;
+            if (locks) {  // lists shared by the item's waves: one insertion at a time per query
+                if (lane == 0)
+                    while (atomicCAS(&locks[gs], 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
             const float kdg = fminf(kdl[gs], ord_dec(s_thr[gs]));
             float* sd = tk_d + gs * k;
             uint64_t* si = tk_i + gs * k;
@@ -356,7 +362,12 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
                 uint32_t* gt = a.thr + it.pair_start + q0 + gs;
                 if (nkd < ord_dec(*gt)) atomicMin(gt, ord_enc(nkd));
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            if (locks) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) atomicExch(&locks[gs], 0u);
+            } else {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            }
         }
     };
 
@@ -490,6 +501,9 @@ __device__ __forceinline__ void screen_partials(const ScanArgs& a, const ScanIte
 
 // Per-wave dynamic LDS: tk_i [16 k] u64 | tk_d [16 k] f32 | kdl [16] f32 | s_thr [16] u32 | ring [kRing] u32.
 __host__ __device__ constexpr size_t screen_wave_lds(uint32_t k) { return (size_t)16 * k * 12 + 64 + 64 + kRing * 4; }
+// Per-workgroup dynamic LDS ahead of the waves' areas: the wide item's shared lists
+// tk_i [16 k] u64 | tk_d [16 k] f32 | kdl [16] f32 | locks [16] u32.
+__host__ __device__ constexpr size_t screen_item_lds(uint32_t k) { return (size_t)16 * k * 12 + 64 + 64; }
 
 // ivf_scan_screen: persistent grid (two 4-wave workgroups per CU) over the plan's queues,
 // like ivf_scan_wide: wide items (a list's segments x <= 16 queries; the 4 waves take the
@@ -499,7 +513,13 @@ template <int M, int KD>
 __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint64_t slds[];
     const uint32_t wv = wave_index();
-    char* base = (char*)slds + (size_t)wv * screen_wave_lds(a.k);
+    // the wide item's lists, shared by its 4 waves (each query's top-k over every segment the
+    // item's waves scan: its k-th tightens 4x faster than one wave's)
+    uint64_t* it_i = slds;
+    float* it_d = (float*)(slds + 16 * a.k);
+    float* it_kd = it_d + 16 * a.k;
+    uint32_t* it_lock = (uint32_t*)(it_kd + 16);
+    char* base = (char*)slds + screen_item_lds(a.k) + (size_t)wv * screen_wave_lds(a.k);
     uint64_t* tk_i = (uint64_t*)base;
     float* tk_d = (float*)(base + (size_t)16 * a.k * 8);
     float* kdl = tk_d + 16 * a.k;
@@ -523,7 +543,7 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
             it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
             if (lane < (int)it.npairs) s_thr_w[lane] = a.thr[it.pair_start + lane];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            screen_segment<M, KD>(a, it, 0, (int)it.npairs, it.seg, tk_d, tk_i, kdl, s_thr_w, ring, true);
+            screen_segment<M, KD>(a, it, 0, (int)it.npairs, it.seg, tk_d, tk_i, kdl, s_thr_w, ring, true, nullptr);
             screen_partials(a, it, 0, (int)it.npairs, it.seg, tk_d, tk_i, true);
         }
     };
@@ -546,30 +566,38 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
         const int nq = (int)it.npairs;
         if (threadIdx.x == 0) s_seg = 0;
         if (threadIdx.x < (uint32_t)nq) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
+        for (uint32_t e = threadIdx.x; e < 16 * a.k; e += blockDim.x) {
+            it_d[e] = __builtin_inff();
+            it_i[e] = kNoId;
+        }
+        if (threadIdx.x < 16) {
+            it_kd[threadIdx.x] = __builtin_inff();
+            it_lock[threadIdx.x] = 0u;
+        }
         __syncthreads();
         const uint32_t seg_vectors = a.seg_blocks * 64;
         const uint32_t nseg = (a.count[it.list] + seg_vectors - 1) / seg_vectors;
         const uint32_t seg0 = it.seg * a.segs_item, seg1 = min(nseg, seg0 + a.segs_item);
-        // A wave keeps its top-k lists across the segments it takes from the item; each
-        // segment it moves on from gets empty partials, its last one the lists.
-        uint32_t prev = ~0u;
+        // The item's waves insert into its shared lists; every segment gets empty partials,
+        // then the item's first segment the lists (every scanned vector is in exactly one
+        // partial, so the merge's multiset top-min(k, n_l) of the union is unchanged).
         for (;;) {
             uint32_t sg = 0;
             if (lane == 0) sg = atomicAdd(&s_seg, 1u);
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
-            if (prev != ~0u) screen_partials(a, it, 0, nq, prev, tk_d, tk_i, false);
-            screen_segment<M, KD>(a, it, 0, nq, sg, tk_d, tk_i, kdl, s_thr, ring, prev == ~0u);
-            prev = sg;
+            screen_segment<M, KD>(a, it, 0, nq, sg, it_d, it_i, it_kd, s_thr, ring, false, it_lock);
+            screen_partials(a, it, 0, nq, sg, it_d, it_i, false);
         }
-        if (prev != ~0u) screen_partials(a, it, 0, nq, prev, tk_d, tk_i, true);
-        __syncthreads();  // s_thr / s_seg are reset by the next item
+        __syncthreads();
+        if (wv == 0) screen_partials(a, it, 0, nq, seg0, it_d, it_i, true);
+        // (the next item's first barrier orders this before the lists are reset)
     }
     if (a.fused) drain_narrow();
 }
 
 bool scan_screen_fits(uint32_t k, uint32_t dp) {
-    return k >= 1 && k <= 64 && dp % 64 == 0 && 4 * screen_wave_lds(k) + 128 <= kLdsBytes / 2;
+    return k >= 1 && k <= 64 && dp % 64 == 0 && screen_item_lds(k) + 4 * screen_wave_lds(k) + 128 <= kLdsBytes / 2;
 }
 
 size_t screen_shadow_u4(uint64_t blocks, uint32_t d4) { return (size_t)(blocks + 2) * d4 * 32; }
@@ -592,8 +620,17 @@ void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, con
 
 void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
     if (!grid_blocks) return;
+    static const bool raised = [] {  // up to half a CU's LDS per workgroup (k = 64: 70 KB)
+        const void* f[] = {(const void*)ivf_scan_screen<kL2, 4>, (const void*)ivf_scan_screen<kL2, 2>,
+                           (const void*)ivf_scan_screen<kIP, 4>, (const void*)ivf_scan_screen<kIP, 2>};
+        for (const void* fn : f)
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes / 2 - 128));
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)raised;
     const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
-    const size_t lds = 4 * screen_wave_lds(a.k);
+    const size_t lds = screen_item_lds(a.k) + 4 * screen_wave_lds(a.k);
     const bool kd4 = (a.dp / 32) % 4 == 0;
     if (metric == kL2) {
         if (kd4) ivf_scan_screen<kL2, 4><<<g, 256, lds, s>>>(a);

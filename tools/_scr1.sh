@@ -1,7 +1,9 @@
 set -o pipefail
-O=gpurun_out/r03s2b; mkdir -p $O
+O=gpurun_out/scr10; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 1000 python -u -m pytest tests -m gpu -v -s --durations=15 --timeout 600 --timeout-method thread > $O/pytest.log 2>&1
-rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 60 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
-tail -1 $O/smoke.log
+timeout -k 10 600 python -u -m pytest tests/test_gpu_screen.py tests/test_gpu_parity.py -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+for w in cfg3 mix cfg4; do
+timeout -k 10 700 python -u tools/knob_sweep.py $w "" "segs_per_item=4" "segs_per_item=16" > $O/$w.log 2>&1 || exit $?
+grep '^{' $O/$w.log
+done
