@@ -665,6 +665,9 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->quiesce();
             h->screen_opt = value != 0;
             h->screen_update();
+        } else if (n == "screen_group") {
+            require(value == 16 || value == 32, "screen_group is 16 or 32");
+            h->screen_group = (uint32_t)value;
         } else if (n == "fused_scan") {
             h->fused_scan = value != 0;
         } else if (n == "fused_merge") {

@@ -304,6 +304,7 @@ struct vdb_ivf {
     bool screen_ready = false;
     bool screen_stale = false;  // lists or centroids changed since the last build
     uint32_t screen_segs_auto = 4;  // segments per screened wide item (upload_directory; option segs_per_item)
+    uint32_t screen_group = 16;     // queries per screened wide item at most: 16 or 32 (option screen_group; 32 measured slower at cfg4: 5.80 vs 5.27 ms)
     DevBuf<uint4> screen_sh;
     DevBuf<float> screen_rows;
     DevBuf<float4> screen_meta;
@@ -1651,11 +1652,13 @@ struct vdb_ivf {
         // the screened scan (default): its items are the exact scan's 16-query wide items
         // and narrow items
         if (screen_stale) screen_update();
-        const bool screened = screen_ready && !tiered() && regs_k == 1 && metric != 2 && vdbk::scan_screen_fits(k, dp);
+        // 32-query items (option screen_group) where their shared lists fit the LDS
+        const uint32_t swq = screen_group == 32 && vdbk::scan_screen_fits(k, dp, 32) ? 32u : 16u;
+        const bool screened = screen_ready && !tiered() && regs_k == 1 && metric != 2 && vdbk::scan_screen_fits(k, dp, swq);
         const uint32_t mfma_min = !screened && wide && waves == 4 && metric != 2 && !(VDB_SCAN_DIAG & 2) &&
                                           vdbk::scan_bounded_fits(d4, k)
                                       ? scan_mfma_min : 0u;
-        const int plan_wide = screened ? vdbk::kWideGroup : (wide ? (int)wide_group : 0);
+        const int plan_wide = screened ? (int)swq : (wide ? (int)wide_group : 0);
         // (screened items: segs_per_item segments, default 4; a wave's top-k carries across
         // the segments it takes from one item)
         const uint32_t segs_screen = segs_item_opt ? segs_item_opt : screen_segs_auto;
@@ -1685,6 +1688,7 @@ struct vdb_ivf {
             sa.dp = dp;
             sa.P = P;
             sa.segs_item = segs_screen;
+            sa.wide_q = swq;
             sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks, vdbk::kPersistentBlocks / 2));
             const uint64_t want = std::max<uint64_t>(max_wide, (max_items + 3) / 4);
             vdbk::launch_scan_screen(metric, (uint32_t)(scan_blocks ? std::min<uint64_t>(want, scan_blocks) : want), sa, s);

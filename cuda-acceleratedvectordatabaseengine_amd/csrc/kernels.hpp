@@ -129,6 +129,7 @@ struct ScanArgs {
     const float4* __restrict__ pst = nullptr;
     uint32_t dp = 0;
     uint32_t P = 0;
+    uint32_t wide_q = 16;  // queries per screened wide item at most (16 or 32)
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);
@@ -141,7 +142,7 @@ size_t scan_bounded_lds(uint32_t d4, uint32_t k);
 bool scan_bounded_fits(uint32_t d4, uint32_t k);
 void launch_scan_bounded(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
 // ---- screened scan (screen.hip): L2 / IP, k <= 64, lists in HBM ----
-bool scan_screen_fits(uint32_t k, uint32_t dp);
+bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq);
 size_t screen_shadow_u4(uint64_t blocks, uint32_t d4);  // shadow size (uint4) incl. the prefetch slack
 void launch_screen_build(const float4* arena, uint64_t blocks, uint32_t d4, const uint32_t* block_list,
                          const float* cent_rm, uint4* shadow, float* rows, float4* meta, hipStream_t s);

@@ -501,32 +501,36 @@ __device__ __forceinline__ void screen_partials(const ScanArgs& a, const ScanIte
 
 // Per-wave dynamic LDS: tk_i [16 k] u64 | tk_d [16 k] f32 | kdl [16] f32 | s_thr [16] u32 | ring [kRing] u32.
 __host__ __device__ constexpr size_t screen_wave_lds(uint32_t k) { return (size_t)16 * k * 12 + 64 + 64 + kRing * 4; }
-// Per-workgroup dynamic LDS ahead of the waves' areas: the wide item's shared lists
-// tk_i [16 k] u64 | tk_d [16 k] f32 | kdl [16] f32 | locks [16] u32.
-__host__ __device__ constexpr size_t screen_item_lds(uint32_t k) { return (size_t)16 * k * 12 + 64 + 64; }
+// Per-workgroup dynamic LDS ahead of the waves' areas: the wide item's shared lists for up to
+// wq (16 or 32) queries: tk_i [wq k] u64 | tk_d [wq k] f32 | kdl [wq] f32 | locks [wq] u32.
+__host__ __device__ constexpr size_t screen_item_lds(uint32_t k, uint32_t wq) { return (size_t)wq * (k * 12 + 8); }
 
 // ivf_scan_screen: persistent grid (two 4-wave workgroups per CU) over the plan's queues,
-// like ivf_scan_wide: wide items (a list's segments x <= 16 queries; the 4 waves take the
-// segments dynamically and share the item's thresholds), then narrow items (one wave each:
-// one segment x <= 4 queries). The last a.fused workgroups start on the narrow queue.
+// like ivf_scan_wide: wide items (a list's segments x <= a.wide_q queries; the 4 waves take
+// the segments dynamically and share the item's lists and thresholds), then narrow items
+// (one wave each: one segment x <= 4 queries). The last a.fused workgroups start on the
+// narrow queue. An item of 17-32 queries splits its waves in two halves of 16 queries that
+// take the item's segments in the same order, side by side on the CU: the list's shadow is
+// read from HBM once for both halves (the second read is served by the L2).
 template <int M, int KD>
 __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint64_t slds[];
     const uint32_t wv = wave_index();
     // the wide item's lists, shared by its 4 waves (each query's top-k over every segment the
     // item's waves scan: its k-th tightens 4x faster than one wave's)
+    const uint32_t wq = a.wide_q;
     uint64_t* it_i = slds;
-    float* it_d = (float*)(slds + 16 * a.k);
-    float* it_kd = it_d + 16 * a.k;
-    uint32_t* it_lock = (uint32_t*)(it_kd + 16);
-    char* base = (char*)slds + screen_item_lds(a.k) + (size_t)wv * screen_wave_lds(a.k);
+    float* it_d = (float*)(slds + wq * a.k);
+    float* it_kd = it_d + wq * a.k;
+    uint32_t* it_lock = (uint32_t*)(it_kd + wq);
+    char* base = (char*)slds + screen_item_lds(a.k, wq) + (size_t)wv * screen_wave_lds(a.k);
     uint64_t* tk_i = (uint64_t*)base;
     float* tk_d = (float*)(base + (size_t)16 * a.k * 8);
     float* kdl = tk_d + 16 * a.k;
     uint32_t* s_thr_w = (uint32_t*)(kdl + 16);
     uint32_t* ring = s_thr_w + 16;
-    __shared__ uint32_t s_next, s_seg;
-    __shared__ uint32_t s_thr[16];
+    __shared__ uint32_t s_next, s_seg[2];
+    __shared__ uint32_t s_thr[32];
     const int lane = lane_id();
 
     auto drain_narrow = [&]() {
@@ -564,13 +568,13 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
         it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
         it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
         const int nq = (int)it.npairs;
-        if (threadIdx.x == 0) s_seg = 0;
+        if (threadIdx.x < 2) s_seg[threadIdx.x] = 0;
         if (threadIdx.x < (uint32_t)nq) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
-        for (uint32_t e = threadIdx.x; e < 16 * a.k; e += blockDim.x) {
+        for (uint32_t e = threadIdx.x; e < (uint32_t)nq * a.k; e += blockDim.x) {
             it_d[e] = __builtin_inff();
             it_i[e] = kNoId;
         }
-        if (threadIdx.x < 16) {
+        if (threadIdx.x < (uint32_t)nq) {
             it_kd[threadIdx.x] = __builtin_inff();
             it_lock[threadIdx.x] = 0u;
         }
@@ -581,23 +585,30 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
         // The item's waves insert into its shared lists; every segment gets empty partials,
         // then the item's first segment the lists (every scanned vector is in exactly one
         // partial, so the merge's multiset top-min(k, n_l) of the union is unchanged).
+        const bool split = nq > 16;
+        const uint32_t half = split ? wv >> 1 : 0u;
+        const int nq0 = split ? (nq + 1) / 2 : nq;  // (balanced halves)
+        const int q0 = half ? nq0 : 0, nqh = half ? nq - nq0 : nq0;
+        const int ko = q0 * (int)a.k;
         for (;;) {
             uint32_t sg = 0;
-            if (lane == 0) sg = atomicAdd(&s_seg, 1u);
+            if (lane == 0) sg = atomicAdd(&s_seg[half], 1u);
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
-            screen_segment<M, KD>(a, it, 0, nq, sg, it_d, it_i, it_kd, s_thr, ring, false, it_lock);
-            screen_partials(a, it, 0, nq, sg, it_d, it_i, false);
+            screen_segment<M, KD>(a, it, q0, nqh, sg, it_d + ko, it_i + ko, it_kd + q0, s_thr + q0, ring, false,
+                                  it_lock + q0);
+            screen_partials(a, it, q0, nqh, sg, it_d + ko, it_i + ko, false);
         }
         __syncthreads();
-        if (wv == 0) screen_partials(a, it, 0, nq, seg0, it_d, it_i, true);
+        if ((wv & 1) == 0 && (wv == 0 || split)) screen_partials(a, it, q0, nqh, seg0, it_d + ko, it_i + ko, true);
         // (the next item's first barrier orders this before the lists are reset)
     }
     if (a.fused) drain_narrow();
 }
 
-bool scan_screen_fits(uint32_t k, uint32_t dp) {
-    return k >= 1 && k <= 64 && dp % 64 == 0 && screen_item_lds(k) + 4 * screen_wave_lds(k) + 128 <= kLdsBytes / 2;
+bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq) {
+    return k >= 1 && k <= 64 && dp % 64 == 0 && (wq == 16 || wq == 32) &&
+           screen_item_lds(k, wq) + 4 * screen_wave_lds(k) + 256 <= kLdsBytes / 2;
 }
 
 size_t screen_shadow_u4(uint64_t blocks, uint32_t d4) { return (size_t)(blocks + 2) * d4 * 32; }
@@ -624,13 +635,13 @@ void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hip
         const void* f[] = {(const void*)ivf_scan_screen<kL2, 4>, (const void*)ivf_scan_screen<kL2, 2>,
                            (const void*)ivf_scan_screen<kIP, 4>, (const void*)ivf_scan_screen<kIP, 2>};
         for (const void* fn : f)
-            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes / 2 - 128));
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes / 2 - 256));
         (void)hipGetLastError();
         return true;
     }();
     (void)raised;
     const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
-    const size_t lds = screen_item_lds(a.k) + 4 * screen_wave_lds(a.k);
+    const size_t lds = screen_item_lds(a.k, a.wide_q) + 4 * screen_wave_lds(a.k);
     const bool kd4 = (a.dp / 32) % 4 == 0;
     if (metric == kL2) {
         if (kd4) ivf_scan_screen<kL2, 4><<<g, 256, lds, s>>>(a);

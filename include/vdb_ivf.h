@@ -292,7 +292,9 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * items; 0: narrow items on a second stream), "screen" (1, default: the screened scan — bf16
  * matrix-core distance bounds from a shadow of the lists, exact fp32 sums only for pairs that can
  * reach a list's top-k; L2/IP, k <= 64, lists in HBM; costs 1.5x the list bytes of extra HBM;
- * 0: the exact VALU scan of every pair), "list_cache_bytes" (0 = every list HBM-resident; > 0 = the list-cache tier above with an
+ * 0: the exact VALU scan of every pair), "screen_group" (16, default, or 32: queries per screened wide
+ * item; 32 splits an item's waves in two halves that stream each segment side by side),
+ * "list_cache_bytes" (0 = every list HBM-resident; > 0 = the list-cache tier above with an
  * HBM cache of that many bytes; a search whose single query probes more fails with
  * VDB_ERR_OUT_OF_MEMORY, a batch probing more is split; setting it replaces the
  * max_gpu_memory cap), "max_gpu_memory" (the Config cap, applied at once), "bounded_stats"

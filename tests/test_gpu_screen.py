@@ -40,6 +40,10 @@ def test_screen_hub_lists(metric, k):
         for seg in (0, 64, 1024):
             g.set_option("seg_vectors", seg)
             assert_same(*search_all(g, Q, nprobe, k, batch), Dr, Ir)
+    # items of up to 32 queries (an item's waves split in two halves; 16 is the default)
+    g.set_option("screen_group", 32)
+    assert_same(*search_all(g, Q, nprobe, k, 130), Dr, Ir)
+    g.set_option("screen_group", 16)
     g.set_option("screen", 0)
     assert_same(*search_all(g, Q, nprobe, k, 130), Dr, Ir)
 
