@@ -385,6 +385,7 @@ struct vdb_ivf {
         DevBuf<vdbk::ScanItem> items{true}, items_w{true};
         DevBuf<uint16_t> qres{true};  // screened scan: per (query, probe) bf16 A rows [B * P][dp]
         DevBuf<float4> pst{true};     // ... and their norms
+        DevBuf<uint32_t> thr4{true};  // ... and, per sorted pair, 4 quarter-list thresholds
         DevBuf<uint8_t> xrec{true}, xgat{true};  // multi-GPU: this rank's packed partials, the gathered records
         DevBuf<float> gq{true};            // group member: the call's queries on this device
         DevBuf<uint32_t> greq{true};       // group member: the call's request starts on this device
@@ -1683,7 +1684,8 @@ struct vdb_ivf {
         if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
         if (screened) {
             vdbk::launch_screen_pairs(metric, w.q, B, P, w.probes.p, cent_rm.p, dp, slot_buf(w, w.qres, (size_t)BP * dp),
-                                      slot_buf(w, w.pst, BP), s);
+                                      slot_buf(w, w.pst, BP), slot_buf(w, w.thr4, (size_t)BP * 4), s);
+            sa.thr4 = w.thr4.p;
             sa.shadow = screen_sh.p;
             sa.rows = screen_rows.p;
             sa.meta = screen_meta.p;

@@ -130,6 +130,7 @@ struct ScanArgs {
     uint32_t dp = 0;
     uint32_t P = 0;
     uint32_t wide_q = 16;  // queries per screened wide item at most (16 or 32)
+    uint32_t* thr4 = nullptr;  // per sorted pair, 4 quarter-list thresholds (screen.hip)
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);
@@ -147,7 +148,7 @@ size_t screen_shadow_u4(uint64_t blocks, uint32_t d4);  // shadow size (uint4) i
 void launch_screen_build(const float4* arena, uint64_t blocks, uint32_t d4, const uint32_t* block_list,
                          const float* cent_rm, uint4* shadow, float* rows, float4* meta, hipStream_t s);
 void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, const uint32_t* probes,
-                         const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, hipStream_t s);
+                         const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, uint32_t* thr4, hipStream_t s);
 void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,

@@ -145,8 +145,10 @@ template <int M>
 __global__ __launch_bounds__(256) void ivf_screen_pairs(const float* __restrict__ q, uint32_t BP, uint32_t P,
                                                         const uint32_t* __restrict__ probes,
                                                         const float* __restrict__ cent_rm, uint32_t dp,
-                                                        uint16_t* __restrict__ qres, float4* __restrict__ pst) {
+                                                        uint16_t* __restrict__ qres, float4* __restrict__ pst,
+                                                        uint32_t* __restrict__ thr4) {
     const int lane = lane_id();
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < 4 * BP; e += gridDim.x * blockDim.x) thr4[e] = kThrInf;
     for (uint32_t i = blockIdx.x * 4 + wave_index(); i < BP; i += gridDim.x * 4) {
         const float* qr = q + (size_t)(i / P) * dp;
         const float* cr = cent_rm + (size_t)probes[i] * dp;
@@ -257,7 +259,7 @@ template <int M, int KD>
 __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
                                                const uint32_t seg, float* tk_d, uint64_t* tk_i, float* kdl,
                                                uint32_t* s_thr, uint32_t* ring, const bool fresh,
-                                               uint32_t* locks) {
+                                               uint32_t* locks, const uint32_t item_slot) {
     const int lane = lane_id();
     const uint32_t dp = a.dp, ks = dp >> 5, d4 = a.d4;
     const uint32_t count = a.count[it.list];
@@ -357,6 +359,12 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
                 si[lane] = tk.id[0];
             }
             if (lane == 0) kdl[gs] = nkd;
+            // the list's ceil(k/4)-th into this item's quarter slot (see thr4 below)
+            const float dj = rd_lane(tk.d[0], (k + 3) / 4 - 1);
+            if (lane == 0 && dj < __builtin_inff()) {
+                uint32_t* s4 = a.thr4 + (size_t)(it.pair_start + q0 + gs) * 4 + (item_slot & 3u);
+                if (dj < ord_dec(*s4)) atomicMin(s4, ord_enc(dj));
+            }
             if (nkd < kdg && lane == 0) {
                 atomicMin(&s_thr[gs], ord_enc(nkd));
                 uint32_t* gt = a.thr + it.pair_start + q0 + gs;
@@ -445,7 +453,15 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
         for (int r = 0; r < 4; ++r) {
             const int g = 4 * (lane >> 4) + r;
             const uint32_t* gt = a.thr + it.pair_start + q0 + min(g, nq - 1);
-            const float cur = fminf(ord_dec(*gt), ord_dec(s_thr[min(g, nq - 1)]));
+            // thr4: per (query, list) the smallest ceil(k/4)-th distance any item of residue
+            // s (item index mod 4) reached, for s = 0..3. Four distinct items hold ceil(k/4)
+            // vectors each at or below the largest of the four: a valid shared threshold,
+            // nearer the k-th of the union of the items' lists than the min of their k-ths
+            // (a.thr) when several items of one list run at once. (m = 2, 4, 8 slots together
+            // measured no better.)
+            const uint4 t4 = *(const uint4*)(a.thr4 + (size_t)(it.pair_start + q0 + min(g, nq - 1)) * 4);
+            const float th4 = fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w)));
+            const float cur = fminf(fminf(ord_dec(*gt), th4), ord_dec(s_thr[min(g, nq - 1)]));
             const float t = block_kth(ubv[r], k);
             if ((lane & 15) == 0 && g < nq && t < cur) {
                 atomicMin(&s_thr[g], ord_enc(t));
@@ -547,7 +563,8 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
             it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
             if (lane < (int)it.npairs) s_thr_w[lane] = a.thr[it.pair_start + lane];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            screen_segment<M, KD>(a, it, 0, (int)it.npairs, it.seg, tk_d, tk_i, kdl, s_thr_w, ring, true, nullptr);
+            screen_segment<M, KD>(a, it, 0, (int)it.npairs, it.seg, tk_d, tk_i, kdl, s_thr_w, ring, true, nullptr,
+                                  it.seg);
             screen_partials(a, it, 0, (int)it.npairs, it.seg, tk_d, tk_i, true);
         }
     };
@@ -596,7 +613,7 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
             screen_segment<M, KD>(a, it, q0, nqh, sg, it_d + ko, it_i + ko, it_kd + q0, s_thr + q0, ring, false,
-                                  it_lock + q0);
+                                  it_lock + q0, it.seg);
             screen_partials(a, it, q0, nqh, sg, it_d + ko, it_i + ko, false);
         }
         __syncthreads();
@@ -621,12 +638,12 @@ void launch_screen_build(const float4* arena, uint64_t blocks, uint32_t d4, cons
 }
 
 void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, const uint32_t* probes,
-                         const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, hipStream_t s) {
+                         const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, uint32_t* thr4, hipStream_t s) {
     const uint32_t BP = B * P;
     if (!BP) return;
     const uint32_t g = std::min<uint32_t>((BP + 3) / 4, 2048);
-    if (metric == kL2) ivf_screen_pairs<kL2><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst);
-    else ivf_screen_pairs<kIP><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst);
+    if (metric == kL2) ivf_screen_pairs<kL2><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst, thr4);
+    else ivf_screen_pairs<kIP><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst, thr4);
 }
 
 void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
