@@ -56,7 +56,11 @@ constexpr int kRing = 512;                          // candidate ring entries pe
 #ifndef VDB_SCREEN_EXACT_PIPE
 #define VDB_SCREEN_EXACT_PIPE 4
 #endif
-constexpr int kExactPipe = VDB_SCREEN_EXACT_PIPE;   // float4 of a row in flight per lane (exact re-check)
+constexpr int kExactPipe = VDB_SCREEN_EXACT_PIPE;   // float4 of a row in flight per lane (re-checks mid-stream)
+#ifndef VDB_SCREEN_EXACT_PIPE_END
+#define VDB_SCREEN_EXACT_PIPE_END 8
+#endif
+constexpr int kExactPipeEnd = VDB_SCREEN_EXACT_PIPE_END;  // ... for a segment's last partial round
 // Timing experiment (a separate build, never an option): 1 drops the candidates instead
 // of re-checking them (the screen stream alone; results INVALID).
 #ifndef VDB_SCREEN_DIAG
@@ -304,7 +308,8 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
     uint32_t head = 0, tail = 0;  // wave-uniform ring cursors
 
     // Exact re-check of up to 64 ring entries (one per lane), then the top-k offers.
-    auto exact_round = [&](uint32_t n) {
+    auto exact_round = [&](uint32_t n, auto pipe_c) {
+        constexpr int kPipe = decltype(pipe_c)::value;
         const bool act = lane < (int)n;
         const uint32_t ent = ring[(head + (act ? (uint32_t)lane : 0u)) & (kRing - 1)];
         head += n;
@@ -315,19 +320,19 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
         const float4* xr = (const float4*)(a.rows + slot * dp);
         const float4* qr = (const float4*)(a.qpad + (size_t)(pairs[g] >> 16) * dp);
         float acc = 0.0f;
-        float4 xb[kExactPipe], qb[kExactPipe];
+        float4 xb[kPipe], qb[kPipe];
 #pragma unroll
-        for (int i = 0; i < kExactPipe; ++i) {
+        for (int i = 0; i < kPipe; ++i) {
             xb[i] = xr[i];
             qb[i] = qr[i];
         }
-        for (uint32_t t0 = 0; t0 < d4; t0 += kExactPipe) {
+        for (uint32_t t0 = 0; t0 < d4; t0 += kPipe) {
 #pragma unroll
-            for (int i = 0; i < kExactPipe; ++i) {
+            for (int i = 0; i < kPipe; ++i) {
                 acc = acc4<M>(acc, qb[i], xb[i]);
-                if (t0 + kExactPipe < d4) {
-                    xb[i] = xr[t0 + kExactPipe + i];
-                    qb[i] = qr[t0 + kExactPipe + i];
+                if (t0 + kPipe < d4) {
+                    xb[i] = xr[t0 + kPipe + i];
+                    qb[i] = qr[t0 + kPipe + i];
                 }
             }
         }
@@ -488,12 +493,13 @@ __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem
                 tail += (uint32_t)__popcll(m);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            // full rounds as they fill; the segment's last tile drains the ring
-            const uint32_t need = (j + 1 == nb && vt == 3) ? 1u : 64u;
+            // full rounds as they fill (the list registers in flight leave room for a shallow
+            // load pipeline); the segment's remainder after the stream, with a deep one
             if (VDB_SCREEN_DIAG & 1) head = tail;
-            while (tail - head >= need) exact_round(min(64u, tail - head));
+            while (tail - head >= 64) exact_round(64u, std::integral_constant<int, kExactPipe>{});
         }
     }
+    while (tail != head) exact_round(min(64u, tail - head), std::integral_constant<int, kExactPipeEnd>{});
     if (a.mstats && lane == 0) atomicAdd(&a.mstats[1], (unsigned long long)nb);
 }
 
