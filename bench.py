@@ -106,7 +106,8 @@ def build_index(vdb, args, device, rank, world):
 def new_index(vdb, args, device):
     # max_gpu_memory=0: every list HBM-resident (the reference's 8 GiB default Config cap
     # would put a 31 GB index on the list-cache tier)
-    return vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(args.dim, args.nlist, vdb.Metric.L2, max_gpu_memory=0,
+    metric = vdb.Metric.InnerProduct if getattr(args, "metric", "l2") == "ip" else vdb.Metric.L2
+    return vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(args.dim, args.nlist, metric, max_gpu_memory=0,
                                                     device=device.index))
 
 

@@ -7,7 +7,8 @@ flight) and the wall time per batch. Options never change results (the result-ch
 timing experiments are separate builds: tools/build_variant.sh -DVDB_SCAN_DIAG=n, selected
 with VDB_IVF_LIB).
 usage: tools/knob_sweep.py cfg3|cfg4|mix "wide_group=32" "seg_vectors=1024,segs_per_item=8" ...
-  cfg4 = rank 0 of the 8-way sharded 100M x 768 index (the per-GPU work of 8 GPUs)
+  cfg4 = rank 0 of the 8-way sharded 100M x 768 index (the per-GPU work of 8 GPUs);
+  ip = the cfg3 index with the inner-product metric
 """
 import json
 import os
@@ -30,7 +31,7 @@ def main():
     args = bench.argparse.Namespace(dim=768, nvec=100_000_000 if big else 10_000_000, nlist=16384 if big else 4096,
                                     nprobe=64 if big else 32, batch=64, k=10, train=100_000, build_chunk=10_000_000,
                                     data="mixture" if wl == "mix" else "iid", mix_components=0, mix_group=0,
-                                    mix_spread=0.35, mix_sigma=0.1)
+                                    mix_spread=0.35, mix_sigma=0.1, metric="ip" if wl == "ip" else "l2")
     vdb = bench.load_vdb()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
