@@ -227,24 +227,6 @@ __device__ __forceinline__ float block_kth(float (&u)[4], int kk) {
     return __shfl(x, (lane_id() & ~15) + (e >> 2));
 }
 
-// Bitonic sort of x over each 16-lane row (DPP exchanges), then the row's c-th smallest
-// (1 <= c <= 16) in every lane of the row. Every lane of the wave must be active.
-__device__ __forceinline__ float row_sorted_at(float x, int c) {
-    const int l = lane_id() & 15;
-#define VDB_ROW_STEP(SIZE, STRIDE)                                           \
-    {                                                                        \
-        const float y = xor_f<STRIDE>(x);                                    \
-        const bool keep_min = ((l & SIZE) == 0) == ((l & STRIDE) == 0);      \
-        x = keep_min ? fminf(x, y) : fmaxf(x, y);                            \
-    }
-    VDB_ROW_STEP(2, 1)
-    VDB_ROW_STEP(4, 2) VDB_ROW_STEP(4, 1)
-    VDB_ROW_STEP(8, 4) VDB_ROW_STEP(8, 2) VDB_ROW_STEP(8, 1)
-    VDB_ROW_STEP(16, 8) VDB_ROW_STEP(16, 4) VDB_ROW_STEP(16, 2) VDB_ROW_STEP(16, 1)
-#undef VDB_ROW_STEP
-    return __shfl(x, (lane_id() & ~15) + c - 1);
-}
-
 __device__ __forceinline__ uint4 ld_nt_u4(const uint4* p) {
     const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
     return make_uint4(v.x, v.y, v.z, v.w);
@@ -254,11 +236,12 @@ __device__ __forceinline__ bf16x8 as_bf16x8(const uint4 v) {
 }
 
 // One wave: segment `seg` of list it.list against the nq (<= 16) queries of the item
-// starting at sorted pair it.pair_start + q0. tk_d / tk_i: this wave's per-query top-k
-// lists (16 x k, LDS), reset when `fresh` (else they carry the wave's earlier segments of
-// the same item, so its thresholds keep improving); kdl: its per-query k-th distances;
-// s_thr: the shared k-th of the item's queries (LDS, lowered with atomicMin); ring: the
-// candidate ring (kRing). The caller writes the partials (screen_partials).
+// starting at sorted pair it.pair_start + q0. tk_d / tk_i: the per-query top-k lists (nq x k,
+// LDS) this wave inserts into: its own, reset when `fresh` (narrow items), or the wide item's
+// lists shared by its 4 waves under `locks` (one insertion at a time per query); kdl: their
+// k-th distances; s_thr: the shared k-th of the item's queries (LDS, lowered with atomicMin);
+// ring: the candidate ring (kRing); item_slot: the item's index (quarter-list thresholds).
+// The caller writes the partials (screen_partials).
 template <int M, int KD>
 __device__ __forceinline__ void screen_segment(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
                                                const uint32_t seg, float* tk_d, uint64_t* tk_i, float* kdl,
