@@ -221,6 +221,48 @@ def cpu_model():
     return "unknown"
 
 
+def footprint(idx, args, world):
+    """Device memory the index holds after the warm-up (the screen is built lazily by the
+    first search): vdb_ivf_gpu_bytes_allocated (every list layout, centroids, workspaces)
+    against the fp32 list bytes (count x dim x 4) and the reference's definition
+    (get_gpu_memory_usage: count x (dim x 4 + 8) per resident list)."""
+    sizes = idx.list_sizes()
+    owned = idx.list_owners() if world > 1 or args.emulate_shard > 1 else None
+    mine = sizes if owned is None else sizes[owned != 0xFFFFFFFF]
+    fp32 = int(mine.sum()) * args.dim * 4
+    alloc = idx.gpu_bytes_allocated()
+    return {"gpu_bytes_allocated": alloc, "fp32_list_bytes": fp32,
+            "over_fp32_lists": round(alloc / fp32, 3) if fp32 else None,
+            "reference_gpu_memory_usage": idx.get_gpu_memory_usage()}
+
+
+def timed_batch_parity(idx, args, queries, out_d, out_i):
+    """The first TIMED batch's device results (one search call of B queries inside the timed
+    region) against the oracle's search of the same B queries as one call (all cores)."""
+    sys.path.insert(0, ROOT)
+    import oracle  # test infrastructure: the checker only
+
+    B, k = args.batch, args.k
+    q0 = args.warmup * B
+    qh = queries[q0:q0 + B].cpu().numpy()
+    o = oracle.OracleIndex(args.dim, args.nlist, 0)
+    o.centroids = idx.centroids
+    sizes = idx.list_sizes()
+    probed = set()
+    for q in qh:
+        probed.update(o.select_nprobe(q, args.nprobe).tolist())
+    for l in sorted(probed):
+        v, i = o.list_buffers(l, int(sizes[l]))
+        if len(i):
+            idx.get_list_into(l, v, i)
+    t0 = time.perf_counter()
+    D, I = o.search(qh, args.nprobe, k, threads=host_cpu_share())
+    Dg, Ig = out_d[q0:q0 + B].cpu().numpy(), out_i[q0:q0 + B].cpu().numpy().view(np.uint64)
+    same = bool(np.array_equal(I, Ig) and np.array_equal(D.view(np.uint32), Dg.view(np.uint32)))
+    return {"batch": f"timed step 0 (queries {q0}..{q0 + B - 1}), one call", "bit_identical": same,
+            "oracle_s": round(time.perf_counter() - t0, 1)}
+
+
 def cpu_baseline(vdb, idx, args, queries_host, budget_s):
     """Time the oracle (reference CPU path restatement) on bounded query samples, the two
     numbers BASELINE.md promises: (1) one core, as the reference's serial query loop
@@ -268,7 +310,8 @@ def cpu_baseline(vdb, idx, args, queries_host, budget_s):
         Dg, Ig = idx.search(qs, nprobe=args.nprobe, k=args.k)
         parity_mt = bool(np.array_equal(Im, Ig) and np.array_equal(Dm.view(np.uint32), Dg.view(np.uint32)))
         mt = {"value": round(n_mt / t_mt, 3), "unit": "queries/s", "cores": threads,
-              "sample": f"{n_mt} queries in one search() call, OpenMP over queries, {t_mt:.1f}s",
+              "sample": f"{n_mt} queries in one search() call, OpenMP over queries, {t_mt:.1f}s "
+                        f"(bounded sample: BASELINE.md's Q = 1000 would take {1000 * t_mt / n_mt:.0f}s)",
               "parity_with_gpu": parity_mt}
         parity &= parity_mt
     return {
@@ -862,14 +905,26 @@ def run(vdb, args, device, rank, world):
     # and 16 B of norms, and reads the fp32 row (4 dp B) of every re-checked pair: its
     # algorithmic bytes. The exact scan reads the fp32 lists once per batch.
     screened = prof.get("bounded_blocks", 0) > 0
+    deferred = screened and prof.get("collect_ms", 0) > 0
     dp = -(-args.dim // 64) * 64
-    if screened:
+    collect_ms = prof.get("collect_ms", 0.0) / launches
+    if deferred:
+        # the dominant kernel is the deferred screen's collect pass: it streams the shadow and
+        # the norms and writes 16 B per collected (query, vector) pair; the exact re-checks
+        # after it read 4 dp B per survivor (reported beside it)
+        vecs = prof["scan_vectors"] / batches
+        collected = prof.get("screen_collected", 0) / batches
+        bytes_per_launch = vecs * (2 * dp + 16) + collected * 16
+        kernel_ms = collect_ms
+    elif screened:
         vecs = prof["scan_vectors"] / batches
         rechecks = prof["exact_reranks"] / batches
         bytes_per_launch = vecs * (2 * dp + 16) + rechecks * 4 * dp
+        kernel_ms = scan_ms
     else:
         bytes_per_launch = fp32_bytes
-    achieved = bytes_per_launch / (scan_ms * 1e-3) / 1e9 if scan_ms > 0 else 0.0
+        kernel_ms = scan_ms
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     key = f"{args.nvec}x{args.dim}/{args.nlist}/{args.nprobe}/{B}/{k}/N{world}"
     if args.data != "iid":
         key += f"/{args.data}"
@@ -914,12 +969,18 @@ def run(vdb, args, device, rank, world):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "ivf_scan_screen" if screened else "ivf_scan_wide",
-            "bytes_model": ("screened: 2 dp B bf16 shadow + 16 B norms per vector of the distinct probed lists "
+            "kernel": "ivf_screen_collect" if deferred else ("ivf_scan_screen" if screened else "ivf_scan_wide"),
+            "bytes_model": ("deferred screen, collect kernel: 2 dp B bf16 shadow + 16 B norms per vector of the "
+                            "distinct probed lists + 16 B per collected (query, vector) candidate" if deferred else
+                            "screened: 2 dp B bf16 shadow + 16 B norms per vector of the distinct probed lists "
                             "+ 4 dp B per exactly re-checked (query, vector) pair" if screened else
                             "exact: 4 D B per vector of the distinct probed lists"),
+            "kernel_ms_per_launch": round(kernel_ms, 4),
             "fp32_list_bytes_per_batch": int(fp32_bytes),
             "fp32_equivalent_GBps": round(fp32_bytes / (scan_ms * 1e-3) / 1e9, 1) if scan_ms > 0 else None,
+            # SURVEY 8(d)'s model (4 D B per vector of the distinct probed lists) over the whole scan
+            # phase: above 1 where the kernel reads the half-size shadow instead of the fp32 lists
+            "frac_fp32_model": round(fp32_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4) if scan_ms > 0 else None,
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
@@ -935,7 +996,11 @@ def run(vdb, args, device, rank, world):
             **({"exact_reranks_per_batch": int(prof["exact_reranks"] / max(prof["batches"], 1)),
                 "bounded_blocks_per_batch": int(prof["bounded_blocks"] / max(prof["batches"], 1))}
                if prof.get("bounded_blocks") else {}),
+            **({"collected_per_batch": int(prof.get("screen_collected", 0) / batches),
+                "recheck_ms_per_batch": round(prof.get("recheck_ms", 0.0) / launches, 4),
+                "recheck_bytes_per_batch": int(prof["exact_reranks"] / batches * 4 * dp)} if deferred else {}),
         },
+        "footprint": footprint(idx, args, world),
         "build": build_info,
         **({"list_cache": idx.cache_stats()} if any(o.startswith("list_cache_bytes=") for o in args.opt) else {}),
         "engine_options": dict(o.split("=", 1) for o in args.opt),
@@ -954,6 +1019,7 @@ def run(vdb, args, device, rank, world):
     if world == 1 and rank == 0 and not args.no_cpu and args.emulate_shard <= 1:
         qh = queries[: args.cpu_queries].cpu().numpy()
         result["cpu_baseline"] = cpu_baseline(vdb, idx, args, qh, args.cpu_budget)
+        result["timed_batch_parity"] = timed_batch_parity(idx, args, queries, out_d, out_i)
     if world == 1 and args.emulate_shard > 1 and args.shard_check > 0:
         qh = queries[: args.shard_check].cpu().numpy()
         result["shard_parity"] = shard_parity(vdb, idx, args, qh, er, args.emulate_shard)

@@ -65,7 +65,9 @@ class Profile(ctypes.Structure):
                 ("scan_bytes", ctypes.c_uint64), ("pair_vectors", ctypes.c_uint64),
                 ("exact_reranks", ctypes.c_uint64), ("bounded_blocks", ctypes.c_uint64),
                 ("computed_vectors", ctypes.c_uint64), ("local_merge_ms", ctypes.c_double),
-                ("exchanges", ctypes.c_uint64), ("exchange_ms", ctypes.c_double), ("rank_merge_ms", ctypes.c_double)]
+                ("exchanges", ctypes.c_uint64), ("exchange_ms", ctypes.c_double), ("rank_merge_ms", ctypes.c_double),
+                ("screen_collected", ctypes.c_uint64), ("collect_ms", ctypes.c_double),
+                ("recheck_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

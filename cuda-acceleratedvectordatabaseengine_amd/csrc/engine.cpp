@@ -575,9 +575,7 @@ uint64_t vdb_ivf_gpu_bytes_allocated(const vdb_ivf* h) {
     if (!h) return 0;
     std::lock_guard<std::mutex> g(h->mu);
     if (h->is_group()) return group::gpu_bytes(h, true);
-    const uint64_t cent = (uint64_t)h->nlist * h->dp * 8;  // row-major + interleaved copies
-    if (h->tiered()) return (h->cache_blocks + 1) * vdb_ivf::block_bytes(h->dp) + cent;
-    return (h->arena_blocks + (h->arena_blocks ? 1 : 0)) * vdb_ivf::block_bytes(h->dp) + cent;
+    return h->device_footprint();
 }
 
 uint64_t vdb_ivf_ntotal(const vdb_ivf* h) { return h ? h->total : 0; }
@@ -665,6 +663,16 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->quiesce();
             h->screen_opt = value != 0;
             h->screen_update();
+        } else if (n == "screen_defer") {
+            h->set_device();
+            h->quiesce();
+            h->screen_defer = value != 0;
+            h->screen_update();
+        } else if (n == "screen_cand_cap") {
+            require(value >= 1024 && value <= (1ll << 30), "screen_cand_cap is 1024 .. 2^30");
+            h->set_device();
+            h->quiesce();
+            h->screen_cand_cap = (uint32_t)value;
         } else if (n == "screen_group") {
             require(value == 16 || value == 32, "screen_group is 16 or 32");
             h->screen_group = (uint32_t)value;
@@ -685,13 +693,12 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->set_device();
             h->set_list_cache((uint64_t)value);
             h->max_gpu_memory = 0;  // explicit residency control replaces the Config cap
+            h->tier_by_cap = false;
         } else if (n == "max_gpu_memory") {
             require(value >= 0, "max_gpu_memory out of range");
             h->set_device();
             h->max_gpu_memory = (uint64_t)value;
-            h->apply_memory_cap(h->count);
-            h->quiesce();
-            h->screen_update();  // the screen's extra bytes count against the cap too
+            h->apply_memory_cap(h->count);  // (on, or back off when the tier came from the cap)
         } else if (n == "bounded_stats") {
             h->bounded_stats = value != 0;  // statistics only: results never change
         } else if (n == "comm_timeout_ms") {
@@ -785,7 +792,7 @@ int vdb_ivf_profile_reset(vdb_ivf* h) {
         p->set_device();
         HIPCHECK(hipDeviceSynchronize());
         p->events_used = 0;
-        HIPCHECK(hipMemsetAsync(p->stats.ensure(8), 0, 64, p->stream));
+        HIPCHECK(hipMemsetAsync(p->stats.ensure(16), 0, 128, p->stream));
         HIPCHECK(hipStreamSynchronize(p->stream));
         h->set_device();
     });
@@ -813,6 +820,14 @@ int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
             p.total_ms += c;
             p.local_merge_ms += m;
             p.scan_launches++;
+            if (e.collected) {  // the deferred screen: the collect kernel, then its re-checks
+                float cl = 0;
+                float rc = 0;
+                HIPCHECK(hipEventElapsedTime(&cl, e.collect_begin, e.collect_end));
+                HIPCHECK(hipEventElapsedTime(&rc, e.collect_end, e.scan_end));
+                p.collect_ms += cl;
+                p.recheck_ms += rc;
+            }
             if (e.xchg) {  // (the exchange of a batch, or of the whole call in the tier)
                 float x = 0, r = 0;
                 HIPCHECK(hipEventElapsedTime(&x, e.end, e.x_end));
@@ -822,16 +837,19 @@ int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
                 p.exchanges++;
             }
         }
-        unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (h->stats.p) HIPCHECK(hipMemcpy(st, h->stats.p, 64, hipMemcpyDeviceToHost));
+        unsigned long long st[16] = {};
+        if (h->stats.p) HIPCHECK(hipMemcpy(st, h->stats.p, 128, hipMemcpyDeviceToHost));
         p.distinct_lists = st[0];
         p.scan_vectors = st[1];
         p.work_items = st[2];
         p.batches = st[3];
         p.scan_bytes = st[1] * (uint64_t)h->dim * 4;
         p.pair_vectors = st[4];
-        p.exact_reranks = st[5];
-        p.bounded_blocks = st[6];
+        // (inline screen / bounded scan: st[5], st[6]; deferred screen: st[8] collected,
+        // st[9] blocks, st[10] re-checked)
+        p.exact_reranks = st[5] + st[10];
+        p.bounded_blocks = st[6] + st[9];
+        p.screen_collected = st[8];
         p.computed_vectors = st[7];
         *out = p;
         hh->set_device();

@@ -160,6 +160,7 @@ struct DevBuf {
         cap = std::max<size_t>(n, 1);
         return p;
     }
+    size_t device_bytes() const { return (p && !host) ? cap * sizeof(T) : 0; }
     void swap(DevBuf& o) {
         std::swap(p, o.p);
         std::swap(cap, o.cap);
@@ -185,6 +186,8 @@ inline uint64_t cdiv(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 struct EventSet {
     hipEvent_t begin, coarse_end, scan_begin, scan_end, end;
+    hipEvent_t collect_begin, collect_end;  // deferred screened scan: around its collect kernel
+    bool collected = false;
     hipEvent_t x_end, m_end;  // multi-GPU: the all-gather done (comm stream), the rank merge done
     bool xchg = false;        // this batch (or call) ended in an exchange
 };
@@ -309,6 +312,19 @@ struct vdb_ivf {
     bool screen_stale = false;  // lists or centroids changed since the last build
     uint32_t screen_segs_auto = 4;  // segments per screened wide item (upload_directory; option segs_per_item)
     uint32_t screen_group = 16;     // queries per screened wide item at most: 16 or 32 (option screen_group; 32 measured slower at cfg4: 5.80 vs 5.27 ms)
+    // Deferred re-checks (option screen_defer, default 1): the scan only collects candidates
+    // against upper-bound thresholds; survivors of each pair's final threshold are re-checked
+    // exactly afterwards from the arena (screen.hip ivf_screen_collect). 0: the inline kernel
+    // (re-checks as candidates appear, from a row-major fp32 copy of the lists).
+    bool screen_defer = true;
+    uint32_t screen_cand_cap = 4u << 20;  // collected candidates per batch (an overflowing pair is recomputed whole)
+    // One fp32 copy of the lists in HBM: while the screen is built, the row-major copy
+    // (screen_rows, slot order: what the exact re-checks read) is the only one and the
+    // interleaved arena is released (arena_dropped); whatever needs the arena (an exact-path
+    // search: k > 64 or the screen off; an add / relayout; export; save) rebuilds it from the
+    // rows first (ensure_arena: one interleave pass), and it then stays until the next
+    // screen build. Footprint while screening: rows + shadow + norms + ids ~ 1.5x the lists.
+    bool arena_dropped = false;
     DevBuf<uint4> screen_sh;
     DevBuf<float> screen_rows;
     DevBuf<float4> screen_meta;
@@ -386,6 +402,13 @@ struct vdb_ivf {
         DevBuf<uint16_t> qres{true};  // screened scan: per (query, probe) bf16 A rows [B * P][dp]
         DevBuf<float4> pst{true};     // ... and their norms
         DevBuf<uint32_t> thr4{true};  // ... and, per sorted pair, 4 quarter-list thresholds
+        // deferred screened scan: collected candidates, per sorted pair survivor counts, offsets and
+        // overflow marks, the survivors' slots grouped per pair, and (tier) their fetched rows
+        DevBuf<uint4> scand{true};
+        DevBuf<uint32_t> scnt{true}, soff{true}, ovf{true}, ubcnt{true};
+        DevBuf<uint2> surv{true};
+        DevBuf<float> ublist{true}, sdist{true};
+        DevBuf<float> srows{true};
         DevBuf<uint8_t> xrec{true}, xgat{true};  // multi-GPU: this rank's packed partials, the gathered records
         DevBuf<float> gq{true};            // group member: the call's queries on this device
         DevBuf<uint32_t> greq{true};       // group member: the call's request starts on this device
@@ -395,6 +418,22 @@ struct vdb_ivf {
         hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
         hipEvent_t scan_done = nullptr;  // (scan_window) this slot's latest scan has finished
         bool used = false;
+        uint64_t device_bytes() const {
+            uint64_t b = 0;
+            for (uint64_t x : {qpad.device_bytes(), cd.device_bytes(), cdelta.device_bytes(), part_d.device_bytes(),
+                               slot_d.device_bytes(), carry_d.device_bytes(), carry2_d.device_bytes(),
+                               part_i.device_bytes(), slot_i.device_bytes(), carry_i.device_bytes(),
+                               carry2_i.device_bytes(), probes.device_bytes(), nseg_qp.device_bytes(), pbqp.device_bytes(),
+                               sorted_pair.device_bytes(), pbs.device_bytes(), counters.device_bytes(),
+                               l1base.device_bytes(), cand.device_bytes(), thr.device_bytes(), l1_items.device_bytes(),
+                               l1_d.device_bytes(), l1_i.device_bytes(), items.device_bytes(), items_w.device_bytes(),
+                               qres.device_bytes(), pst.device_bytes(), thr4.device_bytes(), scand.device_bytes(),
+                               scnt.device_bytes(), soff.device_bytes(), ovf.device_bytes(), ubcnt.device_bytes(),
+                               surv.device_bytes(), ublist.device_bytes(), sdist.device_bytes(), srows.device_bytes(),
+                               xrec.device_bytes(), xgat.device_bytes(), gq.device_bytes(), greq.device_bytes()})
+                b += x;
+            return b;
+        }
     };
     static constexpr int kSlots = VDB_SLOTS;  // workspace slots: batches one handle runs concurrently
     SearchSlot slots[kSlots];
@@ -493,7 +532,7 @@ struct vdb_ivf {
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
         if (home_fd_direct >= 0) ::close(home_fd_direct);
         for (auto& e : events)
-            for (hipEvent_t x : {e.begin, e.coarse_end, e.scan_begin, e.scan_end, e.end, e.x_end, e.m_end})
+            for (hipEvent_t x : {e.begin, e.coarse_end, e.scan_begin, e.scan_end, e.end, e.x_end, e.m_end, e.collect_begin, e.collect_end})
                 (void)hipEventDestroy(x);
         for (auto& sl : slots) {
             if (sl.fork) (void)hipEventDestroy(sl.fork);
@@ -510,6 +549,26 @@ struct vdb_ivf {
     }
 
     void set_device() { HIPCHECK(hipSetDevice(device)); }
+
+    // Every byte of device memory the handle holds (vdb_ivf_gpu_bytes_allocated): lists in
+    // whatever layouts exist (arena, row-major copy, bf16 shadow, norms, ids, list cache),
+    // centroids, directories, the search workspaces of every slot and the staging buffers.
+    uint64_t device_footprint() const {
+        uint64_t b = 0;
+        for (uint64_t x : {cent_rm.device_bytes(), cent_il.device_bytes(), arena.device_bytes(), arena_ids.device_bytes(),
+                           d_block_off.device_bytes(), d_count_local.device_bytes(), d_count_global.device_bytes(),
+                           d_nseg.device_bytes(), screen_sh.device_bytes(), screen_rows.device_bytes(),
+                           screen_meta.device_bytes(), screen_blist.device_bytes(), cache.device_bytes(),
+                           cache_ids.device_bytes(), drows.device_bytes(), dpad.device_bytes(), drows_cs.device_bytes(),
+                           dpad_cs.device_bytes(), out_d.device_bytes(), qin.device_bytes(), out_i.device_bytes(),
+                           d_req.device_bytes(), stats.device_bytes()})
+            b += x;
+        for (const auto& w : slots) b += w.device_bytes();
+        if (co)
+            for (const HostBatch& hb : co->slots)
+                b += hb.dq.device_bytes() + hb.dd.device_bytes() + hb.di.device_bytes() + hb.dreq.device_bytes();
+        return b;
+    }
 
     // ---- host-API search: direct, or through the coalescing queue ----
     void search_host(const float* q, uint32_t n, uint32_t nprobe, uint32_t k, float* dist, uint64_t* ids,
@@ -761,20 +820,42 @@ struct vdb_ivf {
         screen_stale = true;  // rebuilt by the next search (a bulk add appends in many calls)
     }
 
+    // The interleaved arena back from the row-major copy (identical contents: the copy holds
+    // every slot of every block, pads included) plus its zeroed slack block.
+    void ensure_arena() {
+        if (!arena_dropped) return;
+        quiesce();
+        const size_t vec4 = (size_t)(arena_blocks + 1) * d4 * 64;
+        arena.ensure(vec4);
+        HIPCHECK(hipMemsetAsync(arena.p + (size_t)arena_blocks * d4 * 64, 0, (size_t)d4 * 64 * sizeof(float4), stream));
+        vdbk::launch_interleave(screen_rows.p, arena_blocks * 64, dp, arena.p, stream);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipStreamSynchronize(stream));
+        arena_dropped = false;
+    }
+    // Drop the screen's data (the arena made whole first: the rows may be its only copy).
+    void screen_release() {
+        ensure_arena();
+        screen_ready = false;
+        screen_sh.release();
+        screen_rows.release();
+        screen_meta.release();
+        screen_blist.release();
+    }
+
     // (Re)build the screened scan's data from the arena, or drop it. Called by the first
     // search after the lists or centroids change (every search issued before the change
     // was quiesced by it, and none since has read the data) and by the options that
     // decide whether it exists.
     void screen_update() {
         screen_stale = false;
+        ensure_arena();  // (the build reads the arena)
         screen_ready = false;
+        // (Config::max_gpu_memory caps the resident list bytes, as the reference's
+        // gpu_memory_used_ does; the screen's shadow is not list data and is not counted)
         const bool want = screen_opt && metric != 2 && !tiered() && !arena.host && arena_blocks > 0;
-        const uint64_t extra = arena_blocks * 64 * ((uint64_t)dp * 6 + 16);  // shadow + rows + norms
-        if (!want || (max_gpu_memory && arena_blocks * 64 * ((uint64_t)dp * 4 + 8) + extra > max_gpu_memory)) {
-            screen_sh.release();
-            screen_rows.release();
-            screen_meta.release();
-            screen_blist.release();
+        if (!want) {
+            screen_release();
             return;
         }
         std::vector<uint32_t> blist(arena_blocks, 0);
@@ -788,10 +869,7 @@ struct vdb_ivf {
             screen_blist.ensure(arena_blocks);
         } catch (const VdbError&) {  // no room for it: the exact scan serves
             (void)hipGetLastError();
-            screen_sh.release();
-            screen_rows.release();
-            screen_meta.release();
-            screen_blist.release();
+            screen_release();
             return;
         }
         HIPCHECK(hipMemcpyAsync(screen_blist.p, blist.data(), arena_blocks * 4, hipMemcpyHostToDevice, stream));
@@ -800,6 +878,9 @@ struct vdb_ivf {
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipStreamSynchronize(stream));
         screen_ready = true;
+        // the row-major copy is now the lists' fp32 copy: release the arena
+        arena.release();
+        arena_dropped = true;
     }
 
     // Rebuild the arena so list l holds `keep[l]` of its current blocks at new
@@ -809,6 +890,11 @@ struct vdb_ivf {
     }
     void relayout(const std::vector<uint64_t>& new_count, const std::vector<uint8_t>& new_owned, bool host_arena) {
         quiesce();
+        // the screen's data describes the old lists: drop it before the new arena is
+        // allocated (peak HBM old + new arena, not that plus the shadow and rows); the next
+        // search rebuilds it
+        screen_release();
+        screen_stale = true;
         std::vector<uint64_t> new_off(nlist, 0), old_off(nlist, 0);
         std::vector<uint32_t> nblocks(nlist, 0);
         uint64_t blocks = 0;
@@ -1205,6 +1291,12 @@ struct vdb_ivf {
         count = cnt;
         total = 0;
         for (uint32_t l = 0; l < nlist; ++l) total += cnt[l];
+        screen_ready = false;  // (everything is replaced: no arena rebuild for the old lists)
+        arena_dropped = false;
+        screen_sh.release();
+        screen_rows.release();
+        screen_meta.release();
+        screen_blist.release();
         arena.release();  // no home copy in memory: the file is the home
         arena_ids.release();
         arena_blocks = 0;
@@ -1248,12 +1340,20 @@ struct vdb_ivf {
             if (owned[l]) b += cnt[l] * ((uint64_t)dim * 4 + 8);
         return b;
     }
+    bool tier_by_cap = false;  // the tier was entered because the lists outgrew max_gpu_memory
     void apply_memory_cap(const std::vector<uint64_t>& cnt) {
-        if (max_gpu_memory == 0 || max_gpu_memory == ~0ull || tiered() || file_home()) return;
+        if (file_home()) return;
+        if (tier_by_cap && (max_gpu_memory == 0 || stored_list_bytes(cnt) <= max_gpu_memory)) {
+            set_list_cache(0);  // the cap was lifted or raised above the lists: back to HBM
+            tier_by_cap = false;
+            return;
+        }
+        if (max_gpu_memory == 0 || max_gpu_memory == ~0ull || tiered()) return;
         if (stored_list_bytes(cnt) <= max_gpu_memory) return;
         require(max_gpu_memory >= block_bytes(dp),
                 "max_gpu_memory is below one block of 64 vectors (set 0 for no cap)", VDB_ERR_OUT_OF_MEMORY);
         set_list_cache(max_gpu_memory);
+        tier_by_cap = true;
     }
 
     // Row-major [n][dim] device input -> zero-padded [n][dp] (or the input itself).
@@ -1300,6 +1400,14 @@ struct vdb_ivf {
         if (file_home()) {  // the file holds the list row-major, as returned
             if (ids) pread_all(ids, c * 8, file_off[l]);
             if (vectors) pread_all(vectors, c * dim * 4, file_off[l] + c * 8);
+            return;
+        }
+        if (arena_dropped) {  // the row-major copy holds the list in slot (= add) order
+            if (vectors)
+                HIPCHECK(hipMemcpy2DAsync(vectors, (size_t)dim * 4, screen_rows.p + block_off[l] * 64 * dp, (size_t)dp * 4,
+                                          (size_t)dim * 4, c, hipMemcpyDeviceToHost, stream));
+            if (ids) HIPCHECK(hipMemcpyAsync(ids, arena_ids.p + block_off[l] * 64, c * 8, hipMemcpyDeviceToHost, stream));
+            HIPCHECK(hipStreamSynchronize(stream));
             return;
         }
         DevBuf<float> dv;
@@ -1555,11 +1663,13 @@ struct vdb_ivf {
     EventSet& next_events() {
         if (events_used == events.size()) {
             EventSet e;
-            for (hipEvent_t* p : {&e.begin, &e.coarse_end, &e.scan_begin, &e.scan_end, &e.end, &e.x_end, &e.m_end})
+            for (hipEvent_t* p : {&e.begin, &e.coarse_end, &e.scan_begin, &e.scan_end, &e.end, &e.x_end, &e.m_end,
+                                  &e.collect_begin, &e.collect_end})
                 HIPCHECK(hipEventCreate(p));
             events.push_back(e);
         }
         events[events_used].xchg = false;
+        events[events_used].collected = false;
         return events[events_used++];
     }
 
@@ -1587,7 +1697,7 @@ struct vdb_ivf {
         w.pbqp.ensure(BP);
         w.sorted_pair.ensure(BP);
         w.pbs.ensure(BP);
-        w.counters.ensure(8);
+        w.counters.ensure(vdbk::kCounters);
         w.l1base.ensure(BP);
         w.thr.ensure(BP);
         w.l1_items.ensure(max_l1);
@@ -1658,8 +1768,10 @@ struct vdb_ivf {
         // and narrow items
         if (screen_stale) screen_update();
         // 32-query items (option screen_group) where their shared lists fit the LDS
-        const uint32_t swq = screen_group == 32 && vdbk::scan_screen_fits(k, dp, 32) ? 32u : 16u;
+        // (the deferred kernel's items hold at most 16 queries)
+        const uint32_t swq = !screen_defer && screen_group == 32 && vdbk::scan_screen_fits(k, dp, 32) ? 32u : 16u;
         const bool screened = screen_ready && !tiered() && regs_k == 1 && metric != 2 && vdbk::scan_screen_fits(k, dp, swq);
+        if (!screened && arena_dropped) ensure_arena();  // (the exact scans read the arena)
         const uint32_t mfma_min = !screened && wide && waves == 4 && metric != 2 && !(VDB_SCAN_DIAG & 2) &&
                                           vdbk::scan_bounded_fits(d4, k)
                                       ? scan_mfma_min : 0u;
@@ -1683,8 +1795,25 @@ struct vdb_ivf {
         // the bounded items first (the batch's most-probed lists), on the same stream
         if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
         if (screened) {
+            const bool defer = screen_defer;
+            // candidates at most: every (query, vector) pair the batch can have (B queries x the
+            // P largest stored lists), capped by the option
+            const uint32_t ccap = (uint32_t)std::min<uint64_t>(
+                screen_cand_cap, std::max<uint64_t>(1024, (uint64_t)B * nseg_prefix[P] * seg_blocks * 64));
+            if (defer) {
+                slot_buf(w, w.scnt, BP);
+                slot_buf(w, w.ovf, BP);
+                slot_buf(w, w.soff, (size_t)BP + 1);
+                slot_buf(w, w.scand, ccap);
+                slot_buf(w, w.surv, ccap);
+                slot_buf(w, w.sdist, ccap);
+                slot_buf(w, w.ubcnt, BP);
+                slot_buf(w, w.ublist, (size_t)BP * vdbk::kUbLists * k);
+            }
             vdbk::launch_screen_pairs(metric, w.q, B, P, w.probes.p, cent_rm.p, dp, slot_buf(w, w.qres, (size_t)BP * dp),
-                                      slot_buf(w, w.pst, BP), slot_buf(w, w.thr4, (size_t)BP * 4), s);
+                                      slot_buf(w, w.pst, BP), slot_buf(w, w.thr4, (size_t)BP * 4), s,
+                                      defer ? w.scnt.p : nullptr, defer ? w.ovf.p : nullptr,
+                                      defer ? w.counters.p : nullptr, defer ? w.ubcnt.p : nullptr);
             sa.thr4 = w.thr4.p;
             sa.shadow = screen_sh.p;
             sa.rows = screen_rows.p;
@@ -1697,7 +1826,27 @@ struct vdb_ivf {
             sa.wide_q = swq;
             sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks, vdbk::kPersistentBlocks / 2));
             const uint64_t want = std::max<uint64_t>(max_wide, (max_items + 3) / 4);
-            vdbk::launch_scan_screen(metric, (uint32_t)(scan_blocks ? std::min<uint64_t>(want, scan_blocks) : want), sa, s);
+            const uint32_t grid = (uint32_t)(scan_blocks ? std::min<uint64_t>(want, scan_blocks) : want);
+            if (defer) {
+                sa.cand = w.scand.p;
+                sa.cand_cap = ccap;
+                sa.ccount = w.counters.p + vdbk::kCtrCand;
+                sa.ovf = w.ovf.p;
+                sa.ublist = w.ublist.p;
+                sa.ubcnt = w.ubcnt.p;
+                sa.mstats = bounded_stats ? stats.p + 8 : nullptr;
+                if (ev) HIPCHECK(hipEventRecord(ev->collect_begin, s));
+                vdbk::launch_screen_collect(metric, grid, sa, s);
+                if (ev) {
+                    HIPCHECK(hipEventRecord(ev->collect_end, s));
+                    ev->collected = true;
+                }
+                vdbk::launch_screen_select(sa, BP, w.scnt.p, w.soff.p, w.surv.p, w.ovf.p, s);
+                vdbk::launch_screen_recheck(metric, sa, BP, w.probes.p, w.nseg_qp.p, w.soff.p, w.scnt.p, w.surv.p, w.ovf.p,
+                                            nullptr, w.sdist.p, ccap, s);
+            } else {
+                vdbk::launch_scan_screen(metric, grid, sa, s);
+            }
         } else if (wide && fused_scan) {
             // one persistent grid takes both queues (no side stream, no fork/join)
             // (narrow_blocks counts 4-wave workgroups: as many waves start on the narrow queue)
@@ -1911,8 +2060,8 @@ struct vdb_ivf {
     // (allocated once per call, cpp:210-211). `xworld` > 0 sizes the multi-GPU records.
     SearchSlot& begin_call(uint32_t n, uint32_t P, uint32_t k, hipStream_t s, uint32_t xworld) {
         if (!stats.p) {
-            stats.ensure(8);
-            HIPCHECK(hipMemsetAsync(stats.p, 0, 64, s));
+            stats.ensure(16);
+            HIPCHECK(hipMemsetAsync(stats.p, 0, 128, s));
         }
         SearchSlot& w = slots[next_slot];
         next_slot = (next_slot + 1) % kSlots;
@@ -1983,13 +2132,13 @@ struct vdb_ivf {
             require(comm_world == world && comm_rank == rank,
                     "the attached communicator's (rank, world) differs from the handle's shard", VDB_ERR_STATE);
         SearchSlot& w = begin_call(n, P, k, s, xchg ? comm_world : 0);
-        if (xchg && tiered()) {
-            // A sharded index larger than HBM (configs[4]): this rank serves its shard
-            // through its own cache. The tier cuts the call into sub-batches by what this
-            // rank's cache holds, which differs between ranks, so the exchange is per
-            // CALL: the whole call's partials in one record, ONE all-gather, one merge.
-            // (Every rank takes this path whenever its tier is on, so all ranks issue the
-            // same collectives whatever their cache contents.)
+        if (xchg && (tiered() || comm_world > 1)) {
+            // The exchange is per CALL at world > 1: the whole call's partials in one record,
+            // ONE all-gather, one merge. A rank's own state (its tier, switched on by its own
+            // shard's size against max_gpu_memory, and what its cache holds) decides how it
+            // cuts a call into batches, so per-batch exchanges could differ in number and
+            // size between ranks; per call, every rank issues the same collective whatever
+            // its state. With 64-query calls (the bench) a call is one batch.
             slot_buf(w, w.xgat, vdb_rank_record_bytes(n, k) * comm_world);
             call_to_record(w, d_q, n, P, k, s, req_start);
             exchange(w, n, k, d_dist, d_ids, s);

@@ -205,6 +205,7 @@ void add_device(vdb_ivf* g, const float* d_v, const uint64_t* d_ids, const uint3
 uint64_t gpu_bytes(const vdb_ivf* g, bool allocated) {
     uint64_t b = 0;
     for (auto& mb : g->members) b += allocated ? vdb_ivf_gpu_bytes_allocated(mb.get()) : vdb_ivf_gpu_bytes(mb.get());
+    if (allocated) b += g->device_footprint();  // (the group's own host-API staging and stream buffers)
     return b;
 }
 
@@ -498,7 +499,7 @@ int vdb_ivf_attach_comm(vdb_ivf* h, const void* id, uint32_t rank, uint32_t worl
             }
             mine[0] = ((uint64_t)h->dim << 32) | h->nlist;
             mine[1] = ((uint64_t)(uint32_t)h->metric << 32) | h->batch;
-            mine[2] = ((uint64_t)h->tiered() << 1) | (uint64_t)h->stale;
+            mine[2] = (uint64_t)h->stale;  // (the tier may differ between ranks: exchanges are per call)
             mine[3] = fnv;
             mine[4] = h->total;
             DevBuf<uint64_t> dm, dall;
@@ -522,7 +523,7 @@ int vdb_ivf_attach_comm(vdb_ivf* h, const void* id, uint32_t rank, uint32_t worl
             for (uint32_t q = 0; q < world; ++q)
                 require(std::equal(mine.begin(), mine.begin() + 5, all.begin() + words * q),
                         h->rank_tag() + "rank " + std::to_string(q) +
-                            " differs in dimension, nlist, metric, batch, list-cache tier, stale_slots or list sizes",
+                            " differs in dimension, nlist, metric, batch, stale_slots or list sizes",
                         VDB_ERR_STATE);
             for (uint32_t wd = 0; wd < nw; ++wd) {
                 uint64_t any = 0, twice = 0;

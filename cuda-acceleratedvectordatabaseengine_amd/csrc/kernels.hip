@@ -990,6 +990,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         counters[5] = 0;  // bounded workgroups)
         counters[6] = 0;
         counters[7] = n_bounded;  // bounded items: items_w[n_exact, n_exact + n_bounded)
+        counters[kCtrValid] = nvalid;  // (sorted pairs [0, nvalid) are the batch's valid pairs)
         atomicAdd(&stats[0], (unsigned long long)nd);  // (the per-wave sums follow)
         atomicAdd(&stats[2], (unsigned long long)(n_narrow + n_wide));
         atomicAdd(&stats[3], 1ull);

@@ -44,6 +44,12 @@ constexpr int kPlanMaxPairs = 8192;        // batch * nprobe per plan launch
 constexpr int kMaxK = 1024;                // top-k capacity (16 registers x 64 lanes)
 constexpr size_t kLdsBytes = 160 * 1024;   // LDS per CU (gfx950)
 constexpr uint32_t kPersistentBlocks = 512; // scan grid: 2 workgroups per CU on 256 CUs
+// per-batch counters (the plan kernel's [0, 8), then the deferred screened scan's)
+constexpr int kCtrValid = 8;   // valid (query, probe) pairs of the batch (sorted pairs [0, n))
+constexpr int kCtrCand = 9;    // candidates the screen collected (may exceed the buffer)
+constexpr int kCtrSurv = 10;   // survivors of the final thresholds
+constexpr int kCounters = 16;
+constexpr int kUbLists = 32;   // deferred screened scan: upper-bound lists kept per (query, list) pair
 
 struct ScanItem {
     uint32_t list;
@@ -131,6 +137,14 @@ struct ScanArgs {
     uint32_t P = 0;
     uint32_t wide_q = 16;  // queries per screened wide item at most (16 or 32)
     uint32_t* thr4 = nullptr;  // per sorted pair, 4 quarter-list thresholds (screen.hip)
+    // Deferred screened scan: collected (sorted pair, slot, lower bound, rank) entries, their
+    // capacity, the collection counter (counters + kCtrCand) and per sorted pair the overflow mark.
+    uint4* cand = nullptr;
+    uint32_t cand_cap = 0;
+    uint32_t* ccount = nullptr;
+    uint32_t* ovf = nullptr;
+    float* ublist = nullptr;    // per sorted pair kUbLists lists of k upper bounds (the waves' running lists)
+    uint32_t* ubcnt = nullptr;  // ... and how many were offered
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);
@@ -147,9 +161,23 @@ bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq);
 size_t screen_shadow_u4(uint64_t blocks, uint32_t d4);  // shadow size (uint4) incl. the prefetch slack
 void launch_screen_build(const float4* arena, uint64_t blocks, uint32_t d4, const uint32_t* block_list,
                          const float* cent_rm, uint4* shadow, float* rows, float4* meta, hipStream_t s);
+// scnt / ovf / counters (the deferred scan; null for the inline one) are reset too.
 void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, const uint32_t* probes,
-                         const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, uint32_t* thr4, hipStream_t s);
+                         const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, uint32_t* thr4, hipStream_t s,
+                         uint32_t* scnt = nullptr, uint32_t* ovf = nullptr, uint32_t* counters = nullptr,
+                         uint32_t* ubcnt = nullptr);
 void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
+// Deferred screened scan: collect (a.cand), then select (each pair's final threshold, the
+// survivors of it grouped per pair in surv with offsets soff[0 .. nvalid] and their count in
+// counters[kCtrSurv]), then the exact re-check of the survivors into each pair's only partial.
+void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
+void launch_screen_select(const ScanArgs& a, uint32_t BP, uint32_t* scnt, uint32_t* soff, uint2* surv,
+                          const uint32_t* ovf, hipStream_t s);
+// surv: (slot, sorted pair) per survivor; fetched: null = rows from a.rows by slot, else the
+// survivors' rows [survivor][dp] (tier); sdist: their exact distances (max_surv entries).
+void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uint32_t* probes, uint32_t* nseg_qp,
+                           const uint32_t* soff, const uint32_t* scnt, const uint2* surv, const uint32_t* ovf,
+                           const float* fetched, float* sdist, uint32_t max_surv, hipStream_t s);
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                        const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,

@@ -108,13 +108,13 @@ __global__ __launch_bounds__(256) void ivf_screen_build(const float4* __restrict
         const float4* blk = arena + b * d4 * 64;
         const float4* cen = (const float4*)(cent_rm + (size_t)block_list[b] * dp);
         const uint64_t slot = b * 64 + lane;
-        float4* row = (float4*)(rows + slot * dp);
+        float4* row = rows ? (float4*)(rows + slot * dp) : nullptr;
         double x2 = 0.0, b2 = 0.0, e2 = 0.0;
         bool huge = false;
         for (uint32_t t = 0; t < d4; ++t) {
             const float4 x = blk[(size_t)t * 64 + lane];
             const float4 c = cen[t];
-            row[t] = x;
+            if (rows) row[t] = x;  // (the inline scan's row-major copy; null: deferred re-checks read the arena)
             const float xv[4] = {x.x, x.y, x.z, x.w}, cv[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -150,9 +150,18 @@ __global__ __launch_bounds__(256) void ivf_screen_pairs(const float* __restrict_
                                                         const uint32_t* __restrict__ probes,
                                                         const float* __restrict__ cent_rm, uint32_t dp,
                                                         uint16_t* __restrict__ qres, float4* __restrict__ pst,
-                                                        uint32_t* __restrict__ thr4) {
+                                                        uint32_t* __restrict__ thr4, uint32_t* __restrict__ scnt,
+                                                        uint32_t* __restrict__ ovf, uint32_t* __restrict__ counters,
+                                                        uint32_t* __restrict__ ubcnt) {
     const int lane = lane_id();
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < 4 * BP; e += gridDim.x * blockDim.x) thr4[e] = kThrInf;
+    if (scnt)  // (the deferred scan: survivor counts, overflow marks and the candidate count)
+        for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < BP; e += gridDim.x * blockDim.x) {
+            scnt[e] = 0u;
+            ovf[e] = 0u;
+            ubcnt[e] = 0u;
+            if (e == 0) counters[kCtrCand] = 0u;
+        }
     for (uint32_t i = blockIdx.x * 4 + wave_index(); i < BP; i += gridDim.x * 4) {
         const float* qr = q + (size_t)(i / P) * dp;
         const float* cr = cent_rm + (size_t)probes[i] * dp;
@@ -612,8 +621,574 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
     if (a.fused) drain_narrow();
 }
 
+// ============================================================================
+// The DEFERRED screened scan (default): screen every pair, re-check later, only what the
+// list's final threshold leaves.
+//
+// The inline kernel above re-checks a candidate the moment it passes the threshold the
+// wave knows at that point; early in a segment that threshold is loose, so most of its
+// re-checks (~200 per (query, list) pair at the headline) are of vectors that later turn
+// out to be far from the list's top-k. Here the scan only COLLECTS candidates:
+//  * thresholds come from upper bounds alone: every wave keeps, per query, the 64
+//    smallest upper bounds (approx + delta) of the vectors it has screened in its item as
+//    a sorted list in registers (16 lanes x 4 of the query's DPP row; each block's 64 upper
+//    bounds are bitonic-sorted and merged in). k vectors of the list have exact distances
+//    at or below the list's k-th element, so it is a valid shared threshold: published to
+//    the item (LDS) and list-wide (a.thr) like the inline scan's exact k-th, and its
+//    ceil(k/4)-th into the quarter slot of the wave's residue (the 4 waves of a wide item
+//    hold 4 distinct residues, so thr4's maximum is a valid threshold too);
+//  * a pair is collected unless lower bound > th (the inline test): (sorted pair, slot,
+//    lower bound) appended to a.cand (wave-aggregated atomic); beyond the capacity the
+//    pair is marked overflowed;
+//  * every segment's partials are written empty.
+// Then (ivf_screen_filter / _offsets / _scatter / _recheck) each collected pair is kept
+// only if its lower bound is not above the pair's FINAL threshold (min of a.thr and thr4's
+// maximum after the whole list was screened: still >= the list's exact k-th distance, so
+// every member of the list's top-min(k, n) survives), the survivors are grouped per pair,
+// and one wave per (query, list) pair recomputes them with the reference's sequential sum
+// and writes the pair's exact top-k as its first segment partial. On iid 768-D data a
+// pair then re-checks ~k + a few vectors (the vectors within 2 delta of its k-th
+// distance) instead of ~200. An overflowed pair is recomputed exactly over its whole list.
+// ============================================================================
+
+// Ascending 64-element bitonic sort of u (the 16 lanes x 4 registers of each DPP row).
+__device__ __forceinline__ void block_sort64(float (&u)[4]) {
+    const int l = lane_id() & 15;
+    bitonic64_step<2, 1>(u, l);
+    bitonic64_step<4, 2>(u, l), bitonic64_step<4, 1>(u, l);
+    bitonic64_step<8, 4>(u, l), bitonic64_step<8, 2>(u, l), bitonic64_step<8, 1>(u, l);
+    bitonic64_step<16, 8>(u, l), bitonic64_step<16, 4>(u, l), bitonic64_step<16, 2>(u, l), bitonic64_step<16, 1>(u, l);
+    bitonic64_step<32, 16>(u, l), bitonic64_step<32, 8>(u, l), bitonic64_step<32, 4>(u, l);
+    bitonic64_step<32, 2>(u, l), bitonic64_step<32, 1>(u, l);
+    bitonic64_step<64, 32>(u, l), bitonic64_step<64, 16>(u, l), bitonic64_step<64, 8>(u, l);
+    bitonic64_step<64, 4>(u, l), bitonic64_step<64, 2>(u, l), bitonic64_step<64, 1>(u, l);
+}
+// rl (sorted ascending) <- the 64 smallest of rl and u (both sorted ascending), sorted:
+// min(rl[e], u[63 - e]) is bitonic; one merge pass sorts it. Element e = 4 (lane & 15) + v;
+// 63 - e is lane 15 - (lane & 15) (DPP row mirror), register 3 - v.
+__device__ __forceinline__ void merge_sorted64(float (&rl)[4], const float (&u)[4]) {
+    const int l = lane_id() & 15;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const float rv = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(u[3 - v]), 0x140, 0xF,
+                                                                            0xF, false));
+        rl[v] = fminf(rl[v], rv);
+    }
+    bitonic64_step<64, 32>(rl, l), bitonic64_step<64, 16>(rl, l), bitonic64_step<64, 8>(rl, l);
+    bitonic64_step<64, 4>(rl, l), bitonic64_step<64, 2>(rl, l), bitonic64_step<64, 1>(rl, l);
+}
+// Element e (wave-uniform, 0..63) of each DPP row's sorted list, in every lane of the row.
+__device__ __forceinline__ float row_elem(const float (&u)[4], int e) {
+    const int v = e & 3;
+    const float x = v == 0 ? u[0] : v == 1 ? u[1] : v == 2 ? u[2] : u[3];
+    return __shfl(x, (lane_id() & ~15) + (e >> 2));
+}
+
+// One wave: collect the candidates of segment `seg` of list it.list for the nq (<= 16)
+// queries of the item starting at sorted pair it.pair_start + q0. rl: the wave's running
+// lists of upper bounds (4 query rows; reset by the caller per item); s_thr: the item's
+// shared k-th (LDS); residue: the wave's quarter slot (0..3, distinct per wave of an item).
+template <int M, int KD>
+__device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
+                                                const uint32_t seg, float4* rl_lds, uint32_t* s_thr,
+                                                const uint32_t residue) {
+    const int lane = lane_id();
+    const uint32_t dp = a.dp, ks = dp >> 5;
+    const uint32_t count = a.count[it.list];
+    const uint32_t seg_vectors = a.seg_blocks * 64;
+    const uint64_t b0 = a.block_off[it.list] + (uint64_t)seg * a.seg_blocks;
+    const uint32_t v0 = seg * seg_vectors;
+    const uint32_t nv = min(count - v0, seg_vectors);
+    const uint32_t nb = (nv + 63) >> 6;
+    const int k = (int)a.k, kq = ((int)a.k + 3) / 4;
+    const uint32_t* pairs = a.sorted_pair + it.pair_start + q0;
+    const float cm = (float)(4 * dp + 16) * 0x1.02p-24f;
+    const float cr = (float)(dp + 2) * 0x1.02p-24f;
+    const float cu = 0x1.02p-23f;
+    auto pair_of = [&](int g) -> uint32_t {
+        const uint32_t pr = pairs[g];
+        return (pr >> 16) * a.P + (pr & 0xFFFFu);
+    };
+    const int ga = min(lane & 15, nq - 1);
+    const uint4* qa_row = (const uint4*)(a.qres + (size_t)pair_of(ga) * dp) + (lane >> 4);
+    const float4* pst_r[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pst_r[r] = a.pst + pair_of(min(4 * (lane >> 4) + r, nq - 1));
+    uint32_t collected = 0;
+
+    const uint4* sp = a.shadow + b0 * (uint64_t)dp * 8 + lane;
+    uint4 xa[KD][4], qa[KD];
+#pragma unroll
+    for (int u = 0; u < KD; ++u) {
+#pragma unroll
+        for (int vt = 0; vt < 4; ++vt) xa[u][vt] = ld_nt_u4(sp + (size_t)(u * 4 + vt) * 64);
+        qa[u] = qa_row[4 * (u % ks)];
+    }
+    for (uint32_t j = 0; j < nb; ++j) {
+        f32x4 acc[4];
+#pragma unroll
+        for (int vt = 0; vt < 4; ++vt) acc[vt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (uint32_t s0 = 0; s0 < ks; s0 += KD) {
+            static_for<0, KD>([&](auto uu) {
+                constexpr int u = decltype(uu)::value;
+                const bf16x8 A = as_bf16x8(qa[u]);
+#pragma unroll
+                for (int vt = 0; vt < 4; ++vt)
+                    acc[vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, as_bf16x8(xa[u][vt]), acc[vt], 0, 0, 0);
+                const uint64_t nxt = (uint64_t)j * ks + s0 + u + KD;
+#pragma unroll
+                for (int vt = 0; vt < 4; ++vt) xa[u][vt] = ld_nt_u4(sp + (nxt * 4 + vt) * 64);
+                qa[u] = qa_row[4 * ((s0 + u + KD) % ks)];
+            });
+        }
+        // lower bounds into acc, upper bounds into ubv (the inline kernel's bound)
+        float ubv[4][4];
+        float4 pst[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pst[r] = *pst_r[r];
+#pragma unroll
+        for (int vt = 0; vt < 4; ++vt) {
+            const float4 mt = a.meta[(b0 + j) * 64 + 16 * vt + (lane & 15)];
+            const bool valid = j * 64 + 16 * vt + (lane & 15) < nv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float dot = acc[vt][r];
+                const float4 ps = pst[r];
+                const float approx = M == kL2 ? (ps.x + mt.x) - 2.0f * dot : -(ps.x + dot);
+                const float an = ps.y + ps.z, bn = mt.y + mt.z;
+                const float cs = an * mt.z + ps.z * bn + ps.z * mt.z;
+                float del;
+                if (M == kL2) {
+                    const float rest = 2.0f * (cs + cm * (an * bn)) + cu * (ps.x + mt.x + fabsf(approx));
+                    del = rest + cr * (fabsf(approx) + rest);
+                } else {
+                    del = cs + cm * (an * bn) + cr * (ps.y * mt.w) + cu * (ps.y * ps.w + an * bn + fabsf(approx));
+                }
+                del = del * 1.001f + 1e-30f;
+                const float ub = approx + del;
+                acc[vt][r] = approx - del;
+                ubv[r][vt] = valid && ub == ub ? ub : __builtin_inff();
+            }
+        }
+        // per query row: the block's sorted upper bounds into the running list; its k-th
+        // (and ceil(k/4)-th) published; th = the smallest valid threshold known
+        float th[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int g = 4 * (lane >> 4) + r;
+            const int gc = min(g, nq - 1);
+            const uint32_t spi = it.pair_start + q0 + gc;
+            block_sort64(ubv[r]);
+            float4 rv = rl_lds[r * 64 + lane];
+            float rl[4] = {rv.x, rv.y, rv.z, rv.w};
+            merge_sorted64(rl, ubv[r]);
+            rl_lds[r * 64 + lane] = make_float4(rl[0], rl[1], rl[2], rl[3]);
+            const float tw = row_elem(rl, k - 1), tq = row_elem(rl, kq - 1);
+            uint32_t* gt = a.thr + spi;
+            uint32_t* s4 = a.thr4 + (size_t)spi * 4;
+            const uint4 t4 = *(const uint4*)s4;
+            const float th4 = fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w)));
+            const float cur = fminf(fminf(ord_dec(*gt), th4), ord_dec(s_thr[gc]));
+            if ((lane & 15) == 0 && g < nq) {
+                if (tw < cur) {
+                    atomicMin(&s_thr[g], ord_enc(tw));
+                    atomicMin(gt, ord_enc(tw));
+                }
+                if (tq < ord_dec(s4[residue])) atomicMin(s4 + residue, ord_enc(tq));
+            }
+            th[r] = g < nq ? fminf(tw, cur) : -__builtin_inff();
+        }
+        // candidates: one atomic per block for the wave's whole batch of them (the ballots are
+        // recomputed for the writes rather than held: registers)
+        auto is_cand = [&](int vt, int r) {
+            return j * 64 + 16 * vt + (lane & 15) < nv && 4 * (lane >> 4) + r < nq && !(acc[vt][r] > th[r]);
+        };
+        uint32_t tot = 0;
+#pragma unroll
+        for (int vt = 0; vt < 4; ++vt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) tot += (uint32_t)__popcll(__ballot(is_cand(vt, r)));
+        if (tot) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(a.ccount, tot);
+            base = __builtin_amdgcn_readfirstlane(base);
+            collected += tot;
+#pragma unroll
+            for (int vt = 0; vt < 4; ++vt) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const bool c = is_cand(vt, r);
+                    const uint64_t mm = __ballot(c);
+                    if (c) {
+                        const uint32_t idx = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
+                                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+                        const uint32_t spi = it.pair_start + q0 + 4 * (lane >> 4) + r;
+                        const uint32_t slot = (uint32_t)((b0 + j) * 64 + 16 * vt + (lane & 15));
+                        if (idx < a.cand_cap)
+                            a.cand[idx] = make_uint4(spi, slot, __float_as_uint(acc[vt][r]), 0u);
+                        else
+                            a.ovf[spi] = 1u;  // (any store of 1: idempotent)
+                    }
+                    base += (uint32_t)__popcll(mm);
+                }
+            }
+        }
+    }
+    if (a.mstats && lane == 0) {
+        atomicAdd(&a.mstats[0], (unsigned long long)collected);
+        atomicAdd(&a.mstats[1], (unsigned long long)nb);
+    }
+}
+
+__device__ __forceinline__ void reset_rl(float4* rl_lds) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float inf = __builtin_inff();
+        rl_lds[r * 64 + lane] = make_float4(inf, inf, inf, inf);
+    }
+}
+
+// The wave's running lists of the item's nq queries (the k smallest upper bounds of the
+// vectors it screened) appended to their pairs' contributions (a.ublist: per sorted pair
+// kUbLists lists of k; a.ubcnt: how many were offered). Every contribution covers vectors
+// no other contribution covers, so the k-th smallest of their union is a valid threshold
+// (ivf_screen_tfinal); a list beyond the capacity is dropped, which only loosens it.
+__device__ __forceinline__ void contribute_rl(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
+                                              const float4* rl_lds) {
+    const int lane = lane_id();
+    const int k = (int)a.k;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int g = 4 * (lane >> 4) + r;
+        const uint32_t spi = it.pair_start + q0 + min(g, nq - 1);
+        uint32_t slot = 0;
+        if ((lane & 15) == 0 && g < nq) slot = atomicAdd(&a.ubcnt[spi], 1u);
+        slot = __shfl(slot, lane & ~15);
+        const float4 rv = rl_lds[r * 64 + lane];
+        const float rl[4] = {rv.x, rv.y, rv.z, rv.w};
+        if (g < nq && slot < (uint32_t)kUbLists) {
+            float* dst = a.ublist + ((size_t)spi * kUbLists + slot) * k;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int e = 4 * (lane & 15) + v;
+                if (e < k) dst[e] = rl[v];
+            }
+        }
+    }
+}
+
+// ivf_screen_collect: the persistent grid of ivf_scan_screen over the same queues (wide
+// items: a list's segments x <= 16 queries, the 4 waves taking the segments dynamically;
+// narrow items: one wave = one segment x <= 4 queries), collecting instead of re-checking.
+template <int M, int KD>
+__global__ __launch_bounds__(256, 2) void ivf_screen_collect(ScanArgs a) {
+    __shared__ uint32_t s_next, s_seg;
+    __shared__ uint32_t s_thr[16];
+    __shared__ uint32_t s_thr_w[4][16];
+    __shared__ float4 s_rl[4][4 * 64];  // each wave's running lists (4 query rows x 64 lanes)
+    const uint32_t wv = wave_index();
+    const int lane = lane_id();
+    float4* rl = s_rl[wv];
+
+    auto drain_narrow = [&]() {
+        const uint32_t n_narrow = a.counters[0];
+        for (;;) {
+            uint32_t idx = 0;
+            if (lane == 0) idx = atomicAdd(&a.work[0], 1u);
+            idx = __builtin_amdgcn_readfirstlane(idx);
+            if (idx >= n_narrow) break;
+            ScanItem it = a.items[idx];
+            it.list = __builtin_amdgcn_readfirstlane(it.list);
+            it.seg = __builtin_amdgcn_readfirstlane(it.seg);
+            it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
+            it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
+            if (lane < (int)it.npairs) s_thr_w[wv][lane] = a.thr[it.pair_start + lane];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            reset_rl(rl);
+            collect_segment<M, KD>(a, it, 0, (int)it.npairs, it.seg, rl, s_thr_w[wv], it.seg & 3u);
+            contribute_rl(a, it, 0, (int)it.npairs, rl);
+        }
+    };
+
+    const uint32_t n_wide = a.counters[3];
+    if (a.fused && blockIdx.x + a.fused >= gridDim.x) drain_narrow();
+    for (;;) {
+        if (threadIdx.x == 0) s_next = atomicAdd(&a.work[1], 1u);
+        __syncthreads();
+        const uint32_t b = s_next;
+        if (b >= n_wide) break;
+        ScanItem it = a.items_w[b];
+        it.list = __builtin_amdgcn_readfirstlane(it.list);
+        it.seg = __builtin_amdgcn_readfirstlane(it.seg);
+        it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
+        it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
+        const int nq = (int)it.npairs;
+        if (threadIdx.x == 0) s_seg = 0;
+        if (threadIdx.x < (uint32_t)nq) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
+        __syncthreads();
+        const uint32_t seg_vectors = a.seg_blocks * 64;
+        const uint32_t nseg = (a.count[it.list] + seg_vectors - 1) / seg_vectors;
+        const uint32_t seg0 = it.seg * a.segs_item, seg1 = min(nseg, seg0 + a.segs_item);
+        reset_rl(rl);
+        bool any = false;
+        for (;;) {
+            uint32_t sg = 0;
+            if (lane == 0) sg = atomicAdd(&s_seg, 1u);
+            sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
+            if (sg >= seg1) break;
+            collect_segment<M, KD>(a, it, 0, nq, sg, rl, s_thr, wv);
+            any = true;
+        }
+        if (any) contribute_rl(a, it, 0, nq, rl);
+        __syncthreads();  // (s_thr and s_seg are reset by the next item only after every wave is done)
+    }
+    if (a.fused) drain_narrow();
+}
+
+// One wave per valid sorted pair: the k-th smallest of the union of its contributed upper-
+// bound lists (k vectors of the list have exact distances at or below it) lowers a.thr.
+__global__ __launch_bounds__(256) void ivf_screen_tfinal(ScanArgs a) {
+    const int lane = lane_id();
+    const uint32_t nvalid = a.counters[kCtrValid];
+    const int k = (int)a.k;
+    for (uint32_t s = blockIdx.x * 4 + wave_index(); s < nvalid; s += gridDim.x * 4) {
+        const uint32_t nl = min(a.ubcnt[s], (uint32_t)kUbLists);
+        const uint32_t n = nl * (uint32_t)k;
+        const float* src = a.ublist + (size_t)s * kUbLists * k;
+        float best = __builtin_inff();  // the 64 smallest so far, ascending over lanes
+        uint64_t bid = kNoId;
+        for (uint32_t e0 = 0; e0 < n; e0 += 64) {
+            float d = e0 + lane < n ? src[e0 + lane] : __builtin_inff();
+            uint64_t id = kNoId;
+            bitonic_sort64(d, id);
+            bitonic_merge64(best, bid, d, id);
+        }
+        const float kth = rd_lane(best, k - 1);
+        if (lane == 0 && kth < ord_dec(a.thr[s])) a.thr[s] = ord_enc(kth);
+    }
+}
+
+// Per collected pair: keep it if its lower bound is not above its pair's final threshold;
+// its rank among its pair's survivors into .w (~0: dropped).
+__global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ cand, const uint32_t* __restrict__ counters,
+                                                         uint32_t cap, const uint32_t* __restrict__ thr,
+                                                         const uint32_t* __restrict__ thr4,
+                                                         const uint32_t* __restrict__ ovf, uint32_t* __restrict__ scnt) {
+    const uint32_t n = min(counters[kCtrCand], cap);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint4 c = cand[i];
+        const uint32_t sp = c.x;
+        const uint4 t4 = *(const uint4*)(thr4 + (size_t)sp * 4);
+        const float T = fminf(ord_dec(thr[sp]),
+                              fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w))));
+        const bool keep = !ovf[sp] && !(__uint_as_float(c.z) > T);
+        cand[i].w = keep ? atomicAdd(&scnt[sp], 1u) : ~0u;
+    }
+}
+
+// Exclusive scan of the survivor counts of the batch's valid sorted pairs (one workgroup):
+// soff[0 .. nvalid], the total into counters[kCtrSurv].
+__global__ __launch_bounds__(1024) void ivf_screen_offsets(const uint32_t* __restrict__ scnt,
+                                                           uint32_t* __restrict__ counters,
+                                                           uint32_t* __restrict__ soff) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t n = counters[kCtrValid];
+    const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
+    const uint32_t c0 = min(n, threadIdx.x * per), c1 = min(n, c0 + per);
+    uint32_t s = 0;
+    for (uint32_t i = c0; i < c1; ++i) s += scnt[i];
+    // inclusive scan of s over the workgroup
+    uint32_t x = s;
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+    for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
+        if (w < (threadIdx.x >> 6)) wbase += wsum[w];
+        total += wsum[w];
+    }
+    uint32_t o = wbase + x - s;
+    for (uint32_t i = c0; i < c1; ++i) {
+        soff[i] = o;
+        o += scnt[i];
+    }
+    if (threadIdx.x == 0) {
+        soff[n] = total;
+        counters[kCtrSurv] = total;
+    }
+}
+
+__global__ __launch_bounds__(256) void ivf_screen_scatter(const uint4* __restrict__ cand,
+                                                          const uint32_t* __restrict__ counters, uint32_t cap,
+                                                          const uint32_t* __restrict__ soff,
+                                                          uint2* __restrict__ surv) {
+    const uint32_t n = min(counters[kCtrCand], cap);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint4 c = cand[i];
+        if (c.w != ~0u) surv[soff[c.x] + c.w] = make_uint2(c.y, c.x);  // (slot, sorted pair)
+    }
+}
+
+// The exact sequential distance of `slot` for query row qr: from the interleaved arena
+// ([block][d4][64 lanes] float4; device or page-locked host memory) or a row-major row.
+template <int M, bool ROWS>
+__device__ __forceinline__ float exact_dist(const float4* __restrict__ src, uint64_t row_or_slot, uint32_t d4,
+                                            const float4* __restrict__ qr) {
+    constexpr int kP = 8;
+    const float4* base;
+    size_t stride;
+    if (ROWS) {
+        base = src + row_or_slot * d4;
+        stride = 1;
+    } else {
+        base = src + (row_or_slot >> 6) * (uint64_t)d4 * 64 + (row_or_slot & 63);
+        stride = 64;
+    }
+    float acc = 0.0f;
+    float4 xb[kP], qb[kP];
+#pragma unroll
+    for (int i = 0; i < kP; ++i) {
+        xb[i] = i < (int)d4 ? base[(size_t)i * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+        qb[i] = i < (int)d4 ? qr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    for (uint32_t t0 = 0; t0 < d4; t0 += kP) {
+#pragma unroll
+        for (int i = 0; i < kP; ++i) {
+            if (t0 + i < d4) acc = acc4<M>(acc, qb[i], xb[i]);
+            const uint32_t tn = t0 + kP + i;
+            if (tn < d4) {
+                xb[i] = base[(size_t)tn * stride];
+                qb[i] = qr[tn];
+            }
+        }
+    }
+    return dist_finish<M>(acc);
+}
+
+// Exact distances of the survivors (one 64-thread workgroup per kExactRows of them, in
+// their per-pair order): the rows are loaded into LDS together, kExactRows x 1 KiB
+// contiguous wave-loads per 256 dims, all in flight at once, from the row-major fp32 copy
+// of the lists (slot-indexed) or, in the tier, from the fetched rows ([survivor][dp]);
+// then one lane per row runs the reference's sequential sum over its LDS row (row stride
+// d4 + 1 float4: the lanes' rows fall on distinct banks) against its pair's query.
+constexpr int kExactRows = 16;
+constexpr int kExactChunks = 3;  // 64-float4 chunks of a row loaded per pass (768 dims)
+__host__ __device__ constexpr size_t exact_lds(uint32_t d4) { return ((size_t)kExactRows * (d4 + 1) + 64) * 16; }
+
+template <int M>
+__global__ __launch_bounds__(64) void ivf_screen_exact(ScanArgs a, const uint2* __restrict__ surv,
+                                                       const float* __restrict__ fetched,
+                                                       float* __restrict__ sdist) {
+    extern __shared__ __attribute__((aligned(16))) float4 rlds[];
+    const int lane = lane_id();
+    const uint32_t total = a.counters[kCtrSurv];
+    const uint32_t d4 = a.d4, rs = d4 + 1;
+    const float4* src = fetched ? (const float4*)fetched : (const float4*)a.rows;
+    for (uint32_t base = blockIdx.x * kExactRows; base < total; base += gridDim.x * kExactRows) {
+        const uint32_t ng = min((uint32_t)kExactRows, total - base);
+        const uint2 my = lane < (int)ng ? surv[base + lane] : make_uint2(0u, 0u);
+        // every load unconditional (clamped to valid rows and dims) so that all of them are in
+        // flight together; writes of clamped elements go to the LDS dump row kExactRows
+        for (uint32_t c0 = 0; c0 < d4; c0 += 64 * kExactChunks) {
+            float4 v[kExactRows][kExactChunks];
+#pragma unroll
+            for (int r = 0; r < kExactRows; ++r) {
+                const uint32_t rr = min((uint32_t)r, ng - 1);
+                const uint64_t row = fetched ? (uint64_t)(base + rr) : (uint64_t)__builtin_amdgcn_readlane(my.x, (int)rr);
+#pragma unroll
+                for (int c = 0; c < kExactChunks; ++c) v[r][c] = src[row * d4 + min(c0 + 64 * c + lane, d4 - 1)];
+            }
+#pragma unroll
+            for (int r = 0; r < kExactRows; ++r)
+#pragma unroll
+                for (int c = 0; c < kExactChunks; ++c) {
+                    const uint32_t t = c0 + 64 * c + lane;
+                    rlds[(r < (int)ng && t < d4) ? r * rs + t : kExactRows * rs + lane] = v[r][c];
+                }
+        }
+        __syncthreads();
+        if (lane < (int)ng) {
+            const uint32_t q = a.sorted_pair[my.y] >> 16;
+            const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
+            const float4* xr = rlds + (size_t)lane * rs;
+            float acc = 0.0f;
+#pragma unroll 8
+            for (uint32_t t = 0; t < d4; ++t) acc = acc4<M>(acc, qr[t], xr[t]);
+            sdist[base + lane] = dist_finish<M>(acc);
+        }
+        __syncthreads();  // (the next rows overwrite the LDS)
+    }
+}
+
+// One wave per valid sorted (query, list) pair: the exact top-k of its survivors' distances
+// (or, for a pair that overflowed the candidate buffer, of its whole list, recomputed lane
+// = vector from the row-major copy), written as the pair's only partial.
+template <int M>
+__global__ __launch_bounds__(256) void ivf_screen_pair_topk(ScanArgs a, const uint32_t* __restrict__ probes,
+                                                            uint32_t* __restrict__ nseg_qp,
+                                                            const uint32_t* __restrict__ soff,
+                                                            const uint32_t* __restrict__ scnt,
+                                                            const uint2* __restrict__ surv,
+                                                            const float* __restrict__ sdist,
+                                                            const uint32_t* __restrict__ ovf) {
+    const int lane = lane_id();
+    const uint32_t nvalid = a.counters[kCtrValid];
+    const int k = (int)a.k;
+    unsigned long long rechecked = 0;
+    for (uint32_t s = blockIdx.x * 4 + wave_index(); s < nvalid; s += gridDim.x * 4) {
+        const uint32_t pr = a.sorted_pair[s];
+        const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
+        WaveTopK<1> tk;
+        tk.init();
+        float kd = __builtin_inff();
+        uint64_t ki = kNoId;
+        if (ovf[s]) {
+            const uint32_t list = probes[(size_t)q * a.P + p];
+            const uint32_t n = a.count[list];
+            const uint64_t lbase = a.block_off[list] * 64;
+            const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
+            for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                const bool act = i < n;
+                float dist = __builtin_inff();
+                uint64_t id = kNoId;
+                if (act) {
+                    dist = exact_dist<M, true>((const float4*)a.rows, lbase + i, a.d4, qr);
+                    id = a.ids[lbase + i];
+                }
+                offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
+            }
+            rechecked += n;
+        } else {
+            const uint32_t n = scnt[s], o = soff[s];
+            for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                const bool act = i < n;
+                const float dist = act ? sdist[o + i] : __builtin_inff();
+                const uint64_t id = act ? a.ids[surv[o + i].x] : kNoId;
+                offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
+            }
+            rechecked += n;
+        }
+        // the pair's exact top-k is its only partial: the merge reads the first of its segments
+        const uint32_t part = a.part_base_sorted[s];
+        if (lane < k) {
+            a.part_d[(size_t)part * k + lane] = tk.d[0];
+            a.part_i[(size_t)part * k + lane] = tk.id[0];
+        }
+        if (lane == 0) nseg_qp[(size_t)q * a.P + p] = 1u;
+    }
+    if (a.mstats && lane == 0 && rechecked) atomicAdd(&a.mstats[2], rechecked);
+}
+
 bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq) {
-    return k >= 1 && k <= 64 && dp % 64 == 0 && (wq == 16 || wq == 32) &&
+    return k >= 1 && k <= 64 && dp % 64 == 0 && (wq == 16 || wq == 32) && exact_lds(dp / 4) <= kLdsBytes / 2 &&
            screen_item_lds(k, wq) + 4 * screen_wave_lds(k) + 256 <= kLdsBytes / 2;
 }
 
@@ -627,12 +1202,62 @@ void launch_screen_build(const float4* arena, uint64_t blocks, uint32_t d4, cons
 }
 
 void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, const uint32_t* probes,
-                         const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, uint32_t* thr4, hipStream_t s) {
+                         const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, uint32_t* thr4, hipStream_t s,
+                         uint32_t* scnt, uint32_t* ovf, uint32_t* counters, uint32_t* ubcnt) {
     const uint32_t BP = B * P;
     if (!BP) return;
     const uint32_t g = std::min<uint32_t>((BP + 3) / 4, 2048);
-    if (metric == kL2) ivf_screen_pairs<kL2><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst, thr4);
-    else ivf_screen_pairs<kIP><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst, thr4);
+    if (metric == kL2)
+        ivf_screen_pairs<kL2><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst, thr4, scnt, ovf, counters, ubcnt);
+    else
+        ivf_screen_pairs<kIP><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst, thr4, scnt, ovf, counters, ubcnt);
+}
+
+void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
+    if (!grid_blocks) return;
+    const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
+    const bool kd4 = (a.dp / 32) % 4 == 0;
+    if (metric == kL2) {
+        if (kd4) ivf_screen_collect<kL2, 4><<<g, 256, 0, s>>>(a);
+        else ivf_screen_collect<kL2, 2><<<g, 256, 0, s>>>(a);
+    } else {
+        if (kd4) ivf_screen_collect<kIP, 4><<<g, 256, 0, s>>>(a);
+        else ivf_screen_collect<kIP, 2><<<g, 256, 0, s>>>(a);
+    }
+}
+
+void launch_screen_select(const ScanArgs& a, uint32_t BP, uint32_t* scnt, uint32_t* soff, uint2* surv,
+                          const uint32_t* ovf, hipStream_t s) {
+    if (!BP) return;
+    uint32_t* ctr = const_cast<uint32_t*>(a.counters);
+    ivf_screen_tfinal<<<std::max<uint32_t>(1, std::min<uint32_t>(2048, (BP + 3) / 4)), 256, 0, s>>>(a);
+    const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(1024, (a.cand_cap + 255) / 256));
+    ivf_screen_filter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, a.thr, a.thr4, ovf, scnt);
+    ivf_screen_offsets<<<1, 1024, 0, s>>>(scnt, ctr, soff);
+    ivf_screen_scatter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, soff, surv);
+}
+
+void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uint32_t* probes, uint32_t* nseg_qp,
+                           const uint32_t* soff, const uint32_t* scnt, const uint2* surv, const uint32_t* ovf,
+                           const float* fetched, float* sdist, uint32_t max_surv, hipStream_t s) {
+    if (!BP) return;
+    static const bool raised = [] {
+        for (const void* fn : {(const void*)ivf_screen_exact<kL2>, (const void*)ivf_screen_exact<kIP>})
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes / 2));
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)raised;
+    const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>(16384, (max_surv + kExactRows - 1) / kExactRows));
+    const size_t lds = exact_lds(a.d4);
+    const uint32_t gp = std::max<uint32_t>(1, std::min<uint32_t>(2048, (BP + 3) / 4));
+    if (metric == kL2) {
+        ivf_screen_exact<kL2><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
+        ivf_screen_pair_topk<kL2><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, sdist, ovf);
+    } else {
+        ivf_screen_exact<kIP><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
+        ivf_screen_pair_topk<kIP><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, sdist, ovf);
+    }
 }
 
 void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {

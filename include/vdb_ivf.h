@@ -91,6 +91,12 @@ typedef struct vdb_ivf_profile {
     double exchange_ms;        /* summed: this rank's results ready -> all-gather done (the wait for the
                                   slowest rank plus the collective itself) */
     double rank_merge_ms;      /* summed: all-gather done -> final results merged */
+    uint64_t screen_collected; /* deferred screened scan: (query, vector) pairs collected against the
+                                  upper-bound thresholds (option bounded_stats); exact_reranks counts
+                                  the survivors of each pair's final threshold, recomputed exactly */
+    double collect_ms;         /* deferred screened scan: summed durations of its collect kernel (the
+                                  stream of the bf16 shadow; scan_ms covers it and the re-check kernels) */
+    double recheck_ms;         /* ... and of the final thresholds, selection and exact re-checks after it */
 } vdb_ivf_profile;
 
 const char* vdb_last_error(void);

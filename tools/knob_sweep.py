@@ -8,7 +8,8 @@ timing experiments are separate builds: tools/build_variant.sh -DVDB_SCAN_DIAG=n
 with VDB_IVF_LIB).
 usage: tools/knob_sweep.py cfg3|cfg4|mix "wide_group=32" "seg_vectors=1024,segs_per_item=8" ...
   cfg4 = rank 0 of the 8-way sharded 100M x 768 index (the per-GPU work of 8 GPUs);
-  ip = the cfg3 index with the inner-product metric
+  ip = the cfg3 index with the inner-product metric; s8 = rank 0 of the cfg3 index cut 8 ways
+  (the per-GPU work of the 8-GPU headline)
 """
 import json
 import os
@@ -22,7 +23,8 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 DEFAULTS = {"seg_vectors": 0, "segs_per_item": 0, "wide_stride": 1, "fused_scan": 1, "narrow_blocks": 64,
-            "wide_group": 16, "fused_merge": 1, "scan_window": 0, "screen": 1, "bounded_stats": 0, "screen_group": 16}
+            "wide_group": 16, "fused_merge": 1, "scan_window": 0, "screen": 1, "bounded_stats": 0, "screen_group": 16,
+            "screen_defer": 1, "screen_cand_cap": 4 << 20}
 
 
 def main():
@@ -42,6 +44,8 @@ def main():
             idx, _ = bench.build_index_sharded(vdb, args, dev, 0, 8)
         else:
             idx, _ = bench.build_index(vdb, args, dev, 0, 1)
+            if wl == "s8":
+                idx.set_shard(0, 8)
         st = torch.cuda.current_stream()
         B, steps = 64, 12
         q = torch.empty((steps * B, 768), dtype=torch.float32, device=dev)
@@ -72,7 +76,10 @@ def main():
                               "alg_GB": round(alg / 1e9, 2),
                               "pairs_M": round(p["pair_vectors"] / max(p["batches"], 1) / 1e6, 2),
                               "computed_M": round(p["computed_vectors"] / max(p["batches"], 1) / 1e6, 2), "frac": round(alg / (p["scan_ms"] / n * 1e-3) / 8e12, 4),
-                              "rechecks_M": round(p["exact_reranks"] / max(p["batches"], 1) / 1e6, 3)}),
+                              "rechecks_M": round(p["exact_reranks"] / max(p["batches"], 1) / 1e6, 3),
+                              "collected_M": round(p.get("screen_collected", 0) / max(p["batches"], 1) / 1e6, 3),
+                              "collect_ms": round(p.get("collect_ms", 0) / n, 3),
+                              "recheck_ms": round(p.get("recheck_ms", 0) / n, 3)}),
                   flush=True)
             for n_, _ in opts:  # back to defaults
                 idx.set_option(n_, DEFAULTS[n_])

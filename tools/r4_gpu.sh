@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round-4 GPU session helper (run through gpurun from the repo root):
+#   bash tools/r4_gpu.sh <tag> <step>[,<step>...]
+# steps: t:<pytest args, ';'-separated files> | s:<workload>:<opt sets separated by '|'> | b:<bench args>
+#        p:<workload>:<opt sets> (the sweep under rocprofv3 --kernel-trace --stats)
+# Each step runs under its own time limit; a crash (abort, segfault, time limit) ends the
+# session, a failed assertion does not (the next steps still measure).
+set -o pipefail
+TAG=$1
+O=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=/tmp
+i=0
+IFS=',' read -ra STEPS <<< "$2"
+for st in "${STEPS[@]}"; do
+    i=$((i + 1))
+    kind=${st%%:*}
+    arg=${st#*:}
+    case $kind in
+        t) timeout -k 10 900 python -u -m pytest ${arg//;/ } -m gpu -q -rf --timeout 300 --timeout-method thread > "$O/$i.pytest.log" 2>&1
+           rc=$?; tail -15 "$O/$i.pytest.log" ;;
+        s) wl=${arg%%:*}; sets=${arg#*:}
+           IFS='|' read -ra SETS <<< "$sets"
+           timeout -k 10 900 python -u tools/knob_sweep.py "$wl" "${SETS[@]}" > "$O/$i.sweep_$wl.log" 2>&1
+           rc=$?; grep '^{' "$O/$i.sweep_$wl.log" ;;
+        p) wl=${arg%%:*}; sets=${arg#*:}
+           IFS='|' read -ra SETS <<< "$sets"
+           timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof$i" -o run -- python3 -u tools/knob_sweep.py "$wl" "${SETS[@]}" > "$O/$i.prof_$wl.log" 2>&1
+           rc=$?; grep '^{' "$O/$i.prof_$wl.log"; f=$(find "$O/prof$i" -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cut -d, -f1-8 "$f" | head -25 ;;
+        b) timeout -k 10 900 python -u bench.py ${arg//;/ } > "$O/$i.bench.log" 2>&1
+           rc=$?; grep '^{' "$O/$i.bench.log" | cut -c 1-1500 ;;
+    esac
+    echo "[step $i $kind] rc=$rc"
+    case $rc in 0|1) ;; *) tail -30 "$O/$i."*.log; exit $rc ;; esac
+done
