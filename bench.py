@@ -411,8 +411,10 @@ def tier_leg(vdb, idx, args, device, queries):
         od = torch.empty((call, args.k), dtype=torch.float32, device=device)
         oi = torch.empty((call, args.k), dtype=torch.int64, device=device)
         calls = min(args.tier_calls, len(queries) // call)
+        t0 = time.perf_counter()
         h.search_device(queries.data_ptr(), call, args.nprobe, args.k, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
-        torch.cuda.synchronize()  # (warm-up call: code objects, staging, the cache's first contents)
+        torch.cuda.synchronize()  # (warm-up call: code objects, staging, the cache's first contents, the
+        t_first = time.perf_counter() - t0  # screen's shadow built by streaming the file once)
         same = bool(torch.equal(oi, ref_i) and torch.equal(od.view(torch.int32), ref_d.view(torch.int32)))
         s0 = h.cache_stats()
         h.profile_enable(True)
@@ -429,7 +431,20 @@ def tier_leg(vdb, idx, args, device, queries):
         batches = nq / args.batch
         alg = prof["scan_bytes"] / batches  # the lists each batch of --batch queries probes, read once
         read = (s1["file_bytes_read"] - s0["file_bytes_read"]) / batches
-        return {"value": round(nq / el, 1), "unit": "queries/s", "calls": calls - 1, "queries_per_call": call,
+        screen = {}
+        if s1["screen_resident"]:
+            rows = s1["screen_rows_fetched"] - s0["screen_rows_fetched"]
+            screen = {"screen": "the shadow, norms and ids of every stored list HBM-resident; the fp32 rows read "
+                                "from the file only for the exact re-checks' survivors",
+                      "screen_hbm_gb": round(s1["screen_bytes"] / 1e9, 2),
+                      "survivor_rows_per_batch": round(rows / batches, 1),
+                      "survivor_row_bytes_per_batch": int((s1["screen_row_bytes"] - s0["screen_row_bytes"]) / batches),
+                      "screen_batches": s1["screen_batches"] - s0["screen_batches"],
+                      "screen_reruns": s1["screen_reruns"] - s0["screen_reruns"],
+                      "first_call_s_incl_shadow_build": round(t_first, 1),
+                      "collect_ms_per_batch": round(prof.get("collect_ms", 0.0) / max(prof["scan_launches"], 1), 3),
+                      "search_ms_per_batch": round(prof["total_ms"] / max(prof["scan_launches"], 1), 3)}
+        return {"value": round(nq / el, 1), "unit": "queries/s", "calls": calls - 1, "queries_per_call": call, **screen,
                 "file": path, "file_gb": round(file_bytes / 1e9, 2), "save_s": round(t_save, 1),
                 "lists_gb": round(shard_bytes / 1e9, 2),
                 "shard_file": args.emulate_shard > 1 or args.sharded_build,

@@ -52,7 +52,10 @@ class CacheStats(ctypes.Structure):
                 ("resident_lists", ctypes.c_uint64), ("loads", ctypes.c_uint64), ("evictions", ctypes.c_uint64),
                 ("bytes_loaded", ctypes.c_uint64), ("file_bytes_read", ctypes.c_uint64),
                 ("subbatches", ctypes.c_uint64), ("prefetches", ctypes.c_uint64), ("sync_loads", ctypes.c_uint64),
-                ("io_uring", ctypes.c_int32), ("o_direct", ctypes.c_int32)]
+                ("io_uring", ctypes.c_int32), ("o_direct", ctypes.c_int32),
+                ("screen_resident", ctypes.c_int32), ("reserved", ctypes.c_int32), ("screen_bytes", ctypes.c_uint64),
+                ("screen_batches", ctypes.c_uint64), ("screen_rows_fetched", ctypes.c_uint64),
+                ("screen_row_bytes", ctypes.c_uint64), ("screen_reruns", ctypes.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -739,6 +739,15 @@ int vdb_ivf_cache_stats(vdb_ivf* h, vdb_ivf_cache_stats_t* out) {
             out->sync_loads += m->tier_sync_loads;
             out->io_uring |= m->uring && m->uring->uring() ? 1 : 0;
             out->o_direct |= m->home_fd_direct >= 0 ? 1 : 0;
+            if (m->tiered() && m->screen_ready) {
+                out->screen_resident = 1;
+                out->screen_bytes += m->screen_sh.device_bytes() + m->screen_meta.device_bytes() +
+                                     m->screen_ids.device_bytes() + m->screen_blist.device_bytes();
+            }
+            out->screen_batches += m->screen_tier_batches;
+            out->screen_rows_fetched += m->screen_rows_fetched;
+            out->screen_row_bytes += m->screen_row_bytes;
+            out->screen_reruns += m->screen_reruns;
         }
     });
 }

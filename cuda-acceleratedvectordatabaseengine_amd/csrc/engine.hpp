@@ -325,6 +325,22 @@ struct vdb_ivf {
     // rows first (ensure_arena: one interleave pass), and it then stays until the next
     // screen build. Footprint while screening: rows + shadow + norms + ids ~ 1.5x the lists.
     bool arena_dropped = false;
+    // The screen in the list-cache tier (an index larger than HBM, configs[4]): the shadow,
+    // norms and ids of EVERY stored list stay HBM-resident (half the fp32 list bytes), packed
+    // by sblock_off; the fp32 rows stay at the home and only the survivors' rows are read per
+    // batch: straight from the page-locked host arena over PCIe, or, from a file home, by
+    // io_uring into page-locked staging and one copy to HBM (fetch_survivor_rows). No list is
+    // loaded into the cache for such a batch (the cache serves the exact-path searches).
+    std::vector<uint64_t> sblock_off;  // tier: per stored list its first shadow block
+    std::vector<uint32_t> sblist_host; // tier, file home: per shadow block its list
+    uint64_t sblocks = 0;
+    DevBuf<uint64_t> d_sblock_off;
+    DevBuf<uint64_t> screen_ids;       // tier: the ids in shadow slot order
+    DevBuf<float> fetch_stage;         // tier, file home: page-locked staging of the survivors' rows
+    DevBuf<float> fetch_dev;           // ... on the device ([n][dim], padded into the slot's srows)
+    std::vector<uint2> fetch_surv;     // ... their (slot, pair)
+    uint64_t screen_rows_fetched = 0, screen_row_bytes = 0, screen_tier_batches = 0, screen_reruns = 0;
+    uint32_t tier_cand_cap = 0;        // ... a candidate capacity grown by an overflow
     DevBuf<uint4> screen_sh;
     DevBuf<float> screen_rows;
     DevBuf<float4> screen_meta;
@@ -494,7 +510,7 @@ struct vdb_ivf {
     bool coalesce = true;
     uint32_t coalesce_max_queries = 1024;
     uint32_t coalesce_window_us = 0;
-    DevBuf<unsigned long long> stats;
+    DevBuf<unsigned long long> stats, stats_scratch;
 
     bool prof = false;
     std::vector<EventSet> events;
@@ -841,6 +857,9 @@ struct vdb_ivf {
         screen_rows.release();
         screen_meta.release();
         screen_blist.release();
+        screen_ids.release();
+        d_sblock_off.release();
+        sblocks = 0;
     }
 
     // (Re)build the screened scan's data from the arena, or drop it. Called by the first
@@ -853,7 +872,11 @@ struct vdb_ivf {
         screen_ready = false;
         // (Config::max_gpu_memory caps the resident list bytes, as the reference's
         // gpu_memory_used_ does; the screen's shadow is not list data and is not counted)
-        const bool want = screen_opt && metric != 2 && !tiered() && !arena.host && arena_blocks > 0;
+        if (tiered()) {
+            screen_update_tier();
+            return;
+        }
+        const bool want = screen_opt && metric != 2 && !arena.host && arena_blocks > 0;
         if (!want) {
             screen_release();
             return;
@@ -881,6 +904,142 @@ struct vdb_ivf {
         // the row-major copy is now the lists' fp32 copy: release the arena
         arena.release();
         arena_dropped = true;
+    }
+
+    // The tier's screen: shadow + norms + ids of every stored list in HBM (the deferred scan
+    // only: its re-checks read the survivors' rows from the home). Host home: built from the
+    // page-locked arena over PCIe. File home: the lists streamed through the io_uring read
+    // pipeline once, a group of lists at a time, into a device block buffer, built from there.
+    void screen_update_tier() {
+        screen_release();
+        if (!(screen_opt && screen_defer && metric != 2 && dp % 64 == 0)) return;
+        sblock_off.assign(nlist, 0);
+        uint64_t nb = 0;
+        for (uint32_t l = 0; l < nlist; ++l) {
+            if (!owned[l] || count[l] == 0) continue;
+            sblock_off[l] = file_home() ? nb : block_off[l];
+            nb = std::max<uint64_t>(nb, sblock_off[l] + list_blocks(l));
+        }
+        if (nb == 0) return;
+        std::vector<uint32_t> blist(nb, 0);
+        for (uint32_t l = 0; l < nlist; ++l)
+            if (owned[l] && count[l])
+                for (uint64_t b = 0; b < list_blocks(l); ++b) blist[sblock_off[l] + b] = l;
+        try {
+            screen_sh.ensure(vdbk::screen_shadow_u4(nb, d4));
+            screen_meta.ensure((size_t)nb * 64);
+            screen_blist.ensure(nb);
+            screen_ids.ensure((size_t)(nb + 1) * 64);
+            d_sblock_off.ensure(nlist);
+        } catch (const VdbError&) {  // no room: the tier's exact path serves
+            (void)hipGetLastError();
+            screen_release();
+            return;
+        }
+        HIPCHECK(hipMemcpyAsync(screen_blist.p, blist.data(), nb * 4, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemcpyAsync(d_sblock_off.p, sblock_off.data(), nlist * 8, hipMemcpyHostToDevice, stream));
+        if (!file_home()) {
+            vdbk::launch_screen_build(arena.p, nb, d4, screen_blist.p, cent_rm.p, screen_sh.p, nullptr, screen_meta.p,
+                                      stream);
+            HIPCHECK(hipMemcpyAsync(screen_ids.p, arena_ids.p, nb * 64 * 8, hipMemcpyHostToDevice, stream));
+        } else {
+            // groups of consecutive stored lists through a device block buffer of <= 1 GiB
+            const uint64_t gcap = std::max<uint64_t>(cdiv(*std::max_element(count.begin(), count.end()), 64),
+                                                     (1ull << 30) / ((uint64_t)d4 * 64 * 16 + 512));
+            DevBuf<float4> tv;
+            DevBuf<uint64_t> ti;
+            tv.ensure((gcap + 1) * d4 * 64);
+            ti.ensure((gcap + 1) * 64);
+            std::vector<std::pair<uint32_t, uint64_t>> loads;
+            uint64_t g0 = 0, gend = 0;
+            auto flush = [&]() {
+                if (loads.empty()) return;
+                HIPCHECK(hipMemsetAsync(tv.p, 0, (gend - g0) * d4 * 64 * sizeof(float4), stream));
+                load_lists(loads, stream, tv.p, ti.p);
+                vdbk::launch_screen_build(tv.p, gend - g0, d4, screen_blist.p + g0, cent_rm.p,
+                                          screen_sh.p + g0 * (uint64_t)d4 * 32, nullptr, screen_meta.p + g0 * 64, stream);
+                HIPCHECK(hipGetLastError());
+                HIPCHECK(hipMemcpyAsync(screen_ids.p + g0 * 64, ti.p, (gend - g0) * 64 * 8, hipMemcpyDeviceToDevice,
+                                        stream));
+                HIPCHECK(hipStreamSynchronize(stream));  // (the buffers are refilled by the next group)
+                loads.clear();
+            };
+            for (uint32_t l = 0; l < nlist; ++l) {
+                if (!owned[l] || count[l] == 0) continue;
+                if (!loads.empty() && sblock_off[l] + list_blocks(l) - g0 > gcap) flush();
+                if (loads.empty()) g0 = sblock_off[l];
+                loads.push_back({l, sblock_off[l] - g0});
+                gend = sblock_off[l] + list_blocks(l);
+            }
+            flush();
+            sblist_host = blist;
+        }
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipStreamSynchronize(stream));
+        sblocks = nb;
+        screen_ready = true;
+    }
+
+    // Tier, file home: after the deferred scan's selection, read the survivors' rows of the
+    // batch from the file (one read each, io_uring on the buffered descriptor: hot rows stay in
+    // the page cache) into page-locked staging, copy them to the device and pad them to dp.
+    // Returns the rows ([survivor][dp]) for the exact pass, or nullptr when the candidate
+    // buffer overflowed (the caller re-runs the batch with a larger one).
+    const float* fetch_survivor_rows(SearchSlot& w, uint32_t cap, uint32_t& need, hipStream_t s) {
+        uint32_t hc[vdbk::kCounters];
+        HIPCHECK(hipMemcpyAsync(hc, w.counters.p, sizeof(hc), hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        if (hc[vdbk::kCtrCand] > cap) {
+            need = hc[vdbk::kCtrCand];
+            return nullptr;
+        }
+        const uint32_t n = hc[vdbk::kCtrSurv];
+        fetch_surv.resize(n);
+        if (n) HIPCHECK(hipMemcpyAsync(fetch_surv.data(), w.surv.p, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        fetch_stage.host = true;
+        float* st = fetch_stage.ensure((size_t)std::max<uint32_t>(n, 1) * dim);
+        if (!uring) uring.reset(new UringReader(64));
+        const uint64_t row_bytes = (uint64_t)dim * 4;
+        uint32_t next = 0, done = 0;
+        try {
+            while (done < n) {
+                while (next < n && next - done < std::min(uring->capacity(), 64u)) {  // (<= 64 queued or in flight)
+                    const uint64_t slot = fetch_surv[next].x;
+                    const uint32_t l = sblist_host[slot >> 6];
+                    const uint64_t r = slot - sblock_off[l] * 64;
+                    uring->read(home_fd, st + (size_t)next * dim, (uint32_t)row_bytes,
+                                file_off[l] + count[l] * 8 + r * row_bytes, next);
+                    ++next;
+                }
+                for (const UringReader::Done& d : uring->wait(1)) {
+                    require(d.result == (int64_t)row_bytes,
+                            "short read of a survivor row from the list file" +
+                                (d.result < 0 ? std::string(": ") + std::strerror((int)-d.result) : ""),
+                            VDB_ERR_STATE);
+                    ++done;
+                }
+            }
+        } catch (...) {
+            uring->drain();
+            throw;
+        }
+        screen_rows_fetched += n;
+        screen_row_bytes += (uint64_t)n * row_bytes;
+        file_bytes_read += (uint64_t)n * row_bytes;
+        float* rows = slot_buf(w, w.srows, (size_t)std::max<uint32_t>(n, 1) * dp);
+        if (n) {
+            if (dim == dp) {
+                HIPCHECK(hipMemcpyAsync(rows, st, (size_t)n * row_bytes, hipMemcpyHostToDevice, s));
+            } else {
+                HIPCHECK(hipMemcpyAsync(fetch_dev.ensure((size_t)n * dim), st, (size_t)n * row_bytes,
+                                        hipMemcpyHostToDevice, s));
+                vdbk::launch_pad_rows(fetch_dev.p, n, dim, dp, rows, s);
+                HIPCHECK(hipGetLastError());
+            }
+        }
+        HIPCHECK(hipStreamSynchronize(s));  // (the staging is reused by the next batch)
+        return rows;
     }
 
     // Rebuild the arena so list l holds `keep[l]` of its current blocks at new
@@ -1129,14 +1288,17 @@ struct vdb_ivf {
     // each chunk's ids and rows are read (io_uring, up to kStages chunks in flight) into
     // a page-locked staging buffer, copied to HBM, padded to dp and interleaved into the
     // cache's block layout; a buffer is refilled once its copies have landed.
-    void load_lists(const std::vector<std::pair<uint32_t, uint64_t>>& loads, hipStream_t s) {
+    void load_lists(const std::vector<std::pair<uint32_t, uint64_t>>& loads, hipStream_t s,
+                    float4* dst_v = nullptr, uint64_t* dst_i = nullptr) {
+        float4* const tv = dst_v ? dst_v : cache.p;  // (the cache, or a caller's block buffer)
+        uint64_t* const ti = dst_i ? dst_i : cache_ids.p;
         if (!file_home()) {
             for (auto& ld : loads) {
                 const uint32_t l = ld.first;
                 const uint64_t off = ld.second, nb = list_blocks(l);
-                HIPCHECK(hipMemcpyAsync(cache.p + off * d4 * 64, arena.p + block_off[l] * d4 * 64,
+                HIPCHECK(hipMemcpyAsync(tv + off * d4 * 64, arena.p + block_off[l] * d4 * 64,
                                         nb * d4 * 64 * sizeof(float4), hipMemcpyHostToDevice, s));
-                HIPCHECK(hipMemcpyAsync(cache_ids.p + off * 64, arena_ids.p + block_off[l] * 64, nb * 64 * 8,
+                HIPCHECK(hipMemcpyAsync(ti + off * 64, arena_ids.p + block_off[l] * 64, nb * 64 * 8,
                                         hipMemcpyHostToDevice, s));
             }
             return;
@@ -1216,14 +1378,14 @@ struct vdb_ivf {
                             VDB_ERR_STATE);
                     if (--st.reads) continue;
                     --reading;
-                    HIPCHECK(hipMemcpyAsync(cache_ids.p + st.dst_block * 64, st.buf.p + st.ids_delta, st.m * 8,
+                    HIPCHECK(hipMemcpyAsync(ti + st.dst_block * 64, st.buf.p + st.ids_delta, st.m * 8,
                                             hipMemcpyHostToDevice, s));
                     HIPCHECK(hipMemcpyAsync(rows_d.p, st.buf.p + ids_cap + st.vec_delta, st.m * dim * 4,
                                             hipMemcpyHostToDevice, s));
                     HIPCHECK(hipEventRecord(st.copied, s));
                     st.copying = true;
                     vdbk::launch_pad_rows(rows_d.p, st.m, dim, dp, pad_d.p, s);
-                    vdbk::launch_interleave(pad_d.p, st.m, dp, cache.p + st.dst_block * d4 * 64, s);
+                    vdbk::launch_interleave(pad_d.p, st.m, dp, tv + st.dst_block * d4 * 64, s);
                     HIPCHECK(hipGetLastError());
                 }
             }
@@ -1770,7 +1932,8 @@ struct vdb_ivf {
         // 32-query items (option screen_group) where their shared lists fit the LDS
         // (the deferred kernel's items hold at most 16 queries)
         const uint32_t swq = !screen_defer && screen_group == 32 && vdbk::scan_screen_fits(k, dp, 32) ? 32u : 16u;
-        const bool screened = screen_ready && !tiered() && regs_k == 1 && metric != 2 && vdbk::scan_screen_fits(k, dp, swq);
+        const bool screened = screen_ready && (!tiered() || screen_defer) && regs_k == 1 && metric != 2 &&
+                              vdbk::scan_screen_fits(k, dp, swq);
         if (!screened && arena_dropped) ensure_arena();  // (the exact scans read the arena)
         const uint32_t mfma_min = !screened && wide && waves == 4 && metric != 2 && !(VDB_SCAN_DIAG & 2) &&
                                           vdbk::scan_bounded_fits(d4, k)
@@ -1779,9 +1942,12 @@ struct vdb_ivf {
         // (screened items: segs_per_item segments, default 4; a wave's top-k carries across
         // the segments it takes from one item)
         const uint32_t segs_screen = segs_item_opt ? segs_item_opt : screen_segs_auto;
-        vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, plan_wide, screened ? segs_screen : segs_item, w.items.p, w.items_w.p,
-                          w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p, w.l1base.p, w.l1_items.p, stats.p, w.thr.p,
-                          mfma_min, s);
+        auto plan = [&](unsigned long long* st) {
+            vdbk::launch_plan(w.probes.p, d_nseg.p, d_count_local.p, B, P, group, plan_wide, screened ? segs_screen : segs_item,
+                              w.items.p, w.items_w.p, w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p,
+                              w.l1base.p, w.l1_items.p, st, w.thr.p, mfma_min, s);
+        };
+        plan(stats.p);
         const bool in_ring = &w >= slots && &w < slots + kSlots;
         if (scan_window && in_ring && scan_seq >= scan_window) {  // the scan issued scan_window batches ago
             const SearchSlot& prev = slots[scan_hist[(scan_seq - scan_window) % 8]];
@@ -1796,11 +1962,15 @@ struct vdb_ivf {
         if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
         if (screened) {
             const bool defer = screen_defer;
+            // (the tier's file home reads the survivors' rows on the host: the batch then
+            // waits for its selection, and re-runs with a larger buffer if it overflowed)
+            const bool tier_file = tiered() && file_home();
             // candidates at most: every (query, vector) pair the batch can have (B queries x the
             // P largest stored lists), capped by the option
-            const uint32_t ccap = (uint32_t)std::min<uint64_t>(
+            uint32_t ccap = (uint32_t)std::min<uint64_t>(
                 screen_cand_cap, std::max<uint64_t>(1024, (uint64_t)B * nseg_prefix[P] * seg_blocks * 64));
-            if (defer) {
+            if (tier_file) ccap = std::max(ccap, tier_cand_cap);
+            auto alloc_defer = [&]() {
                 slot_buf(w, w.scnt, BP);
                 slot_buf(w, w.ovf, BP);
                 slot_buf(w, w.soff, (size_t)BP + 1);
@@ -1809,11 +1979,16 @@ struct vdb_ivf {
                 slot_buf(w, w.sdist, ccap);
                 slot_buf(w, w.ubcnt, BP);
                 slot_buf(w, w.ublist, (size_t)BP * vdbk::kUbLists * k);
-            }
-            vdbk::launch_screen_pairs(metric, w.q, B, P, w.probes.p, cent_rm.p, dp, slot_buf(w, w.qres, (size_t)BP * dp),
-                                      slot_buf(w, w.pst, BP), slot_buf(w, w.thr4, (size_t)BP * 4), s,
-                                      defer ? w.scnt.p : nullptr, defer ? w.ovf.p : nullptr,
-                                      defer ? w.counters.p : nullptr, defer ? w.ubcnt.p : nullptr);
+            };
+            auto pairs = [&]() {
+                vdbk::launch_screen_pairs(metric, w.q, B, P, w.probes.p, cent_rm.p, dp,
+                                          slot_buf(w, w.qres, (size_t)BP * dp), slot_buf(w, w.pst, BP),
+                                          slot_buf(w, w.thr4, (size_t)BP * 4), s, defer ? w.scnt.p : nullptr,
+                                          defer ? w.ovf.p : nullptr, defer ? w.counters.p : nullptr,
+                                          defer ? w.ubcnt.p : nullptr);
+            };
+            if (defer) alloc_defer();
+            pairs();
             sa.thr4 = w.thr4.p;
             sa.shadow = screen_sh.p;
             sa.rows = screen_rows.p;
@@ -1824,26 +1999,48 @@ struct vdb_ivf {
             sa.P = P;
             sa.segs_item = segs_screen;
             sa.wide_q = swq;
+            if (tiered()) {  // the resident shadow's packing and ids; rows from the home
+                sa.block_off = d_sblock_off.p;
+                sa.ids = screen_ids.p;
+                sa.rows = nullptr;
+                sa.arena = file_home() ? nullptr : arena.p;  // (host home: page-locked, read over PCIe)
+            }
             sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks, vdbk::kPersistentBlocks / 2));
             const uint64_t want = std::max<uint64_t>(max_wide, (max_items + 3) / 4);
             const uint32_t grid = (uint32_t)(scan_blocks ? std::min<uint64_t>(want, scan_blocks) : want);
             if (defer) {
-                sa.cand = w.scand.p;
-                sa.cand_cap = ccap;
-                sa.ccount = w.counters.p + vdbk::kCtrCand;
-                sa.ovf = w.ovf.p;
-                sa.ublist = w.ublist.p;
-                sa.ubcnt = w.ubcnt.p;
-                sa.mstats = bounded_stats ? stats.p + 8 : nullptr;
-                if (ev) HIPCHECK(hipEventRecord(ev->collect_begin, s));
-                vdbk::launch_screen_collect(metric, grid, sa, s);
-                if (ev) {
-                    HIPCHECK(hipEventRecord(ev->collect_end, s));
-                    ev->collected = true;
+                const float* fetched = nullptr;
+                for (int pass = 0;; ++pass) {
+                    if (pass) {  // a re-run after an overflow (tier, file home): plan and pairs reset the state
+                        alloc_defer();
+                        plan(stats_scratch.ensure(16));  // (statistics of the batch are counted once)
+                        pairs();
+                    }
+                    sa.cand = w.scand.p;
+                    sa.cand_cap = ccap;
+                    sa.ccount = w.counters.p + vdbk::kCtrCand;
+                    sa.ovf = w.ovf.p;
+                    sa.ublist = w.ublist.p;
+                    sa.ubcnt = w.ubcnt.p;
+                    sa.mstats = bounded_stats && !pass ? stats.p + 8 : nullptr;
+                    if (ev) HIPCHECK(hipEventRecord(ev->collect_begin, s));
+                    vdbk::launch_screen_collect(metric, grid, sa, s);
+                    if (ev) {
+                        HIPCHECK(hipEventRecord(ev->collect_end, s));
+                        ev->collected = true;
+                    }
+                    vdbk::launch_screen_select(sa, BP, w.scnt.p, w.soff.p, w.surv.p, w.ovf.p, s);
+                    if (!tier_file) break;
+                    uint32_t need = 0;
+                    fetched = fetch_survivor_rows(w, ccap, need, s);
+                    if (fetched) break;
+                    ccap = std::max<uint32_t>(need + need / 2, ccap + 1024);
+                    tier_cand_cap = ccap;  // (kept for the next batches)
+                    ++screen_reruns;
                 }
-                vdbk::launch_screen_select(sa, BP, w.scnt.p, w.soff.p, w.surv.p, w.ovf.p, s);
+                if (tiered()) ++screen_tier_batches;
                 vdbk::launch_screen_recheck(metric, sa, BP, w.probes.p, w.nseg_qp.p, w.soff.p, w.scnt.p, w.surv.p, w.ovf.p,
-                                            nullptr, w.sdist.p, ccap, s);
+                                            fetched, w.sdist.p, ccap, s);
             } else {
                 vdbk::launch_scan_screen(metric, grid, sa, s);
             }
@@ -2043,6 +2240,14 @@ struct vdb_ivf {
         tier_call_used = true;
     }
 
+    // The screen serves a search with this k (the tier: the deferred scan with its shadow
+    // resident; built lazily, so a stale screen is rebuilt first).
+    bool screen_serves(uint32_t k) {
+        if (screen_stale) screen_update();
+        return screen_ready && (!tiered() || screen_defer) && vdbk::topk_regs(k) == 1 && metric != 2 &&
+               vdbk::scan_screen_fits(k, dp, 16);
+    }
+
     uint32_t batch_cap(uint32_t P) const {
         return std::max<uint32_t>(1, std::min<uint32_t>(batch, vdbk::kPlanMaxPairs / P));
     }
@@ -2145,7 +2350,7 @@ struct vdb_ivf {
             end_call(w, s);
             return;
         }
-        if (tiered() && resident_n < storable_n) {  // (every stored list cached: the plain path)
+        if (tiered() && resident_n < storable_n && !screen_serves(k)) {  // (every stored list cached: the plain path)
             search_tiered(w, d_q, n, P, k, d_dist, d_ids, s, req_start);
             end_call(w, s);
             return;
@@ -2167,7 +2372,7 @@ struct vdb_ivf {
         slot_buf(w, w.xrec, vdb_rank_record_bytes(n, k));
         float* rd = rec_dist(w);
         uint64_t* ri = rec_ids(w, n, k);
-        if (tiered() && resident_n < storable_n) {
+        if (tiered() && resident_n < storable_n && !screen_serves(k)) {
             search_tiered(w, d_q, n, P, k, rd, ri, s, req_start);
             return;
         }

@@ -1074,14 +1074,16 @@ __device__ __forceinline__ float exact_dist(const float4* __restrict__ src, uint
 // Exact distances of the survivors (one 64-thread workgroup per kExactRows of them, in
 // their per-pair order): the rows are loaded into LDS together, kExactRows x 1 KiB
 // contiguous wave-loads per 256 dims, all in flight at once, from the row-major fp32 copy
-// of the lists (slot-indexed) or, in the tier, from the fetched rows ([survivor][dp]);
+// of the lists (SRC 0, slot-indexed), from rows fetched from the tier's file home (SRC 1,
+// [survivor][dp]), or from the interleaved arena in page-locked host memory (SRC 2, the
+// tier's host home, read over PCIe);
 // then one lane per row runs the reference's sequential sum over its LDS row (row stride
 // d4 + 1 float4: the lanes' rows fall on distinct banks) against its pair's query.
 constexpr int kExactRows = 16;
 constexpr int kExactChunks = 3;  // 64-float4 chunks of a row loaded per pass (768 dims)
 __host__ __device__ constexpr size_t exact_lds(uint32_t d4) { return ((size_t)kExactRows * (d4 + 1) + 64) * 16; }
 
-template <int M>
+template <int M, int SRC>
 __global__ __launch_bounds__(64) void ivf_screen_exact(ScanArgs a, const uint2* __restrict__ surv,
                                                        const float* __restrict__ fetched,
                                                        float* __restrict__ sdist) {
@@ -1089,7 +1091,7 @@ __global__ __launch_bounds__(64) void ivf_screen_exact(ScanArgs a, const uint2* 
     const int lane = lane_id();
     const uint32_t total = a.counters[kCtrSurv];
     const uint32_t d4 = a.d4, rs = d4 + 1;
-    const float4* src = fetched ? (const float4*)fetched : (const float4*)a.rows;
+    const float4* src = SRC == 1 ? (const float4*)fetched : SRC == 0 ? (const float4*)a.rows : a.arena;
     for (uint32_t base = blockIdx.x * kExactRows; base < total; base += gridDim.x * kExactRows) {
         const uint32_t ng = min((uint32_t)kExactRows, total - base);
         const uint2 my = lane < (int)ng ? surv[base + lane] : make_uint2(0u, 0u);
@@ -1100,9 +1102,12 @@ __global__ __launch_bounds__(64) void ivf_screen_exact(ScanArgs a, const uint2* 
 #pragma unroll
             for (int r = 0; r < kExactRows; ++r) {
                 const uint32_t rr = min((uint32_t)r, ng - 1);
-                const uint64_t row = fetched ? (uint64_t)(base + rr) : (uint64_t)__builtin_amdgcn_readlane(my.x, (int)rr);
+                const uint64_t row = SRC == 1 ? (uint64_t)(base + rr) : (uint64_t)__builtin_amdgcn_readlane(my.x, (int)rr);
 #pragma unroll
-                for (int c = 0; c < kExactChunks; ++c) v[r][c] = src[row * d4 + min(c0 + 64 * c + lane, d4 - 1)];
+                for (int c = 0; c < kExactChunks; ++c) {
+                    const uint32_t t = min(c0 + 64 * c + lane, d4 - 1);
+                    v[r][c] = SRC == 2 ? src[((row >> 6) * d4 + t) * 64 + (row & 63)] : src[row * d4 + t];
+                }
             }
 #pragma unroll
             for (int r = 0; r < kExactRows; ++r)
@@ -1158,8 +1163,9 @@ __global__ __launch_bounds__(256) void ivf_screen_pair_topk(ScanArgs a, const ui
                 const bool act = i < n;
                 float dist = __builtin_inff();
                 uint64_t id = kNoId;
-                if (act) {
-                    dist = exact_dist<M, true>((const float4*)a.rows, lbase + i, a.d4, qr);
+                if (act) {  // (the row-major copy, or the tier's host arena; a file home never overflows)
+                    dist = a.rows ? exact_dist<M, true>((const float4*)a.rows, lbase + i, a.d4, qr)
+                                  : exact_dist<M, false>(a.arena, lbase + i, a.d4, qr);
                     id = a.ids[lbase + i];
                 }
                 offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
@@ -1242,7 +1248,9 @@ void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uin
                            const float* fetched, float* sdist, uint32_t max_surv, hipStream_t s) {
     if (!BP) return;
     static const bool raised = [] {
-        for (const void* fn : {(const void*)ivf_screen_exact<kL2>, (const void*)ivf_screen_exact<kIP>})
+        for (const void* fn : {(const void*)ivf_screen_exact<kL2, 0>, (const void*)ivf_screen_exact<kIP, 0>,
+                               (const void*)ivf_screen_exact<kL2, 1>, (const void*)ivf_screen_exact<kIP, 1>,
+                               (const void*)ivf_screen_exact<kL2, 2>, (const void*)ivf_screen_exact<kIP, 2>})
             (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes / 2));
         (void)hipGetLastError();
         return true;
@@ -1251,13 +1259,16 @@ void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uin
     const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>(16384, (max_surv + kExactRows - 1) / kExactRows));
     const size_t lds = exact_lds(a.d4);
     const uint32_t gp = std::max<uint32_t>(1, std::min<uint32_t>(2048, (BP + 3) / 4));
-    if (metric == kL2) {
-        ivf_screen_exact<kL2><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
-        ivf_screen_pair_topk<kL2><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, sdist, ovf);
-    } else {
-        ivf_screen_exact<kIP><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
-        ivf_screen_pair_topk<kIP><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, sdist, ovf);
-    }
+    const int src = fetched ? 1 : (a.rows ? 0 : 2);
+    auto exact = [&](auto m_c) {
+        constexpr int Mm = decltype(m_c)::value;
+        if (src == 0) ivf_screen_exact<Mm, 0><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
+        else if (src == 1) ivf_screen_exact<Mm, 1><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
+        else ivf_screen_exact<Mm, 2><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
+        ivf_screen_pair_topk<Mm><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, sdist, ovf);
+    };
+    if (metric == kL2) exact(std::integral_constant<int, kL2>{});
+    else exact(std::integral_constant<int, kIP>{});
 }
 
 void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {

@@ -251,6 +251,15 @@ typedef struct vdb_ivf_cache_stats_t {
     uint64_t sync_loads;      /* sub-batches whose lists were loaded before their own scan */
     int32_t io_uring;         /* 1: the file home is read through io_uring (0: pread fallback) */
     int32_t o_direct;         /* 1: the file home is read with O_DIRECT */
+    /* The screen in the tier (L2 / IP, k <= 64): the lists' bf16 shadow, norms and ids stay in
+     * HBM and only the exact re-checks' rows are read from the home, per batch. */
+    int32_t screen_resident;      /* 1: the shadow of every stored list is HBM-resident */
+    int32_t reserved;
+    uint64_t screen_bytes;        /* HBM of the resident shadow, norms and ids */
+    uint64_t screen_batches;      /* batches the screen served in the tier */
+    uint64_t screen_rows_fetched; /* survivors' rows read from the file home (host home: read over PCIe) */
+    uint64_t screen_row_bytes;
+    uint64_t screen_reruns;       /* batches re-run after overflowing the candidate buffer */
 } vdb_ivf_cache_stats_t;
 int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
 /* The tier's home on disk (ListPrefetcher::register_list_file / prefetch_lists,

@@ -4,7 +4,10 @@ get_gpu_memory_usage: ivf_flat_index.cpp:387-471, 690-709). Lists live in page-l
 host memory and HBM caches whole lists; results must stay bit-identical to the oracle
 whatever the cache holds: with evictions, batches split because their probed lists
 overflow the cache, fragmented caches repacked, empty lists (stale slots), the tier
-switched on before or after add, and switched off again."""
+switched on before or after add, and switched off again. These cases exercise the
+list-cache path itself, so the screen is off here (option "screen" 0): with it, L2 / IP
+searches with k <= 64 keep the lists' shadow in HBM and never load lists into the cache
+(the screened tier: test_gpu_screen_tier.py)."""
 import numpy as np
 import pytest
 
@@ -31,6 +34,7 @@ def fixture():
 
 def make(o, X, ids, cache_bytes, before_add):
     g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST))
+    g.set_option("screen", 0)
     g.centroids = o.centroids
     if before_add:
         g.set_option("list_cache_bytes", cache_bytes)
@@ -138,6 +142,7 @@ def test_lists_served_from_file(tmp_path, dim):
     g.save(path)
     del g
     h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    h.set_option("screen", 0)
     dp = 128 if dim > 64 else 64
     blocks = np.array([(o.list_count(l) + 63) // 64 for l in range(NLIST)])
     need = max(int(blocks[o.select_nprobe(q, NPROBE)].sum()) for q in Q)
@@ -174,6 +179,7 @@ def test_tier_pipeline_file_home_next_use_and_prefetch(tmp_path):
     g.save(path)
     del g
     h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST))
+    h.set_option("screen", 0)
     h.set_option("list_cache_bytes", (3 * need + 8) * BLOCK_BYTES)   # room for ~3 queries' lists at once
     h.open_lists(path)
     Dr, Ir = o.search(Q, NPROBE, K)

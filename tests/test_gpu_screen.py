@@ -182,7 +182,8 @@ def test_screen_rebuilt_after_incremental_adds_and_under_the_cap():
         assert p["bounded_blocks"] > 0, p
     # a residency cap that holds the lists: it counts list bytes only (the reference's
     # gpu_memory_used_), so the screen stays; a cap below them moves the lists to the tier
-    # (the screen is not built there), raising it again brings them back with the screen
+    # (the screen serves there with its shadow resident and the rows at home), lifting it
+    # brings them back
     g.set_option("max_gpu_memory", int(20000 * (64 * 4 + 8) * 1.2))
     D, I, p = screen_stats(g, Q, nprobe, k, 64)
     assert_same(D, I, *o.search(Q, nprobe, k))
@@ -190,7 +191,8 @@ def test_screen_rebuilt_after_incremental_adds_and_under_the_cap():
     g.set_option("max_gpu_memory", int(20000 * (64 * 4 + 8) * 0.6))
     D, I, p = screen_stats(g, Q, nprobe, k, 64)
     assert_same(D, I, *o.search(Q, nprobe, k))
-    assert p["bounded_blocks"] == 0 and g.cache_stats()["capacity_bytes"] > 0, p
+    st = g.cache_stats()
+    assert p["bounded_blocks"] > 0 and st["capacity_bytes"] > 0 and st["screen_resident"] == 1, (p, st)
     g.set_option("max_gpu_memory", 0)
     assert g.cache_stats()["capacity_bytes"] == 0
     D, I, p = screen_stats(g, Q, nprobe, k, 64)

@@ -1,0 +1,169 @@
+"""GPU: the screened scan inside the list-cache tier (configs[4]'s shape: a shard larger than
+HBM). The lists' bf16 shadow, norms and ids stay HBM-resident; the fp32 rows stay at the
+home and only the exact re-checks' rows are read per batch: from page-locked host memory over
+PCIe, or from the index file (io_uring, one read per survivor row). Exact-path searches
+(k > 64) on the same handle go through the list cache, under eviction. Every result is
+compared bit for bit with the oracle (ivf_flat_index.cpp:205-256 restated); the residency
+model is the reference's load_list_to_gpu / evict_list_from_gpu (ivf_flat_index.cpp:387-471)
+and its list streaming design (engine/prefetcher.h:139-183).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import load_vdb
+from test_gpu_parity import assert_same
+
+vdb = load_vdb()
+pytestmark = pytest.mark.gpu
+
+NLIST, NPROBE = 64, 8
+
+
+def data(dim, metric=0, n=20000, nq=300, seed=5):
+    X, Q, ids = oracle.reference_test_data(n, nq, dim, seed=seed)
+    o = oracle.OracleIndex(dim, NLIST, metric)
+    o.train(X[:5000])
+    o.add(X, ids)
+    return X, Q, ids, o
+
+
+def block_bytes(dim):
+    dp = -(-dim // 64) * 64
+    return 64 * (dp * 4 + 8)
+
+
+def need_blocks(o, Q, nprobe):
+    blocks = np.array([(o.list_count(l) + 63) // 64 for l in range(NLIST)])
+    return max(int(blocks[o.select_nprobe(q, nprobe)].sum()) for q in Q)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_screened_tier_host_home_mixed_k(metric):
+    """Lists homed in page-locked host memory (the tier entered by list_cache_bytes): k <= 64
+    is served by the resident shadow with the survivors' rows read over PCIe, k > 64 by the
+    list cache under eviction, interleaved on one handle."""
+    dim = 64
+    X, Q, ids, o = data(dim, metric)
+    nprobe = NPROBE if metric == 0 else 2 * NPROBE
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST, vdb.Metric(metric), max_gpu_memory=0))
+    g.centroids = o.centroids
+    g.add(X, ids)
+    g.set_option("list_cache_bytes", (need_blocks(o, Q, nprobe) + 8) * block_bytes(dim))
+    for k in (10, 1, 64, 100, 10, 65, 16):
+        Dr, Ir = o.search(Q, nprobe, k)
+        for batch in (256, 17):
+            g.set_batch(batch)
+            assert_same(*g.search(Q, nprobe=nprobe, k=k), Dr, Ir)
+    st = g.cache_stats()
+    assert st["screen_resident"] == 1 and st["screen_batches"] > 0, st
+    assert st["evictions"] > 0, st  # (the k > 64 searches)
+    # shadow 2 dp + norms 16 + ids 8 bytes per vector (plus block padding): well below the lists
+    assert st["screen_bytes"] < 0.7 * len(X) * (dim * 4 + 8), st
+
+
+@pytest.mark.parametrize("dim", [64, 70])
+def test_screened_tier_file_home(tmp_path, dim):
+    """Lists served from an index file: the shadow is built by streaming the file once;
+    per batch only the survivors' rows are read (far fewer bytes than the probed lists).
+    dim 70 pads the fetched rows to 128."""
+    X, Q, ids, o = data(dim, seed=9)
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    g.centroids = o.centroids
+    g.add(X, ids)
+    path = str(tmp_path / "index.vdb")
+    g.save(path)
+    del g
+    h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    h.set_option("list_cache_bytes", (need_blocks(o, Q, NPROBE) + 8) * block_bytes(dim))
+    h.open_lists(path)
+    Dr, Ir = o.search(Q, NPROBE, 10)
+    for batch in (256, 5):
+        h.set_batch(batch)
+        assert_same(*h.search(Q, nprobe=NPROBE, k=10), Dr, Ir)
+    st = h.cache_stats()
+    assert st["screen_resident"] == 1 and st["loads"] == 0, st
+    assert 0 < st["screen_rows_fetched"] and st["screen_row_bytes"] == st["screen_rows_fetched"] * dim * 4, st
+    probed = sum(o.list_count(l) for q in Q for l in o.select_nprobe(q, NPROBE))
+    assert st["screen_rows_fetched"] < 0.1 * probed * 2, st  # (two passes above)
+    # k > 64 on the same handle: the list cache, under eviction
+    Dr, Ir = o.search(Q, NPROBE, 80)
+    assert_same(*h.search(Q, nprobe=NPROBE, k=80), Dr, Ir)
+    assert h.cache_stats()["evictions"] > 0
+    # and back to the screen
+    assert_same(*h.search(Q, nprobe=NPROBE, k=10), *o.search(Q, NPROBE, 10))
+
+
+def test_screened_tier_file_home_overflow_reruns(tmp_path):
+    """A candidate buffer too small for a batch: the file home cannot recompute a pair over
+    its whole list on the device, so the batch is re-run with a larger buffer."""
+    dim = 64
+    X, Q, ids, o = data(dim, seed=3)
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    g.centroids = o.centroids
+    g.add(X, ids)
+    path = str(tmp_path / "index.vdb")
+    g.save(path)
+    del g
+    h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    h.set_option("list_cache_bytes", (need_blocks(o, Q, NPROBE) + 8) * block_bytes(dim))
+    h.open_lists(path)
+    h.set_option("screen_cand_cap", 1024)
+    h.set_batch(256)
+    assert_same(*h.search(Q, nprobe=NPROBE, k=10), *o.search(Q, NPROBE, 10))
+    assert h.cache_stats()["screen_reruns"] > 0
+
+
+def test_screened_tier_empty_lists_stale_slots(tmp_path):
+    """Reference quirk A1 (an empty probed list keeps the previous query's slot) through the
+    screened tier, host and file homes, across batch boundaries."""
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((3000, 64)).astype(np.float32)
+    Q = rng.standard_normal((300, 64)).astype(np.float32)
+    ids = np.arange(3000, dtype=np.uint64)
+    C = np.concatenate([X[:10], 6.0 + rng.standard_normal((6, 64)).astype(np.float32) * 0.1])
+    C[10:] *= np.where(rng.random((6, 1)) < 0.5, -1, 1).astype(np.float32)
+    o = oracle.OracleIndex(64, 16, 0)
+    o.centroids = C
+    o.add(X, ids)
+    assert any(o.list_count(l) == 0 for l in range(16))
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(64, 16))
+    g.centroids = C
+    g.add(X, ids)
+    g.set_option("list_cache_bytes", 8 * block_bytes(64))
+    Dr, Ir = o.search(Q, 12, 8)
+    for batch in (256, 7):
+        g.set_batch(batch)
+        assert_same(*g.search(Q, nprobe=12, k=8), Dr, Ir)
+    path = str(tmp_path / "stale.vdb")
+    g.save(path)
+    h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(64, 16))
+    h.set_option("list_cache_bytes", 8 * block_bytes(64))
+    h.open_lists(path)
+    for batch in (256, 7):
+        h.set_batch(batch)
+        assert_same(*h.search(Q, nprobe=12, k=8), Dr, Ir)
+    assert h.cache_stats()["screen_batches"] > 0
+
+
+def test_screened_tier_attach_comm_world1_file_home(tmp_path):
+    """A file-home screened tier with an attached communicator (world 1): per-call exchange."""
+    dim = 64
+    X, Q, ids, o = data(dim, seed=21)
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    g.centroids = o.centroids
+    g.add(X, ids)
+    path = str(tmp_path / "index.vdb")
+    g.save(path)
+    del g
+    h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    h.set_option("list_cache_bytes", (need_blocks(o, Q, NPROBE) + 8) * block_bytes(dim))
+    h.open_lists(path)
+    h.attach_comm(vdb.comm_unique_id(), 0, 1)
+    for batch in (256, 33):
+        h.set_batch(batch)
+        assert_same(*h.search(Q, nprobe=NPROBE, k=10), *o.search(Q, NPROBE, 10))
+    assert_same(*h.search(Q, nprobe=NPROBE, k=70), *o.search(Q, NPROBE, 70))  # the list cache
+    st = h.cache_stats()
+    assert st["screen_batches"] > 0 and st["evictions"] > 0, st
+    h.detach_comm()

@@ -37,7 +37,20 @@ def fixture():
     return X, Q, ids, o, blocks, need
 
 
-def test_tier_with_attached_communicator_under_eviction():
+def check_tier_stats(g, screen, o, Q, exact_k=100):
+    """With the screen, k <= 64 searches keep the shadow resident and load no list; a k > 64
+    search on the same handle then runs the list-cache path under eviction. Without it, the
+    searches above already split into sub-batches and evicted."""
+    st = g.cache_stats()
+    if screen:
+        assert st["screen_resident"] == 1 and st["screen_batches"] > 0 and st["loads"] == 0, st
+        assert_same(*g.search(Q, nprobe=NPROBE, k=exact_k), *o.search(Q, NPROBE, exact_k))
+        st = g.cache_stats()
+    assert st["evictions"] > 0 and st["subbatches"] > 1, st
+
+
+@pytest.mark.parametrize("screen", [1, 0], ids=["screened", "list-cache"])
+def test_tier_with_attached_communicator_under_eviction(screen):
     """A tiered handle with an RCCL communicator (world 1): each call's partials go into one
     record, ONE all-gather per call, the merge; results equal the oracle whatever the cache
     holds. The tier may be switched on before or after attach_comm."""
@@ -45,6 +58,7 @@ def test_tier_with_attached_communicator_under_eviction():
     X, Q, ids, o, blocks, need = fixture()
     Dr, Ir = o.search(Q, NPROBE, K)
     g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST, max_gpu_memory=0))
+    g.set_option("screen", screen)
     g.centroids = o.centroids
     g.add(X, ids)
     g.set_option("list_cache_bytes", (need + 8) * BLOCK_BYTES)  # before attach
@@ -52,8 +66,7 @@ def test_tier_with_attached_communicator_under_eviction():
     for batch in (256, 16, 1):
         g.set_batch(batch)
         assert_same(*g.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
-    st = g.cache_stats()
-    assert st["evictions"] > 0 and st["subbatches"] > 1, st
+    check_tier_stats(g, screen, o, Q)
     import time
     t0 = time.time()
     while True:  # (the watchdog polls completions: its count may trail the host by a moment)
@@ -99,8 +112,9 @@ def test_tiered_shard_with_communicator_every_list_cached():
     assert g.cache_stats()["subbatches"] == 0  # everything cached: no tier sub-batches
 
 
+@pytest.mark.parametrize("screen", [1, 0], ids=["screened", "list-cache"])
 @pytest.mark.parametrize("stale", [False, True])
-def test_tiered_group_two_members_one_device_under_eviction(stale):
+def test_tiered_group_two_members_one_device_under_eviction(stale, screen):
     """A 2-member group on one device whose members serve their lists through their own
     list caches: one record per member for the whole call, one exchange, the merge."""
     if stale:  # empty probed lists (reference quirk A1) across sub-batches and members
@@ -122,6 +136,7 @@ def test_tiered_group_two_members_one_device_under_eviction(stale):
         C = o.centroids
         cap = (need + 8) * BLOCK_BYTES
     g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, max_gpu_memory=0, devices=(0, 0)))
+    g.set_option("screen", screen)
     g.centroids = C
     g.add(X, ids)
     g.set_option("list_cache_bytes", cap)  # per member
@@ -130,13 +145,18 @@ def test_tiered_group_two_members_one_device_under_eviction(stale):
         g.set_batch(batch)
         assert_same(*g.search(Q, nprobe=nprobe, k=k), Dr, Ir)
     st = g.cache_stats()  # summed over the members
+    if screen:  # the shadow of both members resident, no list loaded; k > 64: the list caches
+        assert st["screen_resident"] == 1 and st["screen_batches"] > 0 and st["loads"] == 0, st
+        assert_same(*g.search(Q, nprobe=nprobe, k=100), *o.search(Q, nprobe, 100))
+        st = g.cache_stats()
     assert st["capacity_bytes"] > 0 and st["loads"] > 0 and st["subbatches"] > 0, st
     g.warmup_lists([0, 1])
     g.evict_list(0)
     assert_same(*g.search(Q, nprobe=nprobe, k=k), Dr, Ir)
 
 
-def test_shard_files_served_per_rank(tmp_path):
+@pytest.mark.parametrize("screen", [1, 0], ids=["screened", "list-cache"])
+def test_shard_files_served_per_rank(tmp_path, screen):
     """configs[4]'s deployment on one GPU: each rank of an LPT shard plan saves a SHARD
     file (every list's count, only its own lists' rows); a fresh handle serves that file
     through its cache and becomes that rank's shard (rank and world from the file). Each
@@ -163,6 +183,7 @@ def test_shard_files_served_per_rank(tmp_path):
         Dp, Ip = g.search(Q, nprobe=NPROBE, k=K)
         del g
         h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST, max_gpu_memory=0))
+        h.set_option("screen", screen)
         h.set_option("list_cache_bytes", (need + 8) * BLOCK_BYTES)
         h.open_lists(path)
         owners = h.list_owners()
@@ -172,7 +193,11 @@ def test_shard_files_served_per_rank(tmp_path):
         Dh, Ih = h.search(Q, nprobe=NPROBE, k=K)
         assert_same(Dh, Ih, Dp, Ip)
         assert_same(Dh, Ih, *o.search_shard(Q, NPROBE, K, owned.astype(np.uint8)))
-        assert h.cache_stats()["file_bytes_read"] > 0
+        st = h.cache_stats()
+        assert st["file_bytes_read"] > 0
+        if screen:  # the file streamed once (the shadow), then only the survivors' rows
+            assert st["screen_rows_fetched"] > 0 and st["loads"] == 0, st
+            assert st["screen_row_bytes"] < 0.25 * int(sizes[owned].sum()) * D * 4, st
         with pytest.raises(vdb.VdbError):
             h.set_shard((r + 1) % world, world)  # the file holds only this rank's lists
         s = torch.cuda.Stream(dev)
@@ -191,7 +216,8 @@ def test_shard_files_served_per_rank(tmp_path):
     assert_same(od.cpu().numpy(), oi.cpu().numpy().view(np.uint64), *o.search(Q, NPROBE, K))
 
 
-def test_max_gpu_memory_caps_list_residency():
+@pytest.mark.parametrize("screen", [1, 0], ids=["screened", "list-cache"])
+def test_max_gpu_memory_caps_list_residency(screen):
     """Config::max_gpu_memory (the reference's cap on resident list bytes): an index that
     outgrows it is served through the list-cache tier with an HBM cache of that size,
     results unchanged; 0 = no cap; a cap below one query's lists fails the search with
@@ -201,6 +227,7 @@ def test_max_gpu_memory_caps_list_residency():
     cap = (2 * need + 8) * BLOCK_BYTES
     assert cap < len(X) * (D * 4 + 8)
     g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST, max_gpu_memory=cap))
+    g.set_option("screen", screen)
     g.centroids = o.centroids
     g.add(X[:100], ids[:100])
     assert g.cache_stats()["capacity_bytes"] == 0  # still under the cap: every list in HBM
@@ -210,7 +237,11 @@ def test_max_gpu_memory_caps_list_residency():
     # (the footprint also counts the search workspaces: a small allowance)
     assert g.gpu_bytes_allocated() <= cap + (NLIST * 64 * 4 * 2) + BLOCK_BYTES + (1 << 20)
     assert_same(*g.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
-    assert g.cache_stats()["evictions"] > 0
+    check_tier_stats(g, screen, o, Q)
+    # the cap lifted: the lists return to HBM
+    g.set_option("max_gpu_memory", 0)
+    assert g.cache_stats()["capacity_bytes"] == 0
+    assert_same(*g.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
     # no cap
     h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST, max_gpu_memory=0))
     h.centroids = o.centroids
@@ -218,14 +249,21 @@ def test_max_gpu_memory_caps_list_residency():
     assert h.cache_stats()["capacity_bytes"] == 0
     # a cap below one query's lists
     t = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(D, NLIST, max_gpu_memory=max(need // 2, 1) * BLOCK_BYTES))
+    t.set_option("screen", screen)
     t.centroids = o.centroids
     t.add(X, ids)
+    if screen:  # the screened tier loads no list: the small cache does not matter for k <= 64
+        assert_same(*t.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
     with pytest.raises(vdb.VdbError) as ei:
-        t.search(Q, nprobe=NPROBE, k=K)
+        t.search(Q, nprobe=NPROBE, k=100 if screen else K)
     assert ei.value.code == -3
     # the option form applies at once
     h.set_option("max_gpu_memory", cap)
     assert h.cache_stats()["capacity_bytes"] == (cap // BLOCK_BYTES) * BLOCK_BYTES
+    assert_same(*h.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
+    # the cap raised above the lists: back to HBM
+    h.set_option("max_gpu_memory", 10 * len(X) * (D * 4 + 8))
+    assert h.cache_stats()["capacity_bytes"] == 0
     assert_same(*h.search(Q, nprobe=NPROBE, k=K), Dr, Ir)
 
 
