@@ -592,10 +592,13 @@ def main():
     ap.add_argument("--host-threads", type=int, default=8)
     ap.add_argument("--host-calls", type=int, default=400, help="host-API calls of --batch queries each")
     ap.add_argument("--host-coalesce", type=int, default=64, help="max queries per coalesced device batch")
+    ap.add_argument("--asg-file", default="", help=argparse.SUPPRESS)  # (a child of --emulate-rank all)
+    ap.add_argument("--ranks-in-process", action="store_true",
+                    help="--emulate-rank all in this one process (round 3's form) instead of a process per rank")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="engine tuning knob (vdb_ivf_set_option), e.g. wide_stride=1; results never change")
     args = ap.parse_args()
-    if args.emulate_rank == "all":
+    if args.emulate_rank in ("all", "assign") or args.asg_file:
         args.sharded_build = True  # every rank's shard from one assignment pass
         args.emulate_shard = args.emulate_shard or 8
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -606,6 +609,10 @@ def main():
         args.nvec, args.nlist, args.nprobe = {"cfg2": (1_000_000, 256, 16), "cfg3": (10_000_000, 4096, 32),
                                               "cfg4": (100_000_000, 16384, 64)}[args.cfg]
         args.sharded_build |= args.cfg == "cfg4"
+    if args.emulate_rank == "all" and not args.ranks_in_process:
+        if args.inflight <= 0:
+            args.inflight = 3
+        sys.exit(run_emulated_ranks_procs(args))  # (before anything touches the GPU)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.inflight <= 0:
@@ -821,6 +828,112 @@ def make_queries(vdb, args, device):
     return queries, out_d, out_i
 
 
+def child_argv(rank_arg, asg_file):
+    """This command line with --emulate-rank replaced (a child of the emulated-ranks run)."""
+    out, skip = [], False
+    for a in sys.argv[1:]:
+        if skip:
+            skip = False
+            continue
+        if a == "--emulate-rank":
+            skip = True
+            continue
+        if a.startswith("--emulate-rank="):
+            continue
+        out.append(a)
+    return [sys.executable, "-u", os.path.abspath(__file__)] + out + ["--emulate-rank", rank_arg, "--asg-file", asg_file]
+
+
+def child_argv_inflight(args, rank_arg, asg_file):
+    return child_argv(rank_arg, asg_file) + ["--inflight", str(args.inflight)]
+
+
+def run_emulated_ranks_procs(args):
+    """--emulate-rank all: every rank of a W-GPU node in a process of its own, one after
+    the other on this one GPU, as on a real node (one process per GPU): a first child runs
+    the assignment pass and writes the centroids, the assignment and the list sizes to a
+    file; child r builds rank r's LPT shard from it and times it. A fresh process per rank
+    keeps one rank's streams, allocations and code objects from shaping the next rank's
+    timing (round 3 timed the ranks in one process: even ranks stepped 1.4x slower than
+    odd ones at equal scan times). The parent never touches the GPU."""
+    import subprocess
+    import tempfile
+    W = args.emulate_shard
+    f = os.path.join(args.tier_dir or tempfile.gettempdir(), f"vdb_asg_{os.getpid()}.npz")
+    ranks, info = [], {}
+    try:
+        r = subprocess.run(child_argv_inflight(args, "assign", f), stdout=subprocess.PIPE, text=True)
+        sys.stdout.write("".join(l + "\n" for l in r.stdout.splitlines() if not l.startswith("ASSIGN ")))
+        if r.returncode != 0:
+            return r.returncode
+        info = json.loads([l for l in r.stdout.splitlines() if l.startswith("ASSIGN ")][-1][7:])
+        for rk in range(W):
+            r = subprocess.run(child_argv_inflight(args, str(rk), f), stdout=subprocess.PIPE, text=True)
+            rows = [l for l in r.stdout.splitlines() if l.startswith("RANKROW ")]
+            if r.returncode != 0 or not rows:
+                sys.stdout.write(r.stdout)
+                return r.returncode or 1
+            ranks.append(json.loads(rows[-1][8:]))
+            log(0, f"[bench] emulated rank {rk}/{W}: " + rows[-1][8:])
+        with np.load(f) as z:
+            sizes = z["sizes"]
+    finally:
+        if os.path.exists(f):
+            os.unlink(f)
+    plan = vdb_plan_host(args, sizes, W)
+    lists = [int((plan == r).sum()) for r in range(W)]
+    vecs = [int(sizes[plan == r].sum()) for r in range(W)]
+    print(json.dumps({
+        "metric": f"per-rank balance of the {W}-GPU LPT shard plan (emulated on one GPU)",
+        "unit": "ms", "n_gpus": 1, "emulated_ranks": W, "steps": args.steps, "warmup": args.warmup,
+        "config": {"workload": f"{args.nvec // 1_000_000}M x {args.dim}D IVF-Flat L2, nlist {args.nlist}, "
+                               f"nprobe {args.nprobe}, batch {args.batch}, k {args.k}",
+                   "inflight": args.inflight, "data": args.data},
+        "plan": args.plan, "ranks": ranks, "balance": balance(ranks),
+        "shard_lists": lists, "shard_vectors": vecs,
+        "predicted_8gpu_qps_from_max_rank_step": round(args.batch * 1e3 / max(r["ms_per_step"] for r in ranks), 1),
+        "build": info, "process_per_rank": True,
+        "note": "partial (per-rank) results; exchange excluded; each rank's search timed alone, in its own process",
+    }), flush=True)
+    return 0
+
+
+def vdb_plan_host(args, sizes, W):
+    """The LPT owner of every list (host only; no GPU)."""
+    vdb = load_vdb()
+    return vdb.shard_plan(sizes, W)
+
+
+def emulated_assign(vdb, args, device):
+    """The assignment child of --emulate-rank all: pass 1 of the sharded build, saved."""
+    trained, asg, sizes, info = sharded_assign(vdb, args, device, 0)
+    np.savez(args.asg_file, centroids=trained.centroids, asg=asg.cpu().numpy(), sizes=sizes)
+    trained.close()
+    print("ASSIGN " + json.dumps(info), flush=True)
+
+
+def emulated_rank(vdb, args, device, r):
+    """Rank r's child of --emulate-rank all: its LPT shard from the saved assignment, timed."""
+    W = args.emulate_shard
+    with np.load(args.asg_file) as z:
+        centroids, asg, sizes = z["centroids"], torch.from_numpy(z["asg"]).to(device), z["sizes"]
+    queries, out_d, out_i = make_queries(vdb, args, device)
+    idx = new_index(vdb, args, device)
+    idx.centroids = centroids
+    binfo = sharded_append(vdb, args, device, idx, asg, sizes, r, W)
+    del asg
+    torch.cuda.empty_cache()
+    for o in args.opt:
+        name, val = o.split("=", 1)
+        idx.set_option(name, int(val))
+    res = timed_region(vdb, idx, args, device, 0, 1, queries, out_d, out_i)
+    row = dict(res["mine"], rank=r, qps=round(args.steps * args.batch / res["elapsed"], 1),
+               p99_ms=round(res["p99"], 4), latency_mean_ms=round(res["lat_mean"], 4),
+               p99_ms_one_in_flight=round(res["p99_single"], 4),
+               shard_gib=round(idx.gpu_bytes_allocated() / 2**30, 2), append_s=binfo["append_s"])
+    print("RANKROW " + json.dumps(row), flush=True)
+
+
 def run_emulated_ranks(vdb, args, device):
     """--emulate-rank all: the per-GPU work of every rank of a W-GPU node, timed in turn on
     this one GPU. One sharded-build assignment pass; then for each rank r a fresh index
@@ -872,9 +985,15 @@ def run(vdb, args, device, rank, world):
     if args.data == "mixture":
         args.centers = mixture_centers(vdb, args.mix_components or args.nlist, args.mix_group or args.nprobe,
                                        args.dim, args.mix_spread, device)
-    if args.emulate_rank == "all":
+    if args.emulate_rank == "all":  # (--ranks-in-process: the round-3 form, every rank in this process)
         line = run_emulated_ranks(vdb, args, device)
         print(json.dumps(line), flush=True)
+        return
+    if args.emulate_rank == "assign":
+        emulated_assign(vdb, args, device)
+        return
+    if args.asg_file:
+        emulated_rank(vdb, args, device, int(args.emulate_rank))
         return
     er = int(args.emulate_rank)
     if args.sharded_build:

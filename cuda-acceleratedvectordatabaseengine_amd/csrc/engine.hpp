@@ -337,6 +337,10 @@ struct vdb_ivf {
     DevBuf<uint64_t> d_sblock_off;
     DevBuf<uint64_t> screen_ids;       // tier: the ids in shadow slot order
     DevBuf<float> fetch_stage;         // tier, file home: page-locked staging of the survivors' rows
+    DevBuf<char> fetch_bounce;         // ... O_DIRECT reads: 4 KiB-aligned supersets, one slot per read in flight
+    bool tier_row_direct = true;       // option tier_row_direct: survivor rows with O_DIRECT (no page cache)
+    static constexpr uint32_t kRowQD = 256;  // survivor-row reads in flight (their own ring)
+    std::unique_ptr<UringReader> row_uring;
     DevBuf<float> fetch_dev;           // ... on the device ([n][dim], padded into the slot's srows)
     std::vector<uint2> fetch_surv;     // ... their (slot, pair)
     uint64_t screen_rows_fetched = 0, screen_row_bytes = 0, screen_tier_batches = 0, screen_reruns = 0;
@@ -999,34 +1003,69 @@ struct vdb_ivf {
         HIPCHECK(hipStreamSynchronize(s));
         fetch_stage.host = true;
         float* st = fetch_stage.ensure((size_t)std::max<uint32_t>(n, 1) * dim);
-        if (!uring) uring.reset(new UringReader(64));
+        if (!row_uring) row_uring.reset(new UringReader(kRowQD));
+        UringReader* const ur = row_uring.get();
         const uint64_t row_bytes = (uint64_t)dim * 4;
+        // O_DIRECT (where the file system allows it): each read is the 4 KiB-aligned superset
+        // of the row into a bounce slot, copied out on completion; else a buffered read
+        // straight into the staging
+        const bool direct = tier_row_direct && home_fd_direct >= 0;
+        constexpr uint32_t kQD = kRowQD;
+        const uint64_t span = ((row_bytes + 4095) / 4096 + 1) * 4096;
+        char* bounce = nullptr;
+        if (direct) {
+            fetch_bounce.host = true;
+            bounce = fetch_bounce.ensure(kQD * span + 4096);
+            bounce = (char*)(((uintptr_t)bounce + 4095) & ~(uintptr_t)4095);
+        }
+        std::vector<uint32_t> slot_of(kQD), free_slots(kQD);
+        for (uint32_t i = 0; i < kQD; ++i) free_slots[i] = kQD - 1 - i;
+        std::vector<uint64_t> delta(kQD);
+        uint64_t bytes_read = 0;
         uint32_t next = 0, done = 0;
         try {
             while (done < n) {
-                while (next < n && next - done < std::min(uring->capacity(), 64u)) {  // (<= 64 queued or in flight)
+                while (next < n && next - done < std::min(ur->capacity(), kQD)) {  // (<= kQD queued or in flight)
                     const uint64_t slot = fetch_surv[next].x;
                     const uint32_t l = sblist_host[slot >> 6];
                     const uint64_t r = slot - sblock_off[l] * 64;
-                    uring->read(home_fd, st + (size_t)next * dim, (uint32_t)row_bytes,
-                                file_off[l] + count[l] * 8 + r * row_bytes, next);
+                    const uint64_t off = file_off[l] + count[l] * 8 + r * row_bytes;
+                    if (direct) {
+                        const uint32_t b = free_slots.back();
+                        free_slots.pop_back();
+                        const uint64_t a0 = off & ~4095ull, a1 = (off + row_bytes + 4095) & ~4095ull;
+                        delta[b] = off - a0;
+                        slot_of[b] = next;
+                        ur->read(home_fd_direct, bounce + (size_t)b * span, (uint32_t)(a1 - a0), a0,
+                                 ((uint64_t)b << 32) | next);
+                        bytes_read += a1 - a0;
+                    } else {
+                        ur->read(home_fd, st + (size_t)next * dim, (uint32_t)row_bytes, off, next);
+                        bytes_read += row_bytes;
+                    }
                     ++next;
                 }
-                for (const UringReader::Done& d : uring->wait(1)) {
-                    require(d.result == (int64_t)row_bytes,
+                for (const UringReader::Done& d : ur->wait(1)) {
+                    const uint32_t b = (uint32_t)(d.tag >> 32), i = (uint32_t)d.tag;
+                    const int64_t want = direct ? (int64_t)(delta[b] + row_bytes) : (int64_t)row_bytes;
+                    require(d.result >= want,
                             "short read of a survivor row from the list file" +
                                 (d.result < 0 ? std::string(": ") + std::strerror((int)-d.result) : ""),
                             VDB_ERR_STATE);
+                    if (direct) {
+                        std::memcpy(st + (size_t)i * dim, bounce + (size_t)b * span + delta[b], row_bytes);
+                        free_slots.push_back(b);
+                    }
                     ++done;
                 }
             }
         } catch (...) {
-            uring->drain();
+            ur->drain();
             throw;
         }
         screen_rows_fetched += n;
         screen_row_bytes += (uint64_t)n * row_bytes;
-        file_bytes_read += (uint64_t)n * row_bytes;
+        file_bytes_read += bytes_read;  // (with O_DIRECT: the aligned supersets the device delivered)
         float* rows = slot_buf(w, w.srows, (size_t)std::max<uint32_t>(n, 1) * dp);
         if (n) {
             if (dim == dp) {
@@ -1930,8 +1969,9 @@ struct vdb_ivf {
         // and narrow items
         if (screen_stale) screen_update();
         // 32-query items (option screen_group) where their shared lists fit the LDS
-        // (the deferred kernel's items hold at most 16 queries)
-        const uint32_t swq = !screen_defer && screen_group == 32 && vdbk::scan_screen_fits(k, dp, 32) ? 32u : 16u;
+        // 32-query items (option screen_group): the deferred kernel feeds each shadow tile to two
+        // A operands; the inline kernel splits its waves in two halves
+        const uint32_t swq = screen_group == 32 && (screen_defer || vdbk::scan_screen_fits(k, dp, 32)) ? 32u : 16u;
         const bool screened = screen_ready && (!tiered() || screen_defer) && regs_k == 1 && metric != 2 &&
                               vdbk::scan_screen_fits(k, dp, swq);
         if (!screened && arena_dropped) ensure_arena();  // (the exact scans read the arena)

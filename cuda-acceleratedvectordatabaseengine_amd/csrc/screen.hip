@@ -684,11 +684,14 @@ __device__ __forceinline__ float row_elem(const float (&u)[4], int e) {
     return __shfl(x, (lane_id() & ~15) + (e >> 2));
 }
 
-// One wave: collect the candidates of segment `seg` of list it.list for the nq (<= 16)
-// queries of the item starting at sorted pair it.pair_start + q0. rl: the wave's running
-// lists of upper bounds (4 query rows; reset by the caller per item); s_thr: the item's
-// shared k-th (LDS); residue: the wave's quarter slot (0..3, distinct per wave of an item).
-template <int M, int KD>
+// One wave: collect the candidates of segment `seg` of list it.list for the nq (<= 16 NG)
+// queries of the item starting at sorted pair it.pair_start + q0. NG = 2 (items of 17-32
+// queries): every shadow B tile the wave loads feeds two A operands (queries 0-15 and
+// 16-31: 8 MFMAs per k-step), so a list is streamed once per 32 queries, not per 16.
+// rl_lds: the wave's running lists of upper bounds (NG x 4 query rows; reset by the caller
+// per item); s_thr: the item's shared k-th (LDS); residue: the wave's quarter slot (0..3,
+// distinct per wave of an item).
+template <int M, int KD, int NG>
 __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
                                                 const uint32_t seg, float4* rl_lds, uint32_t* s_thr,
                                                 const uint32_t residue) {
@@ -709,127 +712,141 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
         const uint32_t pr = pairs[g];
         return (pr >> 16) * a.P + (pr & 0xFFFFu);
     };
-    const int ga = min(lane & 15, nq - 1);
-    const uint4* qa_row = (const uint4*)(a.qres + (size_t)pair_of(ga) * dp) + (lane >> 4);
-    const float4* pst_r[4];
+    // the MFMA A rows of this lane: query 16 gg + (lane & 15) of group gg, its dims 8 (lane >> 4) ..
+    const uint4* qa_row[NG];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) pst_r[r] = a.pst + pair_of(min(4 * (lane >> 4) + r, nq - 1));
+    for (int gg = 0; gg < NG; ++gg)
+        qa_row[gg] = (const uint4*)(a.qres + (size_t)pair_of(min(16 * gg + (lane & 15), nq - 1)) * dp) + (lane >> 4);
     uint32_t collected = 0;
 
     const uint4* sp = a.shadow + b0 * (uint64_t)dp * 8 + lane;
-    uint4 xa[KD][4], qa[KD];
+    uint4 xa[KD][4], qa[NG][KD];
 #pragma unroll
     for (int u = 0; u < KD; ++u) {
 #pragma unroll
         for (int vt = 0; vt < 4; ++vt) xa[u][vt] = ld_nt_u4(sp + (size_t)(u * 4 + vt) * 64);
-        qa[u] = qa_row[4 * (u % ks)];
+#pragma unroll
+        for (int gg = 0; gg < NG; ++gg) qa[gg][u] = qa_row[gg][4 * (u % ks)];
     }
     for (uint32_t j = 0; j < nb; ++j) {
-        f32x4 acc[4];
+        f32x4 acc[NG][4];
 #pragma unroll
-        for (int vt = 0; vt < 4; ++vt) acc[vt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int gg = 0; gg < NG; ++gg)
+#pragma unroll
+            for (int vt = 0; vt < 4; ++vt) acc[gg][vt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         for (uint32_t s0 = 0; s0 < ks; s0 += KD) {
             static_for<0, KD>([&](auto uu) {
                 constexpr int u = decltype(uu)::value;
-                const bf16x8 A = as_bf16x8(qa[u]);
 #pragma unroll
-                for (int vt = 0; vt < 4; ++vt)
-                    acc[vt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, as_bf16x8(xa[u][vt]), acc[vt], 0, 0, 0);
+                for (int gg = 0; gg < NG; ++gg) {
+                    const bf16x8 A = as_bf16x8(qa[gg][u]);
+#pragma unroll
+                    for (int vt = 0; vt < 4; ++vt)
+                        acc[gg][vt] =
+                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, as_bf16x8(xa[u][vt]), acc[gg][vt], 0, 0, 0);
+                }
                 const uint64_t nxt = (uint64_t)j * ks + s0 + u + KD;
 #pragma unroll
                 for (int vt = 0; vt < 4; ++vt) xa[u][vt] = ld_nt_u4(sp + (nxt * 4 + vt) * 64);
-                qa[u] = qa_row[4 * ((s0 + u + KD) % ks)];
+#pragma unroll
+                for (int gg = 0; gg < NG; ++gg) qa[gg][u] = qa_row[gg][4 * ((s0 + u + KD) % ks)];
             });
         }
-        // lower bounds into acc, upper bounds into ubv (the inline kernel's bound)
-        float ubv[4][4];
-        float4 pst[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pst[r] = *pst_r[r];
+        for (int gg = 0; gg < NG; ++gg) {
+            const int g0 = 16 * gg;  // this group's first query of the item
+            // lower bounds into acc, upper bounds into ubv (the inline kernel's bound)
+            float ubv[4][4];
+            float4 pst[4];
 #pragma unroll
-        for (int vt = 0; vt < 4; ++vt) {
-            const float4 mt = a.meta[(b0 + j) * 64 + 16 * vt + (lane & 15)];
-            const bool valid = j * 64 + 16 * vt + (lane & 15) < nv;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float dot = acc[vt][r];
-                const float4 ps = pst[r];
-                const float approx = M == kL2 ? (ps.x + mt.x) - 2.0f * dot : -(ps.x + dot);
-                const float an = ps.y + ps.z, bn = mt.y + mt.z;
-                const float cs = an * mt.z + ps.z * bn + ps.z * mt.z;
-                float del;
-                if (M == kL2) {
-                    const float rest = 2.0f * (cs + cm * (an * bn)) + cu * (ps.x + mt.x + fabsf(approx));
-                    del = rest + cr * (fabsf(approx) + rest);
-                } else {
-                    del = cs + cm * (an * bn) + cr * (ps.y * mt.w) + cu * (ps.y * ps.w + an * bn + fabsf(approx));
-                }
-                del = del * 1.001f + 1e-30f;
-                const float ub = approx + del;
-                acc[vt][r] = approx - del;
-                ubv[r][vt] = valid && ub == ub ? ub : __builtin_inff();
-            }
-        }
-        // per query row: the block's sorted upper bounds into the running list; its k-th
-        // (and ceil(k/4)-th) published; th = the smallest valid threshold known
-        float th[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int g = 4 * (lane >> 4) + r;
-            const int gc = min(g, nq - 1);
-            const uint32_t spi = it.pair_start + q0 + gc;
-            block_sort64(ubv[r]);
-            float4 rv = rl_lds[r * 64 + lane];
-            float rl[4] = {rv.x, rv.y, rv.z, rv.w};
-            merge_sorted64(rl, ubv[r]);
-            rl_lds[r * 64 + lane] = make_float4(rl[0], rl[1], rl[2], rl[3]);
-            const float tw = row_elem(rl, k - 1), tq = row_elem(rl, kq - 1);
-            uint32_t* gt = a.thr + spi;
-            uint32_t* s4 = a.thr4 + (size_t)spi * 4;
-            const uint4 t4 = *(const uint4*)s4;
-            const float th4 = fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w)));
-            const float cur = fminf(fminf(ord_dec(*gt), th4), ord_dec(s_thr[gc]));
-            if ((lane & 15) == 0 && g < nq) {
-                if (tw < cur) {
-                    atomicMin(&s_thr[g], ord_enc(tw));
-                    atomicMin(gt, ord_enc(tw));
-                }
-                if (tq < ord_dec(s4[residue])) atomicMin(s4 + residue, ord_enc(tq));
-            }
-            th[r] = g < nq ? fminf(tw, cur) : -__builtin_inff();
-        }
-        // candidates: one atomic per block for the wave's whole batch of them (the ballots are
-        // recomputed for the writes rather than held: registers)
-        auto is_cand = [&](int vt, int r) {
-            return j * 64 + 16 * vt + (lane & 15) < nv && 4 * (lane >> 4) + r < nq && !(acc[vt][r] > th[r]);
-        };
-        uint32_t tot = 0;
-#pragma unroll
-        for (int vt = 0; vt < 4; ++vt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) tot += (uint32_t)__popcll(__ballot(is_cand(vt, r)));
-        if (tot) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(a.ccount, tot);
-            base = __builtin_amdgcn_readfirstlane(base);
-            collected += tot;
+            for (int r = 0; r < 4; ++r) pst[r] = a.pst[pair_of(min(g0 + 4 * (lane >> 4) + r, nq - 1))];
 #pragma unroll
             for (int vt = 0; vt < 4; ++vt) {
+                const float4 mt = a.meta[(b0 + j) * 64 + 16 * vt + (lane & 15)];
+                const bool valid = j * 64 + 16 * vt + (lane & 15) < nv;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const bool c = is_cand(vt, r);
-                    const uint64_t mm = __ballot(c);
-                    if (c) {
-                        const uint32_t idx = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32),
-                                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
-                        const uint32_t spi = it.pair_start + q0 + 4 * (lane >> 4) + r;
-                        const uint32_t slot = (uint32_t)((b0 + j) * 64 + 16 * vt + (lane & 15));
-                        if (idx < a.cand_cap)
-                            a.cand[idx] = make_uint4(spi, slot, __float_as_uint(acc[vt][r]), 0u);
-                        else
-                            a.ovf[spi] = 1u;  // (any store of 1: idempotent)
+                    const float dot = acc[gg][vt][r];
+                    const float4 ps = pst[r];
+                    const float approx = M == kL2 ? (ps.x + mt.x) - 2.0f * dot : -(ps.x + dot);
+                    const float an = ps.y + ps.z, bn = mt.y + mt.z;
+                    const float cs = an * mt.z + ps.z * bn + ps.z * mt.z;
+                    float del;
+                    if (M == kL2) {
+                        const float rest = 2.0f * (cs + cm * (an * bn)) + cu * (ps.x + mt.x + fabsf(approx));
+                        del = rest + cr * (fabsf(approx) + rest);
+                    } else {
+                        del = cs + cm * (an * bn) + cr * (ps.y * mt.w) + cu * (ps.y * ps.w + an * bn + fabsf(approx));
                     }
-                    base += (uint32_t)__popcll(mm);
+                    del = del * 1.001f + 1e-30f;
+                    const float ub = approx + del;
+                    acc[gg][vt][r] = approx - del;
+                    ubv[r][vt] = valid && ub == ub ? ub : __builtin_inff();
+                }
+            }
+            // per query row: the block's sorted upper bounds into the running list; its k-th
+            // (and ceil(k/4)-th) published; th = the smallest valid threshold known
+            float th[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int g = g0 + 4 * (lane >> 4) + r;
+                const int gc = min(g, nq - 1);
+                const uint32_t spi = it.pair_start + q0 + gc;
+                block_sort64(ubv[r]);
+                float4* rlp = rl_lds + (gg * 4 + r) * 64 + lane;
+                const float4 rv = *rlp;
+                float rl[4] = {rv.x, rv.y, rv.z, rv.w};
+                merge_sorted64(rl, ubv[r]);
+                *rlp = make_float4(rl[0], rl[1], rl[2], rl[3]);
+                const float tw = row_elem(rl, k - 1), tq = row_elem(rl, kq - 1);
+                uint32_t* gt = a.thr + spi;
+                uint32_t* s4 = a.thr4 + (size_t)spi * 4;
+                const uint4 t4 = *(const uint4*)s4;
+                const float th4 = fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w)));
+                const float cur = fminf(fminf(ord_dec(*gt), th4), ord_dec(s_thr[gc]));
+                if ((lane & 15) == 0 && g < nq) {
+                    if (tw < cur) {
+                        atomicMin(&s_thr[g], ord_enc(tw));
+                        atomicMin(gt, ord_enc(tw));
+                    }
+                    if (tq < ord_dec(s4[residue])) atomicMin(s4 + residue, ord_enc(tq));
+                }
+                th[r] = g < nq ? fminf(tw, cur) : -__builtin_inff();
+            }
+            // candidates: one atomic per block and group for the wave's whole batch of them
+            // (the ballots are recomputed for the writes rather than held: registers)
+            auto is_cand = [&](int vt, int r) {
+                return j * 64 + 16 * vt + (lane & 15) < nv && g0 + 4 * (lane >> 4) + r < nq &&
+                       !(acc[gg][vt][r] > th[r]);
+            };
+            uint32_t tot = 0;
+#pragma unroll
+            for (int vt = 0; vt < 4; ++vt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tot += (uint32_t)__popcll(__ballot(is_cand(vt, r)));
+            if (tot) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(a.ccount, tot);
+                base = __builtin_amdgcn_readfirstlane(base);
+                collected += tot;
+#pragma unroll
+                for (int vt = 0; vt < 4; ++vt) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const bool c = is_cand(vt, r);
+                        const uint64_t mm = __ballot(c);
+                        if (c) {
+                            const uint32_t idx = base + __builtin_amdgcn_mbcnt_hi(
+                                                            (uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+                            const uint32_t spi = it.pair_start + q0 + g0 + 4 * (lane >> 4) + r;
+                            const uint32_t slot = (uint32_t)((b0 + j) * 64 + 16 * vt + (lane & 15));
+                            if (idx < a.cand_cap)
+                                a.cand[idx] = make_uint4(spi, slot, __float_as_uint(acc[gg][vt][r]), 0u);
+                            else
+                                a.ovf[spi] = 1u;  // (any store of 1: idempotent)
+                        }
+                        base += (uint32_t)__popcll(mm);
+                    }
                 }
             }
         }
@@ -840,13 +857,10 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
     }
 }
 
-__device__ __forceinline__ void reset_rl(float4* rl_lds) {
+__device__ __forceinline__ void reset_rl(float4* rl_lds, int rows) {
     const int lane = lane_id();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const float inf = __builtin_inff();
-        rl_lds[r * 64 + lane] = make_float4(inf, inf, inf, inf);
-    }
+    const float inf = __builtin_inff();
+    for (int r = 0; r < rows; ++r) rl_lds[r * 64 + lane] = make_float4(inf, inf, inf, inf);
 }
 
 // The wave's running lists of the item's nq queries (the k smallest upper bounds of the
@@ -858,9 +872,8 @@ __device__ __forceinline__ void contribute_rl(const ScanArgs& a, const ScanItem 
                                               const float4* rl_lds) {
     const int lane = lane_id();
     const int k = (int)a.k;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int g = 4 * (lane >> 4) + r;
+    for (int r = 0; r < (nq + 15) / 16 * 4; ++r) {  // (query rows: 4 per group of 16)
+        const int g = 16 * (r >> 2) + 4 * (lane >> 4) + (r & 3);
         const uint32_t spi = it.pair_start + q0 + min(g, nq - 1);
         uint32_t slot = 0;
         if ((lane & 15) == 0 && g < nq) slot = atomicAdd(&a.ubcnt[spi], 1u);
@@ -879,14 +892,16 @@ __device__ __forceinline__ void contribute_rl(const ScanArgs& a, const ScanItem 
 }
 
 // ivf_screen_collect: the persistent grid of ivf_scan_screen over the same queues (wide
-// items: a list's segments x <= 16 queries, the 4 waves taking the segments dynamically;
-// narrow items: one wave = one segment x <= 4 queries), collecting instead of re-checking.
-template <int M, int KD>
-__global__ __launch_bounds__(256, 2) void ivf_screen_collect(ScanArgs a) {
+// items: a list's segments x <= a.wide_q (16 or 32) queries, the 4 waves taking the
+// segments dynamically; narrow items: one wave = one segment x <= 4 queries), collecting
+// instead of re-checking. W2: items of up to 32 queries (two A operands per shadow tile: the
+// registers of one workgroup per CU; otherwise two).
+template <int M, int KD, bool W2>
+__global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a) {
     __shared__ uint32_t s_next, s_seg;
-    __shared__ uint32_t s_thr[16];
+    __shared__ uint32_t s_thr[32];
     __shared__ uint32_t s_thr_w[4][16];
-    __shared__ float4 s_rl[4][4 * 64];  // each wave's running lists (4 query rows x 64 lanes)
+    __shared__ float4 s_rl[4][8 * 64];  // each wave's running lists (up to 2 groups x 4 query rows x 64 lanes)
     const uint32_t wv = wave_index();
     const int lane = lane_id();
     float4* rl = s_rl[wv];
@@ -905,8 +920,8 @@ __global__ __launch_bounds__(256, 2) void ivf_screen_collect(ScanArgs a) {
             it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
             if (lane < (int)it.npairs) s_thr_w[wv][lane] = a.thr[it.pair_start + lane];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            reset_rl(rl);
-            collect_segment<M, KD>(a, it, 0, (int)it.npairs, it.seg, rl, s_thr_w[wv], it.seg & 3u);
+            reset_rl(rl, 4);
+            collect_segment<M, KD, 1>(a, it, 0, (int)it.npairs, it.seg, rl, s_thr_w[wv], it.seg & 3u);
             contribute_rl(a, it, 0, (int)it.npairs, rl);
         }
     };
@@ -930,14 +945,15 @@ __global__ __launch_bounds__(256, 2) void ivf_screen_collect(ScanArgs a) {
         const uint32_t seg_vectors = a.seg_blocks * 64;
         const uint32_t nseg = (a.count[it.list] + seg_vectors - 1) / seg_vectors;
         const uint32_t seg0 = it.seg * a.segs_item, seg1 = min(nseg, seg0 + a.segs_item);
-        reset_rl(rl);
+        reset_rl(rl, nq > 16 ? 8 : 4);
         bool any = false;
         for (;;) {
             uint32_t sg = 0;
             if (lane == 0) sg = atomicAdd(&s_seg, 1u);
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
-            collect_segment<M, KD>(a, it, 0, nq, sg, rl, s_thr, wv);
+            if (W2 && nq > 16) collect_segment<M, KD, 2>(a, it, 0, nq, sg, rl, s_thr, wv);
+            else collect_segment<M, KD, 1>(a, it, 0, nq, sg, rl, s_thr, wv);
             any = true;
         }
         if (any) contribute_rl(a, it, 0, nq, rl);
@@ -1221,14 +1237,21 @@ void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, con
 
 void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
     if (!grid_blocks) return;
-    const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
+    const bool w2 = a.wide_q > 16;
+    const uint32_t g = std::min<uint32_t>(grid_blocks, w2 ? kPersistentBlocks / 2 : kPersistentBlocks);
     const bool kd4 = (a.dp / 32) % 4 == 0;
+    auto go = [&](auto m_c, auto w_c) {
+        constexpr int Mm = decltype(m_c)::value;
+        constexpr bool Ww = decltype(w_c)::value;
+        if (kd4) ivf_screen_collect<Mm, 4, Ww><<<g, 256, 0, s>>>(a);
+        else ivf_screen_collect<Mm, 2, Ww><<<g, 256, 0, s>>>(a);
+    };
     if (metric == kL2) {
-        if (kd4) ivf_screen_collect<kL2, 4><<<g, 256, 0, s>>>(a);
-        else ivf_screen_collect<kL2, 2><<<g, 256, 0, s>>>(a);
+        if (w2) go(std::integral_constant<int, kL2>{}, std::true_type{});
+        else go(std::integral_constant<int, kL2>{}, std::false_type{});
     } else {
-        if (kd4) ivf_screen_collect<kIP, 4><<<g, 256, 0, s>>>(a);
-        else ivf_screen_collect<kIP, 2><<<g, 256, 0, s>>>(a);
+        if (w2) go(std::integral_constant<int, kIP>{}, std::true_type{});
+        else go(std::integral_constant<int, kIP>{}, std::false_type{});
     }
 }
 
