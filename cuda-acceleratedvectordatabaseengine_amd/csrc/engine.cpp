@@ -676,7 +676,7 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "tier_row_direct") {
             h->tier_row_direct = value != 0;
         } else if (n == "screen_group") {
-            require(value == 16 || value == 32, "screen_group is 16 or 32");
+            require(value == 0 || value == 16 || value == 32, "screen_group is 0 (auto), 16 or 32");
             h->screen_group = (uint32_t)value;
         } else if (n == "fused_scan") {
             h->fused_scan = value != 0;

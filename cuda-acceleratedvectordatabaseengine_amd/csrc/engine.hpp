@@ -311,7 +311,7 @@ struct vdb_ivf {
     bool screen_ready = false;
     bool screen_stale = false;  // lists or centroids changed since the last build
     uint32_t screen_segs_auto = 4;  // segments per screened wide item (upload_directory; option segs_per_item)
-    uint32_t screen_group = 16;     // queries per screened wide item at most: 16 or 32 (option screen_group; 32 measured slower at cfg4: 5.80 vs 5.27 ms)
+    uint32_t screen_group = 0;      // queries per screened wide item at most: 16 or 32, 0 = automatic (option screen_group)
     // Deferred re-checks (option screen_defer, default 1): the scan only collects candidates
     // against upper-bound thresholds; survivors of each pair's final threshold are re-checked
     // exactly afterwards from the arena (screen.hip ivf_screen_collect). 0: the inline kernel
@@ -799,10 +799,12 @@ struct vdb_ivf {
             seg_blocks = seg_blocks_opt;
         } else {
             seg_blocks = 8;  // 512 vectors at most by default (1024 is an explicit option)
-            // (The screened scan keeps 512: its items carry a wave's top-k across segments,
-            // and at the 1/8 shard of the 10M x 768 index 512-vector segments in items of 8
-            // measured 116K QPS at 3 in flight against 107K for 256 x 8 and 94K for 256 x 4.)
-            const bool screen_may = screen_opt && metric != 2 && !tiered();
+            // (The deferred screen keeps 512 for large shards; a small one (the 1/8 shard of the
+            // 10M x 768 index: 1.25M vectors) gets 256-vector segments in items of 4, enough
+            // items to fill the chip: collect 0.43 vs 0.50 ms; the full 10M index and the cfg4
+            // shard are 4-6 % slower with them. The inline screen measured 512 x 8 best.)
+            const bool screen_may = screen_opt && metric != 2;
+            if (screen_may && screen_defer && local < (4ull << 20)) seg_blocks = 4;
             while (!screen_may && seg_blocks > 1 && local / ((uint64_t)seg_blocks * 64) < 4096) seg_blocks >>= 1;
         }
         std::vector<uint32_t> cl(nlist), cg(nlist), ns(nlist);
@@ -831,6 +833,7 @@ struct vdb_ivf {
             }
             const double mean_seg = wsum > 0 ? wseg / wsum : 0.0;
             screen_segs_auto = mean_seg < 16.0 ? 4u : (mean_seg < 96.0 ? 8u : 16u);
+            if (seg_blocks == 4 && screen_defer && !seg_blocks_opt) screen_segs_auto = 4;  // (the small-shard choice)
         }
         std::vector<uint32_t> sorted(ns);
         std::sort(sorted.begin(), sorted.end(), std::greater<uint32_t>());
@@ -1971,7 +1974,10 @@ struct vdb_ivf {
         // 32-query items (option screen_group) where their shared lists fit the LDS
         // 32-query items (option screen_group): the deferred kernel feeds each shadow tile to two
         // A operands; the inline kernel splits its waves in two halves
-        const uint32_t swq = screen_group == 32 && (screen_defer || vdbk::scan_screen_fits(k, dp, 32)) ? 32u : 16u;
+        // (0 = automatic: 32 from nprobe 64 up, where hub lists are probed by many queries of a
+        // batch: cfg4 shard collect 4.45 vs 4.69 ms; 16 below: cfg3 2.54 vs 2.72 ms)
+        const uint32_t sg_want = screen_group ? screen_group : (screen_defer && P >= 64 ? 32u : 16u);
+        const uint32_t swq = sg_want == 32 && (screen_defer || vdbk::scan_screen_fits(k, dp, 32)) ? 32u : 16u;
         const bool screened = screen_ready && (!tiered() || screen_defer) && regs_k == 1 && metric != 2 &&
                               vdbk::scan_screen_fits(k, dp, swq);
         if (!screened && arena_dropped) ensure_arena();  // (the exact scans read the arena)

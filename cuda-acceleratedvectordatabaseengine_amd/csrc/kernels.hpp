@@ -49,7 +49,7 @@ constexpr int kCtrValid = 8;   // valid (query, probe) pairs of the batch (sorte
 constexpr int kCtrCand = 9;    // candidates the screen collected (may exceed the buffer)
 constexpr int kCtrSurv = 10;   // survivors of the final thresholds
 constexpr int kCounters = 16;
-constexpr int kUbLists = 64;   // deferred screened scan: upper-bound lists kept per (query, list) pair
+constexpr int kUbLists = 128;   // deferred screened scan: upper-bound lists kept per (query, list) pair
 
 struct ScanItem {
     uint32_t list;

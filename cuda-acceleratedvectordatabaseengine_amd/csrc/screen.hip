@@ -785,20 +785,28 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                 }
             }
             // per query row: the block's sorted upper bounds into the running list; its k-th
-            // (and ceil(k/4)-th) published; th = the smallest valid threshold known
+            // (and ceil(k/4)-th) published; th = the smallest valid threshold known. A block
+            // none of whose upper bounds is below any row's current k-th cannot change those
+            // rows' first k elements (the only ones used): its sort and merge are skipped (the
+            // list's elements k .. 63 may then go stale; elements 0 .. k-1 stay exact)
             float th[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int g = g0 + 4 * (lane >> 4) + r;
                 const int gc = min(g, nq - 1);
                 const uint32_t spi = it.pair_start + q0 + gc;
-                block_sort64(ubv[r]);
                 float4* rlp = rl_lds + (gg * 4 + r) * 64 + lane;
                 const float4 rv = *rlp;
                 float rl[4] = {rv.x, rv.y, rv.z, rv.w};
-                merge_sorted64(rl, ubv[r]);
-                *rlp = make_float4(rl[0], rl[1], rl[2], rl[3]);
-                const float tw = row_elem(rl, k - 1), tq = row_elem(rl, kq - 1);
+                float tw = row_elem(rl, k - 1), tq = row_elem(rl, kq - 1);
+                const float bmin = fminf(fminf(ubv[r][0], ubv[r][1]), fminf(ubv[r][2], ubv[r][3]));
+                if (__ballot(bmin < tw)) {
+                    block_sort64(ubv[r]);
+                    merge_sorted64(rl, ubv[r]);
+                    *rlp = make_float4(rl[0], rl[1], rl[2], rl[3]);
+                    tw = row_elem(rl, k - 1);
+                    tq = row_elem(rl, kq - 1);
+                }
                 uint32_t* gt = a.thr + spi;
                 uint32_t* s4 = a.thr4 + (size_t)spi * 4;
                 const uint4 t4 = *(const uint4*)s4;
@@ -1239,11 +1247,14 @@ void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, 
     if (!grid_blocks) return;
     const bool w2 = a.wide_q > 16;
     const uint32_t g = std::min<uint32_t>(grid_blocks, w2 ? kPersistentBlocks / 2 : kPersistentBlocks);
-    const bool kd4 = (a.dp / 32) % 4 == 0;
+    const bool kd4 = (a.dp / 32) % 4 == 0, kd8 = (a.dp / 32) % 8 == 0;
     auto go = [&](auto m_c, auto w_c) {
         constexpr int Mm = decltype(m_c)::value;
         constexpr bool Ww = decltype(w_c)::value;
-        if (kd4) ivf_screen_collect<Mm, 4, Ww><<<g, 256, 0, s>>>(a);
+        // (32-query items run one workgroup per CU: 8 k-steps of shadow in flight per wave
+        // keep as many bytes in flight per CU as two workgroups of 4 k-steps)
+        if (Ww && kd8) ivf_screen_collect<Mm, 8, Ww><<<g, 256, 0, s>>>(a);
+        else if (kd4) ivf_screen_collect<Mm, 4, Ww><<<g, 256, 0, s>>>(a);
         else ivf_screen_collect<Mm, 2, Ww><<<g, 256, 0, s>>>(a);
     };
     if (metric == kL2) {

@@ -63,10 +63,13 @@ typedef struct vdb_ivf_config {
                                  reference's gpu_memory_used_, ivf_flat_index.cpp:398-402). Once an add
                                  takes the lists above it, the handle switches to the list-cache tier
                                  with an HBM cache of this many bytes (lists home in page-locked host
-                                 memory; results unchanged). 0 = no cap: every list HBM-resident
-                                 (288 GB per GPU). The reference searches lists that do not fit on the
-                                 CPU; here a search whose single query probes more than the cap fails
-                                 with VDB_ERR_OUT_OF_MEMORY. */
+                                 memory; results unchanged); lifting or raising the cap above the lists
+                                 brings them back. Only list bytes count: the screen's bf16 shadow
+                                 (about half the list bytes) is not list data. 0 = no cap: every list
+                                 HBM-resident (288 GB per GPU). The reference searches lists that do
+                                 not fit on the CPU; here an exact-path search (k > 64, Cosine, screen
+                                 off) whose single query probes more than the cap fails with
+                                 VDB_ERR_OUT_OF_MEMORY; the screened tier loads no list. */
     int32_t device;           /* HIP device ordinal */
 } vdb_ivf_config;
 
@@ -192,9 +195,10 @@ int vdb_ivf_plan_shard_owners(vdb_ivf* index, uint32_t rank, uint32_t world, con
  * so every rank receives the FINAL results. Every rank must issue the same search calls
  * (same n, nprobe, k and batch option) in the same order; on such a handle vdb_ivf_search
  * does not coalesce concurrent callers (the grouping would depend on each rank's timing):
- * calls run one at a time. With the list-cache tier on (the same setting on every rank),
- * each rank serves its shard through its own cache and a call ends in ONE all-gather of
- * the whole call's partials instead of one per batch. */
+ * calls run one at a time. At world > 1 a call ends in ONE all-gather of the whole call's
+ * partials (not one per batch): a rank's own state (its list-cache tier, which its shard's
+ * size may switch on, and what its cache holds) shapes its batches, so only per-call
+ * exchanges are the same on every rank. */
 #define VDB_COMM_ID_BYTES 128
 int vdb_comm_unique_id(void* id); /* VDB_COMM_ID_BYTES bytes (ncclGetUniqueId) */
 int vdb_ivf_attach_comm(vdb_ivf* index, const void* id, uint32_t rank, uint32_t world);
@@ -202,7 +206,7 @@ int vdb_ivf_detach_comm(vdb_ivf* index);
 /* The communicator's deadline (option "comm_timeout_ms", default 120000): init is
  * non-blocking and polled, so a rank that never joins makes vdb_ivf_attach_comm fail with
  * VDB_ERR_DEVICE naming this rank; at attach every rank's dimension, nlist, metric, batch,
- * tier setting, stale_slots and list sizes are compared, and the ranks' stored lists must
+ * stale_slots and list sizes are compared, and the ranks' stored lists must
  * partition the non-empty lists (VDB_ERR_STATE otherwise). Each exchange's completion is watched; one
  * still pending after the deadline marks the communicator failed (later searches fail with
  * the message). vdb_ivf_comm_status returns VDB_OK, or VDB_ERR_DEVICE with that message,
@@ -270,15 +274,21 @@ int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
  * vdb_ivf_warmup, and evicted like any cached list. Needs "list_cache_bytes" > 0 set
  * first; the handle becomes read-only (add fails with VDB_ERR_STATE). A shard file
  * (vdb_ivf_save of a handle with world > 1: every list's count, only the rank's own lists'
- * rows) makes this handle that rank's shard (rank and world from the file, checked against
- * the LPT plan); vdb_ivf_attach_comm then serves a sharded index larger than the node's
- * HBM from every rank's own file. */
+ * rows) makes this handle that rank's shard: rank and world come from the file and the lists
+ * it stores define the shard (any plan; nothing is checked against a plan here, only
+ * vdb_ivf_attach_comm's partition check across the ranks); vdb_ivf_attach_comm then serves a
+ * sharded index larger than the node's HBM from every rank's own file.
+ * With the screen (L2 / IP, k <= 64) the first search streams the file once to build the
+ * lists' bf16 shadow, norms and ids in HBM; later searches read only the exact re-checks'
+ * rows from the file (one O_DIRECT read each, option "tier_row_direct" 0: buffered). */
 int vdb_ivf_open_lists(vdb_ivf* index, const char* path);
 
 /* get_gpu_memory_usage's definition: count * (dim * 4 + 8) bytes per GPU-resident list. */
 uint64_t vdb_ivf_gpu_bytes(const vdb_ivf* index);
-/* HBM this handle really holds for lists and centroids (64-row blocks, dimension padding,
- * the scan's slack block, the whole cache in the list-cache tier). */
+/* Device memory this handle really holds: the lists in every layout it keeps (row-major
+ * fp32 copy, bf16 shadow and norms while the screen serves; the interleaved arena otherwise
+ * or when an exact-path search rebuilt it; the whole cache in the list-cache tier), ids,
+ * centroids, directories, every search workspace and staging buffer. */
 uint64_t vdb_ivf_gpu_bytes_allocated(const vdb_ivf* index);
 uint64_t vdb_ivf_ntotal(const vdb_ivf* index);
 uint32_t vdb_ivf_dimension(const vdb_ivf* index);
@@ -306,9 +316,16 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * "fused_scan" (1, default: one persistent scan grid takes both the wide and the narrow
  * items; 0: narrow items on a second stream), "screen" (1, default: the screened scan — bf16
  * matrix-core distance bounds from a shadow of the lists, exact fp32 sums only for pairs that can
- * reach a list's top-k; L2/IP, k <= 64, lists in HBM; costs 1.5x the list bytes of extra HBM;
- * 0: the exact VALU scan of every pair), "screen_group" (16, default, or 32: queries per screened wide
- * item; 32 splits an item's waves in two halves that stream each segment side by side),
+ * reach a list's top-k; L2/IP, k <= 64; the lists are then held as a row-major fp32 copy plus the
+ * bf16 shadow and norms, ~1.5x the list bytes; in the list-cache tier the shadow alone stays
+ * in HBM and the rows at home; 0: the exact VALU scan of every pair), "screen_group" (16,
+ * default, or 32: queries per screened wide item; with the deferred scan every shadow tile
+ * then feeds two 16-query A operands, inline: two wave halves), "screen_defer" (1, default:
+ * the screen collects candidates against upper-bound thresholds and re-checks afterwards only
+ * the survivors of each (query, list) pair's final threshold; 0: re-checks inline as
+ * candidates appear), "screen_cand_cap" (collected candidates per batch, default 4M; a pair
+ * beyond it is recomputed over its whole list, a file-home tier batch re-run with more),
+ * "tier_row_direct" (1, default: the screened tier reads survivors' rows with O_DIRECT),
  * "list_cache_bytes" (0 = every list HBM-resident; > 0 = the list-cache tier above with an
  * HBM cache of that many bytes; a search whose single query probes more fails with
  * VDB_ERR_OUT_OF_MEMORY, a batch probing more is split; setting it replaces the

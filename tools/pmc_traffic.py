@@ -47,7 +47,7 @@ def summarise(d, batches, key):
             name = row["Kernel_Name"].split("(")[0].replace("void ", "")
             per_kernel[name] += float(row["Counter_Value"])
             dispatches[name].add(row.get("Dispatch_Id", ""))
-    scan = {k: v for k, v in per_kernel.items() if "ivf_scan" in k}
+    scan = {k: v for k, v in per_kernel.items() if "ivf_scan" in k or "ivf_screen_collect" in k}
     kib = sum(scan.values())
     return {
         "workload": key,
