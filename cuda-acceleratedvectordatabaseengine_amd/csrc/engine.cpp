@@ -673,6 +673,16 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->set_device();
             h->quiesce();
             h->screen_cand_cap = (uint32_t)value;
+        } else if (n == "screen_floor_ppm") {
+            require(value >= 0 && value <= 1000000, "screen_floor_ppm is 0 (never) .. 1000000");
+            h->screen_floor_ppm = (uint32_t)value;
+            h->screen_skip_left = h->screen_floor_streak = h->floor_probe = 0;
+        } else if (n == "screen_floor_min") {
+            require(value >= 0, "screen_floor_min is >= 0");
+            h->screen_floor_min = (uint64_t)value;
+        } else if (n == "screen_floor_skip") {
+            require(value >= 1 && value < (1ll << 20), "screen_floor_skip is 1 .. 2^20");
+            h->screen_floor_skip = (uint32_t)value;
         } else if (n == "tier_row_direct") {
             h->tier_row_direct = value != 0;
         } else if (n == "screen_group") {
@@ -803,6 +813,7 @@ int vdb_ivf_profile_reset(vdb_ivf* h) {
         p->set_device();
         HIPCHECK(hipDeviceSynchronize());
         p->events_used = 0;
+        p->screen_floor_batches = p->screen_floor_trips = 0;
         HIPCHECK(hipMemsetAsync(p->stats.ensure(16), 0, 128, p->stream));
         HIPCHECK(hipStreamSynchronize(p->stream));
         h->set_device();
@@ -861,6 +872,8 @@ int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
         p.exact_reranks = st[5] + st[10];
         p.bounded_blocks = st[6] + st[9];
         p.screen_collected = st[8];
+        p.screen_floor_batches = h->screen_floor_batches;
+        p.screen_floor_trips = h->screen_floor_trips;
         p.computed_vectors = st[7];
         *out = p;
         hh->set_device();

@@ -345,6 +345,49 @@ struct vdb_ivf {
     std::vector<uint2> fetch_surv;     // ... their (slot, pair)
     uint64_t screen_rows_fetched = 0, screen_row_bytes = 0, screen_tier_batches = 0, screen_reruns = 0;
     uint32_t tier_cand_cap = 0;        // ... a candidate capacity grown by an overflow
+    // Run-time floor under the screen (lists in HBM): every deferred batch reports to
+    // page-locked host memory its survivors (or an overflow of the candidate buffer), its
+    // (query, vector) pairs and k x its valid (query, list) pairs (the survivors no screen can
+    // avoid). When a completed batch of at least screen_floor_min pairs overflowed, or its
+    // survivors beyond those exceed screen_floor_ppm of its pairs (a data regime where the
+    // bound is wider than the distance spread: the exact re-checks then cost more than the
+    // exact scan saves), the next batches run the exact scan, then the screen is tried again:
+    // screen_floor_skip batches after a first trip, twice as many after each further trip in
+    // a row (at most 32x), so a dataset that never screens pays one screened batch per
+    // thousand: after a trip, the screen is retried on one batch, and the batches issued
+    // while its report is outstanding run the exact scan (the reports of batches already in
+    // flight at a trip belong to that trip). Results are the same either way; only speed changes. (Break-even at cfg3: the
+    // exact scan 4.9 ms against the screen's 2.7 ms plus ~4.6 ns per survivor, ~9 % of the
+    // batch's 5.0M pairs; 5 % leaves room for the retries.)
+    uint32_t screen_floor_ppm = 50000;  // option screen_floor_ppm (0: never fall back)
+    uint32_t screen_floor_skip = 32;    // option screen_floor_skip
+    uint64_t screen_floor_min = 1u << 22;  // option screen_floor_min (pairs of a batch the floor judges)
+    uint32_t screen_skip_left = 0, screen_floor_seq = 0, screen_floor_seen = 0, screen_floor_streak = 0;
+    uint32_t floor_probe = 0, floor_trip_seq = 0;  // (the retry batch's sequence; the last trip's)
+    uint64_t screen_floor_batches = 0, screen_floor_trips = 0;
+    DevBuf<uint4> floor_host;           // page-locked, one entry per workspace slot
+    void floor_poll() {
+        if (!floor_host.p) return;
+        for (int i = 0; i < kSlots; ++i) {
+            const volatile uint32_t* f = (const volatile uint32_t*)(floor_host.p + i);
+            const uint4 v = make_uint4(f[0], f[1], f[2], f[3]);
+            if (!v.z || (int32_t)(v.z - screen_floor_seen) <= 0) continue;
+            screen_floor_seen = v.z;
+            const bool probe = floor_probe && v.z == floor_probe;
+            if (probe) floor_probe = 0;
+            if (!screen_floor_ppm || v.y < screen_floor_min) continue;
+            if (screen_floor_trips && (int32_t)(v.z - floor_trip_seq) <= 0) continue;  // (in flight at the trip)
+            const uint64_t excess = v.x > v.w ? (uint64_t)v.x - v.w : 0;
+            if (v.x == ~0u || excess * 1000000ull > (uint64_t)screen_floor_ppm * v.y) {
+                screen_skip_left = screen_floor_skip << std::min<uint32_t>(screen_floor_streak, 5);
+                ++screen_floor_streak;
+                ++screen_floor_trips;
+                floor_trip_seq = screen_floor_seq;
+            } else if (probe) {
+                screen_floor_streak = 0;
+            }
+        }
+    }
     DevBuf<uint4> screen_sh;
     DevBuf<float> screen_rows;
     DevBuf<float4> screen_meta;
@@ -1978,8 +2021,19 @@ struct vdb_ivf {
         // batch: cfg4 shard collect 4.45 vs 4.69 ms; 16 below: cfg3 2.54 vs 2.72 ms)
         const uint32_t sg_want = screen_group ? screen_group : (screen_defer && P >= 64 ? 32u : 16u);
         const uint32_t swq = sg_want == 32 && (screen_defer || vdbk::scan_screen_fits(k, dp, 32)) ? 32u : 16u;
-        const bool screened = screen_ready && (!tiered() || screen_defer) && regs_k == 1 && metric != 2 &&
-                              vdbk::scan_screen_fits(k, dp, swq);
+        bool screened = screen_ready && (!tiered() || screen_defer) && regs_k == 1 && metric != 2 &&
+                        vdbk::scan_screen_fits(k, dp, swq);
+        bool floor_retry = false;
+        if (screened && !tiered() && screen_defer) {  // the run-time floor (lists in HBM only)
+            floor_poll();
+            if (screen_skip_left || floor_probe) {
+                if (screen_skip_left) --screen_skip_left;
+                ++screen_floor_batches;
+                screened = false;
+            } else {
+                floor_retry = screen_floor_streak > 0;
+            }
+        }
         if (!screened && arena_dropped) ensure_arena();  // (the exact scans read the arena)
         const uint32_t mfma_min = !screened && wide && waves == 4 && metric != 2 && !(VDB_SCAN_DIAG & 2) &&
                                           vdbk::scan_bounded_fits(d4, k)
@@ -2068,6 +2122,16 @@ struct vdb_ivf {
                     sa.ovf = w.ovf.p;
                     sa.ublist = w.ublist.p;
                     sa.ubcnt = w.ubcnt.p;
+                    if (!tiered()) {
+                        if (!floor_host.p) {
+                            floor_host.host = true;
+                            std::memset(floor_host.ensure(kSlots), 0, kSlots * sizeof(uint4));
+                        }
+                        sa.floor_out = floor_host.p + (in_ring ? (&w - slots) : 0);
+                        if (!++screen_floor_seq) ++screen_floor_seq;  // (0: never written)
+                        sa.floor_seq = screen_floor_seq;
+                        if (floor_retry) floor_probe = screen_floor_seq;
+                    }
                     sa.mstats = bounded_stats && !pass ? stats.p + 8 : nullptr;
                     if (ev) HIPCHECK(hipEventRecord(ev->collect_begin, s));
                     vdbk::launch_screen_collect(metric, grid, sa, s);
@@ -2086,7 +2150,7 @@ struct vdb_ivf {
                 }
                 if (tiered()) ++screen_tier_batches;
                 vdbk::launch_screen_recheck(metric, sa, BP, w.probes.p, w.nseg_qp.p, w.soff.p, w.scnt.p, w.surv.p, w.ovf.p,
-                                            fetched, w.sdist.p, ccap, s);
+                                            fetched, w.sdist.p, ccap, (uint32_t)nseg_prefix[1], s);
             } else {
                 vdbk::launch_scan_screen(metric, grid, sa, s);
             }

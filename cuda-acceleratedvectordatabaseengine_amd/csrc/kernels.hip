@@ -716,11 +716,15 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     __shared__ uint32_t sh[33];
     __shared__ uint32_t sh_multi[(VDB_SEED_LEVELS + 2) * 17];
     __shared__ uint32_t s_nvalid;
+    __shared__ unsigned long long s_pairs;
     const uint32_t tid = threadIdx.x;
     const uint32_t BP = B * P;
     const uint32_t wide = wide_on;  // wide group size (0: no wide items)
 
-    if (tid == 0) s_nvalid = 0;
+    if (tid == 0) {
+        s_nvalid = 0;
+        s_pairs = 0;
+    }
     for (uint32_t i = tid; i < BP; i += blockDim.x) thr[i] = kThrInf;  // the scan's shared thresholds
     for (uint32_t i = tid; i < NP; i += blockDim.x) {
         uint32_t key = kInvalidKey;
@@ -976,6 +980,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         lsum += __shfl_xor(lsum, off);
         csum += __shfl_xor(csum, off);
     }
+    if ((tid & 63) == 0 && vsum) atomicAdd(&s_pairs, vsum);
     if ((tid & 63) == 0) {
         if (vsum) atomicAdd(&stats[4], vsum);
         if (lsum) atomicAdd(&stats[1], lsum);
@@ -991,6 +996,10 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         counters[6] = 0;
         counters[7] = n_bounded;  // bounded items: items_w[n_exact, n_exact + n_bounded)
         counters[kCtrValid] = nvalid;  // (sorted pairs [0, nvalid) are the batch's valid pairs)
+    }
+    __syncthreads();  // (s_pairs complete)
+    if (tid == 0) {
+        counters[kCtrPairs] = (uint32_t)min(s_pairs, 0xFFFFFFFFull);
         atomicAdd(&stats[0], (unsigned long long)nd);  // (the per-wave sums follow)
         atomicAdd(&stats[2], (unsigned long long)(n_narrow + n_wide));
         atomicAdd(&stats[3], 1ull);

@@ -48,6 +48,7 @@ constexpr uint32_t kPersistentBlocks = 512; // scan grid: 2 workgroups per CU on
 constexpr int kCtrValid = 8;   // valid (query, probe) pairs of the batch (sorted pairs [0, n))
 constexpr int kCtrCand = 9;    // candidates the screen collected (may exceed the buffer)
 constexpr int kCtrSurv = 10;   // survivors of the final thresholds
+constexpr int kCtrPairs = 11;  // (query, vector) pairs of the batch (saturating at 2^32 - 1)
 constexpr int kCounters = 16;
 constexpr int kUbLists = 128;   // deferred screened scan: upper-bound lists kept per (query, list) pair
 
@@ -143,6 +144,8 @@ struct ScanArgs {
     uint32_t cand_cap = 0;
     uint32_t* ccount = nullptr;
     uint32_t* ovf = nullptr;
+    uint4* floor_out = nullptr; // (page-locked, mapped) {survivors, pairs, sequence, 1} of the batch: the run-time floor
+    uint32_t floor_seq = 0;
     float* ublist = nullptr;    // per sorted pair kUbLists lists of k upper bounds (the waves' running lists)
     uint32_t* ubcnt = nullptr;  // ... and how many were offered
 };
@@ -177,7 +180,7 @@ void launch_screen_select(const ScanArgs& a, uint32_t BP, uint32_t* scnt, uint32
 // survivors' rows [survivor][dp] (tier); sdist: their exact distances (max_surv entries).
 void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uint32_t* probes, uint32_t* nseg_qp,
                            const uint32_t* soff, const uint32_t* scnt, const uint2* surv, const uint32_t* ovf,
-                           const float* fetched, float* sdist, uint32_t max_surv, hipStream_t s);
+                           const float* fetched, float* sdist, uint32_t max_surv, uint32_t smax, hipStream_t s);
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                        const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,

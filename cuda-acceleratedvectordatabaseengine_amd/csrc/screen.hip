@@ -1015,7 +1015,8 @@ __global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ can
 // soff[0 .. nvalid], the total into counters[kCtrSurv].
 __global__ __launch_bounds__(1024) void ivf_screen_offsets(const uint32_t* __restrict__ scnt,
                                                            uint32_t* __restrict__ counters,
-                                                           uint32_t* __restrict__ soff) {
+                                                           uint32_t* __restrict__ soff, uint4* __restrict__ floor_out,
+                                                           uint32_t floor_seq, uint32_t cap, uint32_t k) {
     __shared__ uint32_t wsum[16];
     const uint32_t n = counters[kCtrValid];
     const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
@@ -1045,6 +1046,11 @@ __global__ __launch_bounds__(1024) void ivf_screen_offsets(const uint32_t* __res
     if (threadIdx.x == 0) {
         soff[n] = total;
         counters[kCtrSurv] = total;
+        // (the run-time floor's feedback, one 16-byte vector store to page-locked host memory:
+        // {survivors or ~0 after an overflow, (query, vector) pairs, sequence, k x valid pairs})
+        if (floor_out)
+            *floor_out = make_uint4(counters[kCtrCand] > cap ? ~0u : total, counters[kCtrPairs], floor_seq,
+                                    (uint32_t)min(0xFFFFFFFFull, (unsigned long long)k * n));
     }
 }
 
@@ -1155,9 +1161,12 @@ __global__ __launch_bounds__(64) void ivf_screen_exact(ScanArgs a, const uint2* 
     }
 }
 
-// One wave per valid sorted (query, list) pair: the exact top-k of its survivors' distances
-// (or, for a pair that overflowed the candidate buffer, of its whole list, recomputed lane
-// = vector from the row-major copy), written as the pair's only partial.
+// One wave per valid sorted (query, list) pair: the exact top-k of its survivors' distances,
+// written as the pair's only partial. A pair that overflowed the candidate buffer keeps its
+// planned segments instead: one wave per (pair, segment) recomputes the segment lane =
+// vector from the row-major copy and writes the segment's partial (neighbouring waves take
+// the same segment of one list for neighbouring queries: its rows are shared in L2), so a
+// batch in the cancellation regime costs a parallel dense pass, not one wave per pair.
 template <int M>
 __global__ __launch_bounds__(256) void ivf_screen_pair_topk(ScanArgs a, const uint32_t* __restrict__ probes,
                                                             uint32_t* __restrict__ nseg_qp,
@@ -1165,47 +1174,29 @@ __global__ __launch_bounds__(256) void ivf_screen_pair_topk(ScanArgs a, const ui
                                                             const uint32_t* __restrict__ scnt,
                                                             const uint2* __restrict__ surv,
                                                             const float* __restrict__ sdist,
-                                                            const uint32_t* __restrict__ ovf) {
+                                                            const uint32_t* __restrict__ ovf, uint32_t smax) {
     const int lane = lane_id();
     const uint32_t nvalid = a.counters[kCtrValid];
     const int k = (int)a.k;
+    const uint32_t wv = blockIdx.x * 4 + wave_index(), nw = gridDim.x * 4;
     unsigned long long rechecked = 0;
-    for (uint32_t s = blockIdx.x * 4 + wave_index(); s < nvalid; s += gridDim.x * 4) {
+    for (uint32_t s = wv; s < nvalid; s += nw) {
+        if (ovf[s]) continue;
         const uint32_t pr = a.sorted_pair[s];
         const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
         WaveTopK<1> tk;
         tk.init();
         float kd = __builtin_inff();
         uint64_t ki = kNoId;
-        if (ovf[s]) {
-            const uint32_t list = probes[(size_t)q * a.P + p];
-            const uint32_t n = a.count[list];
-            const uint64_t lbase = a.block_off[list] * 64;
-            const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
-            for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-                const uint32_t i = i0 + lane;
-                const bool act = i < n;
-                float dist = __builtin_inff();
-                uint64_t id = kNoId;
-                if (act) {  // (the row-major copy, or the tier's host arena; a file home never overflows)
-                    dist = a.rows ? exact_dist<M, true>((const float4*)a.rows, lbase + i, a.d4, qr)
-                                  : exact_dist<M, false>(a.arena, lbase + i, a.d4, qr);
-                    id = a.ids[lbase + i];
-                }
-                offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
-            }
-            rechecked += n;
-        } else {
-            const uint32_t n = scnt[s], o = soff[s];
-            for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-                const uint32_t i = i0 + lane;
-                const bool act = i < n;
-                const float dist = act ? sdist[o + i] : __builtin_inff();
-                const uint64_t id = act ? a.ids[surv[o + i].x] : kNoId;
-                offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
-            }
-            rechecked += n;
+        const uint32_t n = scnt[s], o = soff[s];
+        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool act = i < n;
+            const float dist = act ? sdist[o + i] : __builtin_inff();
+            const uint64_t id = act ? a.ids[surv[o + i].x] : kNoId;
+            offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
         }
+        rechecked += n;
         // the pair's exact top-k is its only partial: the merge reads the first of its segments
         const uint32_t part = a.part_base_sorted[s];
         if (lane < k) {
@@ -1213,6 +1204,41 @@ __global__ __launch_bounds__(256) void ivf_screen_pair_topk(ScanArgs a, const ui
             a.part_i[(size_t)part * k + lane] = tk.id[0];
         }
         if (lane == 0) nseg_qp[(size_t)q * a.P + p] = 1u;
+    }
+    const uint64_t tasks = (uint64_t)nvalid * smax;
+    const uint32_t segv = a.seg_blocks * 64;
+    for (uint64_t t = wv; t < tasks; t += nw) {
+        const uint32_t s = (uint32_t)(t % nvalid), j = (uint32_t)(t / nvalid);
+        if (!ovf[s]) continue;
+        const uint32_t pr = a.sorted_pair[s];
+        const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
+        if (j >= nseg_qp[(size_t)q * a.P + p]) continue;  // (the planned segments: untouched above)
+        const uint32_t list = probes[(size_t)q * a.P + p];
+        const uint32_t n = min(a.count[list], (j + 1) * segv);
+        const uint64_t lbase = a.block_off[list] * 64;
+        const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
+        WaveTopK<1> tk;
+        tk.init();
+        float kd = __builtin_inff();
+        uint64_t ki = kNoId;
+        for (uint32_t i0 = j * segv; i0 < n; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool act = i < n;
+            float dist = __builtin_inff();
+            uint64_t id = kNoId;
+            if (act) {  // (the row-major copy, or the tier's host arena; a file home never overflows)
+                dist = a.rows ? exact_dist<M, true>((const float4*)a.rows, lbase + i, a.d4, qr)
+                              : exact_dist<M, false>(a.arena, lbase + i, a.d4, qr);
+                id = a.ids[lbase + i];
+            }
+            offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
+        }
+        rechecked += n > j * segv ? n - j * segv : 0;
+        const uint32_t part = a.part_base_sorted[s] + j;
+        if (lane < k) {
+            a.part_d[(size_t)part * k + lane] = tk.d[0];
+            a.part_i[(size_t)part * k + lane] = tk.id[0];
+        }
     }
     if (a.mstats && lane == 0 && rechecked) atomicAdd(&a.mstats[2], rechecked);
 }
@@ -1273,13 +1299,13 @@ void launch_screen_select(const ScanArgs& a, uint32_t BP, uint32_t* scnt, uint32
     ivf_screen_tfinal<<<std::max<uint32_t>(1, std::min<uint32_t>(2048, (BP + 3) / 4)), 256, 0, s>>>(a);
     const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(1024, (a.cand_cap + 255) / 256));
     ivf_screen_filter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, a.thr, a.thr4, ovf, scnt);
-    ivf_screen_offsets<<<1, 1024, 0, s>>>(scnt, ctr, soff);
+    ivf_screen_offsets<<<1, 1024, 0, s>>>(scnt, ctr, soff, a.floor_out, a.floor_seq, a.cand_cap, a.k);
     ivf_screen_scatter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, soff, surv);
 }
 
 void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uint32_t* probes, uint32_t* nseg_qp,
                            const uint32_t* soff, const uint32_t* scnt, const uint2* surv, const uint32_t* ovf,
-                           const float* fetched, float* sdist, uint32_t max_surv, hipStream_t s) {
+                           const float* fetched, float* sdist, uint32_t max_surv, uint32_t smax, hipStream_t s) {
     if (!BP) return;
     static const bool raised = [] {
         for (const void* fn : {(const void*)ivf_screen_exact<kL2, 0>, (const void*)ivf_screen_exact<kIP, 0>,
@@ -1292,14 +1318,15 @@ void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uin
     (void)raised;
     const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>(16384, (max_surv + kExactRows - 1) / kExactRows));
     const size_t lds = exact_lds(a.d4);
-    const uint32_t gp = std::max<uint32_t>(1, std::min<uint32_t>(2048, (BP + 3) / 4));
+    // (waves enough for the pairs, and for the (pair, segment) tasks of overflowed pairs)
+    const uint32_t gp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, ((uint64_t)BP * smax + 3) / 4));
     const int src = fetched ? 1 : (a.rows ? 0 : 2);
     auto exact = [&](auto m_c) {
         constexpr int Mm = decltype(m_c)::value;
         if (src == 0) ivf_screen_exact<Mm, 0><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
         else if (src == 1) ivf_screen_exact<Mm, 1><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
         else ivf_screen_exact<Mm, 2><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
-        ivf_screen_pair_topk<Mm><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, sdist, ovf);
+        ivf_screen_pair_topk<Mm><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, sdist, ovf, smax);
     };
     if (metric == kL2) exact(std::integral_constant<int, kL2>{});
     else exact(std::integral_constant<int, kIP>{});

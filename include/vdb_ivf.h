@@ -100,6 +100,8 @@ typedef struct vdb_ivf_profile {
     double collect_ms;         /* deferred screened scan: summed durations of its collect kernel (the
                                   stream of the bf16 shadow; scan_ms covers it and the re-check kernels) */
     double recheck_ms;         /* ... and of the final thresholds, selection and exact re-checks after it */
+    uint64_t screen_floor_batches; /* batches the run-time floor ran on the exact scan */
+    uint64_t screen_floor_trips;   /* screened batches that tripped the floor */
 } vdb_ivf_profile;
 
 const char* vdb_last_error(void);
@@ -326,6 +328,11 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * candidates appear), "screen_cand_cap" (collected candidates per batch, default 4M; a pair
  * beyond it is recomputed over its whole list, a file-home tier batch re-run with more),
  * "tier_row_direct" (1, default: the screened tier reads survivors' rows with O_DIRECT),
+ * "screen_floor_ppm" (50000, default: a screened batch of at least "screen_floor_min" (4M)
+ * (query, vector) pairs that overflowed its candidate buffer, or whose survivors beyond k per
+ * (query, list) pair exceed this many per million of its pairs, sends the next
+ * "screen_floor_skip" (32) batches to the exact scan, twice as many after each further trip in
+ * a row (at most 32x), then the screen is tried again; 0: never; lists in HBM only),
  * "list_cache_bytes" (0 = every list HBM-resident; > 0 = the list-cache tier above with an
  * HBM cache of that many bytes; a search whose single query probes more fails with
  * VDB_ERR_OUT_OF_MEMORY, a batch probing more is split; setting it replaces the

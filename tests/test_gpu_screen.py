@@ -76,15 +76,19 @@ def test_screen_is_taken_and_prunes(defer):
 @pytest.mark.parametrize("metric", [0, 1])
 def test_screen_deferred_overflow_recomputes_the_pair(metric):
     """A candidate buffer far too small for the batch: every pair whose candidates do not fit
-    is marked and recomputed exactly over its whole list; results unchanged."""
+    is marked and recomputed exactly over its whole list, one wave per planned segment (one
+    and several segments per list); results unchanged."""
     X, ids, lists, C, Q = hub_data(48, seed=77)
     g, o = lists_pair(X, ids, lists, C, metric)
     nprobe = 3 if metric == 0 else 6
     Dr, Ir = o.search(Q, nprobe, 10)
     g.set_option("screen_cand_cap", 1024)
-    D, I, p = screen_stats(g, Q, nprobe, 10, 130)
-    assert_same(D, I, Dr, Ir)
-    assert p["screen_collected"] > 1024, p
+    g.set_option("screen_floor_ppm", 0)  # (the floor would send the next batches to the exact scan)
+    for seg in (64, 0):
+        g.set_option("seg_vectors", seg)
+        D, I, p = screen_stats(g, Q, nprobe, 10, 130)
+        assert_same(D, I, Dr, Ir)
+        assert p["screen_collected"] > 1024, p
     g.set_option("screen_cand_cap", 4 << 20)
     assert_same(*search_all(g, Q, nprobe, 10, 130), Dr, Ir)
 
@@ -120,6 +124,37 @@ def test_screen_cancellation_every_pair_a_candidate(metric, defer):
     assert_same(D, I, Dr, Ir)
     if metric == 0:
         assert p["exact_reranks"] < 0.5 * p["pair_vectors"], p
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_screen_run_time_floor(metric):
+    """The cancellation regime call after call: a batch whose survivors exceed
+    screen_floor_ppm of its pairs trips the floor, and the next screen_floor_skip batches
+    run the exact scan; results stay bit-identical through every switch. screen_floor_ppm 0
+    never trips."""
+    rng = np.random.default_rng(12)
+    dim = 48
+    c = (100.0 / np.sqrt(dim)) * np.ones(dim, np.float32)
+    X = (c + 0.01 * rng.standard_normal((8000, dim))).astype(np.float32)
+    Q = (c + 0.01 * rng.standard_normal((6 * 32, dim))).astype(np.float32)
+    lists = (rng.random(8000) >= 0.7).astype(np.int64)
+    ids = np.arange(8000, dtype=np.uint64)
+    C = np.stack([np.zeros_like(c), -c]).astype(np.float32)
+    g, o = lists_pair(X, ids, lists, C, metric)
+    g.set_option("screen_floor_skip", 3)
+    g.set_option("screen_floor_min", 0)  # (these batches are small: 32 x ~5600 pairs)
+    for ppm in (50000, 0):
+        g.set_option("screen_floor_ppm", ppm)
+        g.profile_reset()
+        for j in range(6):  # one batch per call: each call's report is read by the next
+            q = Q[32 * j:32 * (j + 1)]
+            assert_same(*search_all(g, q, 2, 10, 32), *o.search(q, 2, 10))
+        p = g.profile_read()
+        if ppm:
+            # calls 0, 4 screened (each trips: 3, then 6 exact batches), calls 1-3 and 5 exact
+            assert p["screen_floor_trips"] == 2 and p["screen_floor_batches"] == 4, p
+        else:
+            assert p["screen_floor_trips"] == 0 and p["screen_floor_batches"] == 0, p
 
 
 def test_screen_ties_duplicates_nonfinite_huge_subnormal():

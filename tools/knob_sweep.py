@@ -9,7 +9,9 @@ with VDB_IVF_LIB).
 usage: tools/knob_sweep.py cfg3|cfg4|mix "wide_group=32" "seg_vectors=1024,segs_per_item=8" ...
   cfg4 = rank 0 of the 8-way sharded 100M x 768 index (the per-GPU work of 8 GPUs);
   ip = the cfg3 index with the inner-product metric; s8 = rank 0 of the cfg3 index cut 8 ways
-  (the per-GPU work of the 8-GPU headline)
+  (the per-GPU work of the 8-GPU headline); cancel = the screen's cancellation regime at 2M
+  vectors (test_gpu_screen.py's tiny ball far from the origin, 128-D, two lists whose
+  centroids are far from the ball: every pair a candidate), nprobe 2
 """
 import json
 import os
@@ -24,7 +26,7 @@ import bench  # noqa: E402
 
 DEFAULTS = {"seg_vectors": 0, "segs_per_item": 0, "wide_stride": 1, "fused_scan": 1, "narrow_blocks": 64,
             "wide_group": 16, "fused_merge": 1, "scan_window": 0, "screen": 1, "bounded_stats": 0, "screen_group": 0,
-            "screen_defer": 1, "screen_cand_cap": 4 << 20}
+            "screen_defer": 1, "screen_cand_cap": 4 << 20, "screen_floor_ppm": 5000}
 
 
 def main():
@@ -37,6 +39,8 @@ def main():
     vdb = bench.load_vdb()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if wl == "cancel":
+        return cancel(vdb, dev, sets)
     with torch.cuda.stream(torch.cuda.Stream(dev)):
         if args.data == "mixture":
             args.centers = bench.mixture_centers(vdb, args.nlist, args.nprobe, args.dim, args.mix_spread, dev)
@@ -83,6 +87,49 @@ def main():
                   flush=True)
             for n_, _ in opts:  # back to defaults
                 idx.set_option(n_, DEFAULTS[n_])
+
+
+def cancel(vdb, dev, sets):
+    """The cancellation regime (the bound wider than the whole distance spread) at 2M x 128."""
+    dim, n, B, steps = 128, 2_000_000, 64, 1000
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    c = torch.full((dim,), 100.0 / dim ** 0.5, device=dev)
+    X = (c + 0.01 * torch.randn((n, dim), generator=g, device=dev)).contiguous()
+    Q = (c + 0.01 * torch.randn(((steps + 2) * B, dim), generator=g, device=dev)).contiguous()
+    ids = torch.arange(n, dtype=torch.int64, device=dev)
+    idx = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, 2, max_gpu_memory=0))
+    idx.centroids = torch.stack([torch.zeros_like(c), -c]).cpu().numpy()
+    idx.add_device(X.data_ptr(), ids.data_ptr(), n)
+    st = torch.cuda.current_stream()
+    od = torch.empty((B, 10), dtype=torch.float32, device=dev)
+    oi = torch.empty((B, 10), dtype=torch.int64, device=dev)
+    ref = None
+    for s in sets:
+        opts = [o.split("=") for o in s.split(",") if o]
+        for nm, v in opts:
+            idx.set_option(nm, int(v))
+        for j in range(2):
+            idx.search_device(Q[j * B:].data_ptr(), B, 2, 10, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        p0 = idx.profile_read()
+        t0 = time.perf_counter()
+        for j in range(steps):
+            idx.search_device(Q[(j + 2) * B:].data_ptr(), B, 2, 10, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / steps * 1e3
+        p = idx.profile_read()
+        same = None
+        if ref is None:
+            ref = (od.clone(), oi.clone())
+        else:
+            same = bool(torch.equal(oi, ref[1]) and torch.equal(od.view(torch.int32), ref[0].view(torch.int32)))
+        print(json.dumps({"workload": "cancel", "opts": s, "wall_ms": round(wall, 3),
+                          "floor_batches": p["screen_floor_batches"] - p0["screen_floor_batches"],
+                          "floor_trips": p["screen_floor_trips"] - p0["screen_floor_trips"],
+                          "same_results_as_first": same}), flush=True)
+        for nm, _ in opts:
+            idx.set_option(nm, DEFAULTS[nm])
 
 
 if __name__ == "__main__":
