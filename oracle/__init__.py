@@ -54,6 +54,10 @@ def lib():
             "oracle_search_mt": (None, [vp, _f32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _f32p, _u64p, ctypes.c_int]),
             "oracle_search_shard": (None, [vp, _f32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p, _f32p, _u64p]),
             "oracle_search_shard_mt": (None, [vp, _f32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p, _f32p, _u64p, ctypes.c_int]),
+            "oracle_stream_begin": (vp, [vp, _f32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+            "oracle_stream_probed": (ctypes.c_uint32, [vp, ctypes.c_uint32]),
+            "oracle_stream_scan": (None, [vp, ctypes.c_uint32, ctypes.c_int]),
+            "oracle_stream_finish": (None, [vp, _u8p, _f32p, _u64p]),
             "oracle_merge_ranks": (None, [_f32p, _u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _f32p, _u64p]),
             "oracle_select_nprobe": (None, [vp, _f32p, ctypes.c_uint32, _u32p]),
             "oracle_assign": (None, [vp, _f32p, ctypes.c_uint64, _u32p]),
@@ -143,6 +147,35 @@ class OracleIndex:
             lib().oracle_search_shard_mt(self._h, _p(q, _f32p), n, nprobe, k, _p(o, _u8p), _p(D, _f32p),
                                          _p(I, _u64p), threads)
         return D, I
+
+    def search_shard_streamed(self, queries: np.ndarray, nprobe: int, k: int, owned: np.ndarray, counts,
+                              fill, threads: int = 0):
+        """search_shard over a shard that never sits in the checker's memory whole: every
+        list's count is set (emptiness), then each owned probed list is loaded alone —
+        fill(l, vectors, ids) writes its rows in place — scanned for every query probing it,
+        and dropped. Returns (D, I, vectors loaded)."""
+        q = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, self.dim)
+        o = np.ascontiguousarray(owned, dtype=np.uint8)
+        n = q.shape[0]
+        for l in range(self.nlist):
+            self.set_list_count(l, int(counts[l]))
+        st = lib().oracle_stream_begin(self._h, _p(q, _f32p), n, nprobe, k)
+        loaded = 0
+        try:
+            for l in range(self.nlist):
+                c = int(counts[l])
+                if not (o[l] and c and lib().oracle_stream_probed(st, l)):
+                    continue
+                v, i = self.list_buffers(l, c)
+                fill(l, v, i)
+                lib().oracle_stream_scan(st, l, threads)
+                self.set_list_count(l, c)  # (rows dropped)
+                loaded += c
+        finally:
+            D = np.empty((n, k), dtype=np.float32)
+            I = np.empty((n, k), dtype=np.uint64)
+            lib().oracle_stream_finish(st, _p(o, _u8p), _p(D, _f32p), _p(I, _u64p))
+        return D, I, loaded
 
     def select_nprobe(self, query: np.ndarray, nprobe: int) -> np.ndarray:
         q = np.ascontiguousarray(query, dtype=np.float32)

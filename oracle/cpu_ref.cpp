@@ -358,6 +358,64 @@ void oracle_search_shard_mt(oracle_ivf* h, const float* queries, uint32_t n, uin
         });
 }
 
+// oracle_search_shard_mt with the lists streamed in one at a time (a shard larger than the
+// checker's memory): begin records the call's probes, scan takes the (query, probe) pairs of
+// the one list currently holding rows, finish replays the slot logic. Bit-identical to
+// oracle_search_shard when every owned probed list is scanned once.
+struct oracle_stream {
+    oracle_ivf* h;
+    std::vector<float> queries;
+    uint32_t n, nprobe, P, k;
+    std::vector<std::vector<uint32_t>> probes;
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> pairs_of;  // per list: its (query, probe) pairs
+    std::vector<std::vector<Cand>> res;
+};
+
+oracle_stream* oracle_stream_begin(oracle_ivf* h, const float* queries, uint32_t n, uint32_t nprobe, uint32_t k) {
+    oracle_stream* st = new oracle_stream{h, std::vector<float>(queries, queries + (size_t)n * h->dim), n, nprobe,
+                                          std::min(nprobe, h->nlist), k, {}, {}, {}};
+    st->probes.resize(n);
+    st->pairs_of.resize(h->nlist);
+    st->res.resize((size_t)n * st->P);
+    for (uint32_t q = 0; q < n; ++q) {
+        st->probes[q] = h->select(queries + (size_t)q * h->dim, nprobe);
+        for (uint32_t p = 0; p < st->P; ++p) st->pairs_of[st->probes[q][p]].emplace_back(q, p);
+    }
+    return st;
+}
+
+uint32_t oracle_stream_probed(const oracle_stream* st, uint32_t l) { return (uint32_t)st->pairs_of[l].size(); }
+
+void oracle_stream_scan(oracle_stream* st, uint32_t l, int threads) {
+    const auto& pq = st->pairs_of[l];
+    const uint64_t cnt = st->h->lists[l].count;
+    if (!cnt) return;
+#ifdef _OPENMP
+    int nt = threads > 0 ? threads : omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+#endif
+    for (int64_t e = 0; e < (int64_t)pq.size(); ++e) {
+        const uint32_t q = pq[e].first, p = pq[e].second;
+        st->h->scan_list(l, st->queries.data() + (size_t)q * st->h->dim, std::min<uint64_t>(st->k, cnt),
+                         st->res[(size_t)q * st->P + p]);
+    }
+    (void)threads;
+}
+
+void oracle_stream_finish(oracle_stream* st, const uint8_t* owned, float* D, uint64_t* I) {
+    static const std::vector<Cand> kEmpty;
+    const uint32_t P = st->P, k = st->k;
+    run_search(
+        st->h, st->queries.data(), st->n, st->nprobe,
+        [&](uint32_t q, uint32_t p, uint32_t, const float*, std::vector<Cand>& out) { out = st->res[(size_t)q * P + p]; },
+        [&](uint32_t q, const std::vector<Slot>& slots) {
+            std::vector<const std::vector<Cand>*> ptrs;
+            for (const Slot& s : slots) ptrs.push_back(s.source >= 0 && owned[s.source] ? &s.res : &kEmpty);
+            merge(ptrs, k, D + (size_t)q * k, I + (size_t)q * k);
+        });
+    delete st;
+}
+
 void oracle_merge_ranks(const float* dist, const uint64_t* ids, uint32_t nranks, uint32_t n,
                         uint32_t k, float* out_dist, uint64_t* out_ids) {
     for (uint32_t q = 0; q < n; ++q) {

@@ -47,6 +47,15 @@ void oracle_search_shard(oracle_ivf* h, const float* queries, uint32_t n, uint32
                          uint32_t k, const uint8_t* owned, float* distances, uint64_t* indices);
 void oracle_search_shard_mt(oracle_ivf* h, const float* queries, uint32_t n, uint32_t nprobe, uint32_t k,
                             const uint8_t* owned, float* D, uint64_t* I, int threads);
+/* oracle_search_shard over a shard streamed in one list at a time: begin records the call's
+ * probes (the centroids and every list's count must be set), then for each owned probed list
+ * load its rows (oracle_list_resize), oracle_stream_scan it and drop the rows again
+ * (oracle_list_set_count); finish writes the partials and frees the stream. */
+typedef struct oracle_stream oracle_stream;
+oracle_stream* oracle_stream_begin(oracle_ivf* h, const float* queries, uint32_t n, uint32_t nprobe, uint32_t k);
+uint32_t oracle_stream_probed(const oracle_stream* st, uint32_t list);
+void oracle_stream_scan(oracle_stream* st, uint32_t list, int threads);
+void oracle_stream_finish(oracle_stream* st, const uint8_t* owned, float* distances, uint64_t* indices);
 void oracle_merge_ranks(const float* dist, const uint64_t* ids, uint32_t nranks, uint32_t n,
                         uint32_t k, float* out_dist, uint64_t* out_ids);
 

@@ -164,6 +164,20 @@ def test_count_only_lists_keep_shard_results():
             c.set_list_count(l, len(i))
     Dc, Ic = c.search_shard(Q, 36, 10, owned)
     assert np.array_equal(Ic, I) and np.array_equal(bits(Dc), bits(D))
+    # streamed: one owned probed list holds rows at a time (bench.py's full-shard check)
+    s = oracle.OracleIndex(16, 40, 0)
+    s.centroids = o.centroids
+    counts = [o.list_count(l) for l in range(40)]
+    filled = []
+
+    def fill(l, v, i):
+        filled.append(l)
+        v[...], i[...] = o.get_list(l)
+
+    Ds, Is, loaded = s.search_shard_streamed(Q, 36, 10, owned, counts, fill, threads=3)
+    assert np.array_equal(Is, I) and np.array_equal(bits(Ds), bits(D))
+    assert len(set(filled)) == len(filled) and all(owned[l] for l in filled)
+    assert loaded == sum(counts[l] for l in filled) > 0
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))), ids=os.path.basename)
