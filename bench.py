@@ -769,6 +769,29 @@ def timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, che
     step_ms_single = [a.elapsed_time(b) for a, b in zip(s_ev, e_ev)]
     p99_single = percentile(step_ms_single, 0.99)
     mine = rank_breakdown(rank, prof, elapsed * 1e3 / max(args.steps, 1), step_ms_single)
+    if args.rehearsal:
+        # The ranks of a rehearsal share one GPU: a phase's HIP-event interval on one rank also
+        # holds the other ranks' kernels that run meanwhile. The same local searches once more,
+        # the ranks taking turns (a barrier between them, nothing else on the GPU), give each
+        # rank's own phase times.
+        idx.profile_enable(True)
+        idx.profile_reset()
+        st = streams[0]
+        for j in range(args.prof_steps):
+            q = queries[(args.warmup + args.steps + j) * B:]
+            for r in range(world):
+                dist.barrier()
+                if r == rank:
+                    idx.search_device(q.data_ptr(), B, args.nprobe, k, part[0].data_ptr(), part[0].data_ptr() + ids_off,
+                                      st.cuda_stream)
+                    st.synchronize()
+        dist.barrier()
+        pa = idx.profile_read()
+        idx.profile_enable(False)
+        na = max(pa["scan_launches"], 1)
+        mine["ranks_taking_turns"] = {"scan_ms": round(pa["scan_ms"] / na, 4), "coarse_ms": round(pa["coarse_ms"] / na, 4),
+                                      "local_merge_ms": round(pa.get("local_merge_ms", 0.0) / na, 4),
+                                      "search_ms": round(pa["total_ms"] / na, 4)}
     per_rank = None
     if world > 1:
         t = torch.tensor([p99_single], dtype=torch.float64, device=ctrl)

@@ -4,6 +4,7 @@
 # steps: t:<pytest args, ';'-separated files> | s:<workload>:<opt sets separated by '|'> | b:<bench args>
 #        p:<workload>:<opt sets> (the sweep under rocprofv3 --kernel-trace --stats)
 #        m:<counters ';'-separated>:<workload>:<opt sets> (one rocprofv3 --pmc pass over the sweep)
+#        q:<bench args> (bench.py under rocprofv3 --kernel-trace --stats)
 # Each step runs under its own time limit; a crash (abort, segfault, time limit) ends the
 # session, a failed assertion does not (the next steps still measure).
 set -o pipefail
@@ -32,6 +33,8 @@ for st in "${STEPS[@]}"; do
            IFS='|' read -ra SETS <<< "$sets"
            timeout -s KILL 600 rocprofv3 --pmc ${cnt//;/ } --kernel-include-regex "ivf_screen_collect|ivf_scan_" -d "$O/pmc$i" -o run -f csv -- python3 -u tools/knob_sweep.py "$wl" "${SETS[@]}" > "$O/$i.pmc_$wl.log" 2>&1
            rc=$?; grep '^{' "$O/$i.pmc_$wl.log"; find "$O/pmc$i" -name '*counter_collection.csv' | head -1 ;;
+        q) timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof$i" -o run -- python3 -u bench.py ${arg//;/ } > "$O/$i.qbench.log" 2>&1
+           rc=$?; grep '^{' "$O/$i.qbench.log" | cut -c 1-1500; find "$O/prof$i" -name '*kernel_stats.csv' | head -3 ;;
         b) timeout -k 10 900 python -u bench.py ${arg//;/ } > "$O/$i.bench.log" 2>&1
            rc=$?; grep '^{' "$O/$i.bench.log" | cut -c 1-1500 ;;
     esac
