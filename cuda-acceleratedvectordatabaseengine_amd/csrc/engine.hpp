@@ -302,11 +302,13 @@ struct vdb_ivf {
     // Screened scan (screen.hip, option "screen", on by default): every (query, vector)
     // distance is bounded on the matrix cores from a bf16 shadow of the lists and computed
     // exactly (the reference's sequential fp32 sum) only where it can reach the list's
-    // top-k; results are bit-identical to the exact scan. Built from the arena whenever
-    // the lists change (upload_directory): the shadow in MFMA operand order (half the
-    // arena's bytes), the fp32 rows in slot order for the exact re-checks, per-slot norms.
-    // Not built for the tier (lists not all in HBM), for Cosine, or when the extra 1.5x of
-    // the list bytes does not fit (Config::max_gpu_memory, or a failed allocation).
+    // top-k; results are bit-identical to the exact scan. Built from the arena by the first
+    // search after the lists change: the shadow in MFMA operand order (half the arena's
+    // bytes), the fp32 rows in slot order (then the lists' only fp32 copy: the arena is
+    // released and rebuilt from them on demand), per-slot norms. The tier keeps the shadow,
+    // norms and ids of every stored list resident (screen_update_tier). Not built for
+    // Cosine, or when an allocation fails (the exact scan serves); max_gpu_memory caps list
+    // bytes only.
     bool screen_opt = true;
     bool screen_ready = false;
     bool screen_stale = false;  // lists or centroids changed since the last build
