@@ -444,6 +444,24 @@ def tier_leg(vdb, idx, args, device, queries):
                       "first_call_s_incl_shadow_build": round(t_first, 1),
                       "collect_ms_per_batch": round(prof.get("collect_ms", 0.0) / max(prof["scan_launches"], 1), 3),
                       "search_ms_per_batch": round(prof["total_ms"] / max(prof["scan_launches"], 1), 3)}
+        variants = []
+        for vs in args.tier_variant:  # the same timed calls again under other engine options
+            opts = [o.split("=") for o in vs.split(",") if o]
+            for nm, v in opts:
+                h.set_option(nm, int(v))
+            v0 = h.cache_stats()
+            t0 = time.perf_counter()
+            for j in range(1, calls):
+                h.search_device(queries[j * call:].data_ptr(), call, args.nprobe, args.k, od.data_ptr(), oi.data_ptr(),
+                                st.cuda_stream)
+            torch.cuda.synchronize()
+            ev = time.perf_counter() - t0
+            v1 = h.cache_stats()
+            variants.append({"opts": vs, "value": round(nq / ev, 1),
+                             "survivor_rows_read_per_batch": round((v1["screen_rows_fetched"] - v0["screen_rows_fetched"]) / batches, 1),
+                             "file_read_gbps": round((v1["file_bytes_read"] - v0["file_bytes_read"]) / ev / 1e9, 2)})
+        if variants:
+            screen["variants"] = variants
         return {"value": round(nq / el, 1), "unit": "queries/s", "calls": calls - 1, "queries_per_call": call, **screen,
                 "file": path, "file_gb": round(file_bytes / 1e9, 2), "save_s": round(t_save, 1),
                 "lists_gb": round(shard_bytes / 1e9, 2),
@@ -580,6 +598,8 @@ def main():
                     help="> 0: also serve the index from a file through the list-cache tier with this HBM cache")
     ap.add_argument("--tier-call", type=int, default=512, help="queries per search call in the tier leg")
     ap.add_argument("--tier-calls", type=int, default=8)
+    ap.add_argument("--tier-variant", action="append", default=[], metavar="NAME=V[,NAME=V]",
+                    help="tier leg: time the same calls again with these engine options (repeatable)")
     ap.add_argument("--tier-dir", default="", help="directory for the tier leg's index file (default: TMPDIR)")
     ap.add_argument("--host-api", action="store_true",
                     help="also time the host API (vdb_ivf_search) from --host-threads caller threads")

@@ -680,9 +680,15 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "screen_floor_min") {
             require(value >= 0, "screen_floor_min is >= 0");
             h->screen_floor_min = (uint64_t)value;
+        } else if (n == "screen_thr_every") {
+            require(value >= 0 && value <= 1024, "screen_thr_every is 0 (automatic) .. 1024");
+            h->screen_thr_every = (uint32_t)value;
         } else if (n == "screen_floor_skip") {
             require(value >= 1 && value < (1ll << 20), "screen_floor_skip is 1 .. 2^20");
             h->screen_floor_skip = (uint32_t)value;
+        } else if (n == "tier_row_qd") {
+            require(value >= 1 && value <= 4096, "tier_row_qd is 1 .. 4096");
+            h->tier_row_qd = (uint32_t)value;
         } else if (n == "tier_row_direct") {
             h->tier_row_direct = value != 0;
         } else if (n == "screen_group") {

@@ -314,6 +314,7 @@ struct vdb_ivf {
     bool screen_stale = false;  // lists or centroids changed since the last build
     uint32_t screen_segs_auto = 4;  // segments per screened wide item (upload_directory; option segs_per_item)
     uint32_t screen_group = 0;      // queries per screened wide item at most: 16 or 32, 0 = automatic (option screen_group)
+    uint32_t screen_thr_every = 0;  // deferred collect: blocks between re-reads of the shared thresholds, 0 = automatic (option screen_thr_every)
     // Deferred re-checks (option screen_defer, default 1): the scan only collects candidates
     // against upper-bound thresholds; survivors of each pair's final threshold are re-checked
     // exactly afterwards from the arena (screen.hip ivf_screen_collect). 0: the inline kernel
@@ -341,7 +342,7 @@ struct vdb_ivf {
     DevBuf<float> fetch_stage;         // tier, file home: page-locked staging of the survivors' rows
     DevBuf<char> fetch_bounce;         // ... O_DIRECT reads: 4 KiB-aligned supersets, one slot per read in flight
     bool tier_row_direct = true;       // option tier_row_direct: survivor rows with O_DIRECT (no page cache)
-    static constexpr uint32_t kRowQD = 256;  // survivor-row reads in flight (their own ring)
+    uint32_t tier_row_qd = 256;        // option tier_row_qd: survivor-row reads in flight (their own ring)
     std::unique_ptr<UringReader> row_uring;
     DevBuf<float> fetch_dev;           // ... on the device ([n][dim], padded into the slot's srows)
     std::vector<uint2> fetch_surv;     // ... their (slot, pair)
@@ -1051,14 +1052,15 @@ struct vdb_ivf {
         HIPCHECK(hipStreamSynchronize(s));
         fetch_stage.host = true;
         float* st = fetch_stage.ensure((size_t)std::max<uint32_t>(n, 1) * dim);
-        if (!row_uring) row_uring.reset(new UringReader(kRowQD));
+        if (row_uring && row_uring->capacity() < tier_row_qd) row_uring.reset();
+        if (!row_uring) row_uring.reset(new UringReader(tier_row_qd));
         UringReader* const ur = row_uring.get();
         const uint64_t row_bytes = (uint64_t)dim * 4;
         // O_DIRECT (where the file system allows it): each read is the 4 KiB-aligned superset
         // of the row into a bounce slot, copied out on completion; else a buffered read
         // straight into the staging
         const bool direct = tier_row_direct && home_fd_direct >= 0;
-        constexpr uint32_t kQD = kRowQD;
+        const uint32_t kQD = std::min(tier_row_qd, row_uring->capacity());
         const uint64_t span = ((row_bytes + 4095) / 4096 + 1) * 4096;
         char* bounce = nullptr;
         if (direct) {
@@ -1070,11 +1072,27 @@ struct vdb_ivf {
         for (uint32_t i = 0; i < kQD; ++i) free_slots[i] = kQD - 1 - i;
         std::vector<uint64_t> delta(kQD);
         uint64_t bytes_read = 0;
+        // one read per distinct row (a row surviving for several queries is read once), issued
+        // in file order; the duplicates are copied from the first reader's staging row
+        std::vector<uint32_t> order(n);
+        for (uint32_t i = 0; i < n; ++i) order[i] = i;
+        std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+            return fetch_surv[x].x != fetch_surv[y].x ? fetch_surv[x].x < fetch_surv[y].x : x < y;
+        });
+        std::vector<uint32_t> uniq;
+        std::vector<std::pair<uint32_t, uint32_t>> dups;  // (survivor, survivor holding its row)
+        uniq.reserve(n);
+        for (uint32_t t = 0; t < n; ++t) {
+            if (t && fetch_surv[order[t]].x == fetch_surv[order[t - 1]].x) dups.push_back({order[t], uniq.back()});
+            else uniq.push_back(order[t]);
+        }
+        const uint32_t nu = (uint32_t)uniq.size();
         uint32_t next = 0, done = 0;
         try {
-            while (done < n) {
-                while (next < n && next - done < std::min(ur->capacity(), kQD)) {  // (<= kQD queued or in flight)
-                    const uint64_t slot = fetch_surv[next].x;
+            while (done < nu) {
+                while (next < nu && next - done < kQD) {  // (<= kQD queued or in flight)
+                    const uint32_t si = uniq[next];
+                    const uint64_t slot = fetch_surv[si].x;
                     const uint32_t l = sblist_host[slot >> 6];
                     const uint64_t r = slot - sblock_off[l] * 64;
                     const uint64_t off = file_off[l] + count[l] * 8 + r * row_bytes;
@@ -1083,12 +1101,12 @@ struct vdb_ivf {
                         free_slots.pop_back();
                         const uint64_t a0 = off & ~4095ull, a1 = (off + row_bytes + 4095) & ~4095ull;
                         delta[b] = off - a0;
-                        slot_of[b] = next;
+                        slot_of[b] = si;
                         ur->read(home_fd_direct, bounce + (size_t)b * span, (uint32_t)(a1 - a0), a0,
-                                 ((uint64_t)b << 32) | next);
+                                 ((uint64_t)b << 32) | si);
                         bytes_read += a1 - a0;
                     } else {
-                        ur->read(home_fd, st + (size_t)next * dim, (uint32_t)row_bytes, off, next);
+                        ur->read(home_fd, st + (size_t)si * dim, (uint32_t)row_bytes, off, si);
                         bytes_read += row_bytes;
                     }
                     ++next;
@@ -1111,8 +1129,9 @@ struct vdb_ivf {
             ur->drain();
             throw;
         }
-        screen_rows_fetched += n;
-        screen_row_bytes += (uint64_t)n * row_bytes;
+        for (const auto& d : dups) std::memcpy(st + (size_t)d.first * dim, st + (size_t)d.second * dim, row_bytes);
+        screen_rows_fetched += nu;
+        screen_row_bytes += (uint64_t)nu * row_bytes;
         file_bytes_read += bytes_read;  // (with O_DIRECT: the aligned supersets the device delivered)
         float* rows = slot_buf(w, w.srows, (size_t)std::max<uint32_t>(n, 1) * dp);
         if (n) {
@@ -2101,6 +2120,10 @@ struct vdb_ivf {
             sa.P = P;
             sa.segs_item = segs_screen;
             sa.wide_q = swq;
+            // (32-query items run one workgroup per CU, so a shared-threshold read's latency is
+            // exposed: re-read every 4 blocks, cfg4 shard collect 4.14 -> 3.87 ms; 16-query
+            // items hide it and keep the freshest value, 1/8 shard 0.543 vs 0.552 ms)
+            sa.thr_every = screen_thr_every ? screen_thr_every : (swq == 32 ? 4u : 1u);
             if (tiered()) {  // the resident shadow's packing and ids; rows from the home
                 sa.block_off = d_sblock_off.p;
                 sa.ids = screen_ids.p;

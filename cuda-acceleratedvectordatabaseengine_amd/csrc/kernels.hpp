@@ -137,6 +137,7 @@ struct ScanArgs {
     uint32_t dp = 0;
     uint32_t P = 0;
     uint32_t wide_q = 16;  // queries per screened wide item at most (16 or 32)
+    uint32_t thr_every = 1;  // deferred screen: blocks between re-reads of the shared (global) thresholds
     uint32_t* thr4 = nullptr;  // per sorted pair, 4 quarter-list thresholds (screen.hip)
     // Deferred screened scan: collected (sorted pair, slot, lower bound, rank) entries, their
     // capacity, the collection counter (counters + kCtrCand) and per sorted pair the overflow mark.

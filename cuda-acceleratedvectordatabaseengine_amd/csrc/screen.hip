@@ -718,6 +718,15 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
     for (int gg = 0; gg < NG; ++gg)
         qa_row[gg] = (const uint4*)(a.qres + (size_t)pair_of(min(16 * gg + (lane & 15), nq - 1)) * dp) + (lane >> 4);
     uint32_t collected = 0;
+    // the shared thresholds (list-wide k-th, quarter slots) as last read: re-read every
+    // thr_every blocks (a stale value is larger, so only looser: still valid) so their
+    // latency is not paid by every block
+    float gthr[NG][4], gq4[NG][4];  // (and this wave's quarter slot)
+#pragma unroll
+    for (int gg = 0; gg < NG; ++gg)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gthr[gg][r] = gq4[gg][r] = __builtin_inff();
+    const uint32_t thr_every = a.thr_every;
 
     const uint4* sp = a.shadow + b0 * (uint64_t)dp * 8 + lane;
     uint4 xa[KD][4], qa[NG][KD];
@@ -809,16 +818,23 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                 }
                 uint32_t* gt = a.thr + spi;
                 uint32_t* s4 = a.thr4 + (size_t)spi * 4;
-                const uint4 t4 = *(const uint4*)s4;
-                const float th4 = fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w)));
-                const float cur = fminf(fminf(ord_dec(*gt), th4), ord_dec(s_thr[gc]));
+                if (j % thr_every == 0) {
+                    const uint4 t4 = *(const uint4*)s4;
+                    const float th4 = fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w)));
+                    gthr[gg][r] = fminf(ord_dec(*gt), th4);
+                    const uint32_t m4 = residue == 0 ? t4.x : residue == 1 ? t4.y : residue == 2 ? t4.z : t4.w;
+                    gq4[gg][r] = ord_dec(m4);
+                }
+                const float cur = fminf(gthr[gg][r], ord_dec(s_thr[gc]));
                 if ((lane & 15) == 0 && g < nq) {
                     if (tw < cur) {
                         atomicMin(&s_thr[g], ord_enc(tw));
                         atomicMin(gt, ord_enc(tw));
                     }
-                    if (tq < ord_dec(s4[residue])) atomicMin(s4 + residue, ord_enc(tq));
+                    if (tq < gq4[gg][r]) atomicMin(s4 + residue, ord_enc(tq));
                 }
+                gthr[gg][r] = fminf(gthr[gg][r], tw);
+                gq4[gg][r] = fminf(gq4[gg][r], tq);
                 th[r] = g < nq ? fminf(tw, cur) : -__builtin_inff();
             }
             // candidates: one atomic per block and group for the wave's whole batch of them
@@ -1205,7 +1221,8 @@ __global__ __launch_bounds__(256) void ivf_screen_pair_topk(ScanArgs a, const ui
         }
         if (lane == 0) nseg_qp[(size_t)q * a.P + p] = 1u;
     }
-    const uint64_t tasks = (uint64_t)nvalid * smax;
+    // (no pair overflowed unless the batch collected more candidates than the buffer holds)
+    const uint64_t tasks = a.counters[kCtrCand] > a.cand_cap ? (uint64_t)nvalid * smax : 0;
     const uint32_t segv = a.seg_blocks * 64;
     for (uint64_t t = wv; t < tasks; t += nw) {
         const uint32_t s = (uint32_t)(t % nvalid), j = (uint32_t)(t / nvalid);
@@ -1318,8 +1335,8 @@ void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uin
     (void)raised;
     const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>(16384, (max_surv + kExactRows - 1) / kExactRows));
     const size_t lds = exact_lds(a.d4);
-    // (waves enough for the pairs, and for the (pair, segment) tasks of overflowed pairs)
-    const uint32_t gp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, ((uint64_t)BP * smax + 3) / 4));
+    // (a wave per pair, and at least 2048 waves for the (pair, segment) tasks of overflowed pairs)
+    const uint32_t gp = std::max<uint32_t>(512, std::min<uint32_t>(2048, (BP + 3) / 4));
     const int src = fetched ? 1 : (a.rows ? 0 : 2);
     auto exact = [&](auto m_c) {
         constexpr int Mm = decltype(m_c)::value;
