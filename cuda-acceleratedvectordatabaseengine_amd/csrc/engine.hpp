@@ -845,12 +845,11 @@ struct vdb_ivf {
             seg_blocks = seg_blocks_opt;
         } else {
             seg_blocks = 8;  // 512 vectors at most by default (1024 is an explicit option)
-            // (The deferred screen keeps 512 for large shards; a small one (the 1/8 shard of the
-            // 10M x 768 index: 1.25M vectors) gets 256-vector segments in items of 4, enough
-            // items to fill the chip: collect 0.43 vs 0.50 ms; the full 10M index and the cfg4
-            // shard are 4-6 % slower with them. The inline screen measured 512 x 8 best.)
+            // (The screen keeps 512 at every shard size. 256-vector segments in items of 4 made
+            // the 1/8 shard's one-in-flight scan faster (0.549 vs 0.575 ms) but its batches at
+            // 3 in flight slower (0.47 vs 0.41 ms per step over the 8 emulated ranks: more
+            // items, partials and merge work per batch), so throughput keeps 512.)
             const bool screen_may = screen_opt && metric != 2;
-            if (screen_may && screen_defer && local < (4ull << 20)) seg_blocks = 4;
             while (!screen_may && seg_blocks > 1 && local / ((uint64_t)seg_blocks * 64) < 4096) seg_blocks >>= 1;
         }
         std::vector<uint32_t> cl(nlist), cg(nlist), ns(nlist);
@@ -879,7 +878,6 @@ struct vdb_ivf {
             }
             const double mean_seg = wsum > 0 ? wseg / wsum : 0.0;
             screen_segs_auto = mean_seg < 16.0 ? 4u : (mean_seg < 96.0 ? 8u : 16u);
-            if (seg_blocks == 4 && screen_defer && !seg_blocks_opt) screen_segs_auto = 4;  // (the small-shard choice)
         }
         std::vector<uint32_t> sorted(ns);
         std::sort(sorted.begin(), sorted.end(), std::greater<uint32_t>());
