@@ -49,14 +49,18 @@ def summarise(d, batches, key):
             dispatches[name].add(row.get("Dispatch_Id", ""))
     scan = {k: v for k, v in per_kernel.items() if "ivf_scan" in k or "ivf_screen_collect" in k}
     kib = sum(scan.values())
+    # the deferred screen: one collect dispatch per batch, whatever else the command ran
+    ncol = sum(len(v) for k, v in dispatches.items() if "ivf_screen_collect" in k)
+    if ncol:
+        batches = ncol
     return {
         "workload": key,
         "build_id": build_id(),
         "hbm_bytes_per_scan_launch": int(kib * 1024.0 * 2.0 / batches),
         "source": "rocprofv3 --pmc FETCH_SIZE (KiB, x2 gfx950 correction) summed over the ivf_scan_* "
-                  f"dispatches of {batches} batches",
+                  f"and ivf_screen_collect dispatches of {batches} batches",
         "per_kernel_bytes_per_batch": {k: int(v * 2048 / batches) for k, v in scan.items()},
-        "dispatches": {k: len(v) for k, v in dispatches.items() if "ivf_scan" in k},
+        "dispatches": {k: len(v) for k, v in dispatches.items() if "ivf_scan" in k or "ivf_screen_collect" in k},
     }
 
 

@@ -36,13 +36,17 @@ TJ="$O/traffic.json"
 [[ ",$STEPS," == *",traffic"* ]] || TJ="$R/profiles/traffic.json"
 CFG4="--cfg cfg4 --emulate-shard 8 --no-cpu --inflight 3"
 if has traffic; then
-    run pmc_iid 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ivf_scan_ -d "$O/pmc_iid" -o f -f csv -- python3 bench.py $SHORT
-    run pmc_mix 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ivf_scan_ -d "$O/pmc_mix" -o f -f csv -- python3 bench.py $SHORT --data mixture
+    run pmc_iid 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ivf_scan_|ivf_screen_collect" -d "$O/pmc_iid" -o f -f csv -- python3 bench.py $SHORT
+    run pmc_mix 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ivf_scan_|ivf_screen_collect" -d "$O/pmc_mix" -o f -f csv -- python3 bench.py $SHORT --data mixture
     python3 tools/pmc_traffic.py "$O/traffic.json" "$O/pmc_iid" 8 "10000000x768/4096/32/64/10/N1" \
         "$O/pmc_mix" 8 "10000000x768/4096/32/64/10/N1/mixture" | tail -3
 fi
+if has traffic8; then
+    run pmc_emu8 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ivf_scan_|ivf_screen_collect" -d "$O/pmc_emu8" -o f -f csv -- python3 bench.py $SHORT --emulate-shard 8 --inflight 3
+    python3 tools/pmc_traffic.py "$O/traffic.json" "$O/pmc_emu8" 8 "10000000x768/4096/32/64/10/N1/shard0of8" | tail -3
+fi
 if has traffic4; then
-    run pmc_cfg4 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex ivf_scan_ -d "$O/pmc_cfg4" -o f -f csv -- python3 bench.py $CFG4 --steps 5 --warmup 1 --prof-steps 2
+    run pmc_cfg4 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ivf_scan_|ivf_screen_collect" -d "$O/pmc_cfg4" -o f -f csv -- python3 bench.py $CFG4 --steps 5 --warmup 1 --prof-steps 2
     python3 tools/pmc_traffic.py "$O/traffic.json" "$O/pmc_cfg4" 8 "100000000x768/16384/64/64/10/N1/shard0of8" | tail -3
 fi
 if has mfma; then
