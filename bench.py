@@ -1079,13 +1079,16 @@ def run(vdb, args, device, rank, world):
     deferred = screened and prof.get("collect_ms", 0) > 0
     dp = -(-args.dim // 64) * 64
     collect_ms = prof.get("collect_ms", 0.0) / launches
+    # the deferred screen's shadow: bf16 (default), or int8 + a 4 B scale per vector (option screen_i8=1)
+    shadow_i8 = deferred and "screen_i8=1" in args.opt
+    shadow_b = dp + 4 if shadow_i8 else 2 * dp
     if deferred:
         # the dominant kernel is the deferred screen's collect pass: it streams the shadow and
         # the norms and writes 16 B per collected (query, vector) pair; the exact re-checks
         # after it read 4 dp B per survivor (reported beside it)
         vecs = prof["scan_vectors"] / batches
         collected = prof.get("screen_collected", 0) / batches
-        bytes_per_launch = vecs * (2 * dp + 16) + collected * 16
+        bytes_per_launch = vecs * (shadow_b + 16) + collected * 16
         kernel_ms = collect_ms
     elif screened:
         vecs = prof["scan_vectors"] / batches
@@ -1141,8 +1144,10 @@ def run(vdb, args, device, rank, world):
         "roofline": {
             "bound": "hbm",
             "kernel": "ivf_screen_collect" if deferred else ("ivf_scan_screen" if screened else "ivf_scan_wide"),
-            "bytes_model": ("deferred screen, collect kernel: 2 dp B bf16 shadow + 16 B norms per vector of the "
-                            "distinct probed lists + 16 B per collected (query, vector) candidate" if deferred else
+            "bytes_model": ((("deferred screen, collect kernel: dp B int8 shadow + 4 B scale" if shadow_i8 else
+                              "deferred screen, collect kernel: 2 dp B bf16 shadow") +
+                             " + 16 B norms per vector of the distinct probed lists + 16 B per collected (query, vector) "
+                             "candidate") if deferred else
                             "screened: 2 dp B bf16 shadow + 16 B norms per vector of the distinct probed lists "
                             "+ 4 dp B per exactly re-checked (query, vector) pair" if screened else
                             "exact: 4 D B per vector of the distinct probed lists"),

@@ -668,6 +668,11 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->quiesce();
             h->screen_defer = value != 0;
             h->screen_update();
+        } else if (n == "screen_i8") {
+            h->set_device();
+            h->quiesce();
+            h->screen_i8 = value != 0;
+            h->screen_update();
         } else if (n == "screen_cand_cap") {
             require(value >= 1024 && value <= (1ll << 30), "screen_cand_cap is 1024 .. 2^30");
             h->set_device();

@@ -314,6 +314,14 @@ struct vdb_ivf {
     bool screen_stale = false;  // lists or centroids changed since the last build
     uint32_t screen_segs_auto = 4;  // segments per screened wide item (upload_directory; option segs_per_item)
     uint32_t screen_group = 0;      // queries per screened wide item at most: 16 or 32, 0 = automatic (option screen_group)
+    // Shadow format of the deferred screen (option screen_i8): 1 = int8 with a per-vector scale
+    // (half the bf16 shadow's bytes, a ~4.6x wider bound); 0 (default) = bf16. Measured on the
+    // same box: the int8 collect is VALU-bound (bounds and candidate appends per pair, not
+    // bytes): cfg3 collect 2.12 vs 2.49 ms but 6.3x the re-checks (0.58 vs 0.17 ms), scan 2.72
+    // vs 2.67 ms; cfg4 shard 4.29 vs 4.09 ms; 1/8 shard 0.523 vs 0.560 ms. The inline kernel
+    // (screen_defer 0) always uses bf16.
+    bool screen_i8 = false;
+    bool want_i8() const { return screen_i8 && screen_defer; }
     uint32_t screen_thr_every = 0;  // deferred collect: blocks between re-reads of the shared thresholds, 0 = automatic (option screen_thr_every)
     // Deferred re-checks (option screen_defer, default 1): the scan only collects candidates
     // against upper-bound thresholds; survivors of each pair's final threshold are re-checked
@@ -394,6 +402,8 @@ struct vdb_ivf {
     DevBuf<uint4> screen_sh;
     DevBuf<float> screen_rows;
     DevBuf<float4> screen_meta;
+    DevBuf<float> screen_scale;  // int8 shadow: per slot s_b
+    bool screen_fmt_i8 = false;  // the shadow built is int8 (else bf16)
     DevBuf<uint32_t> screen_blist;  // the list of every arena block (residuals against its centroid)
 
     // List-cache tier (option list_cache_bytes > 0), the reference's residency model
@@ -467,6 +477,7 @@ struct vdb_ivf {
         DevBuf<vdbk::ScanItem> items{true}, items_w{true};
         DevBuf<uint16_t> qres{true};  // screened scan: per (query, probe) bf16 A rows [B * P][dp]
         DevBuf<float4> pst{true};     // ... and their norms
+        DevBuf<float> qscale{true};   // ... and (int8 shadow) their scales
         DevBuf<uint32_t> thr4{true};  // ... and, per sorted pair, 4 quarter-list thresholds
         // deferred screened scan: collected candidates, per sorted pair survivor counts, offsets and
         // overflow marks, the survivors' slots grouped per pair, and (tier) their fetched rows
@@ -493,7 +504,7 @@ struct vdb_ivf {
                                sorted_pair.device_bytes(), pbs.device_bytes(), counters.device_bytes(),
                                l1base.device_bytes(), cand.device_bytes(), thr.device_bytes(), l1_items.device_bytes(),
                                l1_d.device_bytes(), l1_i.device_bytes(), items.device_bytes(), items_w.device_bytes(),
-                               qres.device_bytes(), pst.device_bytes(), thr4.device_bytes(), scand.device_bytes(),
+                               qres.device_bytes(), pst.device_bytes(), qscale.device_bytes(), thr4.device_bytes(), scand.device_bytes(),
                                scnt.device_bytes(), soff.device_bytes(), ovf.device_bytes(), ubcnt.device_bytes(),
                                surv.device_bytes(), ublist.device_bytes(), sdist.device_bytes(), srows.device_bytes(),
                                xrec.device_bytes(), xgat.device_bytes(), gq.device_bytes(), greq.device_bytes()})
@@ -624,7 +635,8 @@ struct vdb_ivf {
         for (uint64_t x : {cent_rm.device_bytes(), cent_il.device_bytes(), arena.device_bytes(), arena_ids.device_bytes(),
                            d_block_off.device_bytes(), d_count_local.device_bytes(), d_count_global.device_bytes(),
                            d_nseg.device_bytes(), screen_sh.device_bytes(), screen_rows.device_bytes(),
-                           screen_meta.device_bytes(), screen_blist.device_bytes(), cache.device_bytes(),
+                           screen_meta.device_bytes(), screen_blist.device_bytes(), screen_scale.device_bytes(),
+                           screen_ids.device_bytes(), d_sblock_off.device_bytes(), cache.device_bytes(),
                            cache_ids.device_bytes(), drows.device_bytes(), dpad.device_bytes(), drows_cs.device_bytes(),
                            dpad_cs.device_bytes(), out_d.device_bytes(), qin.device_bytes(), out_i.device_bytes(),
                            d_req.device_bytes(), stats.device_bytes()})
@@ -907,6 +919,7 @@ struct vdb_ivf {
         screen_sh.release();
         screen_rows.release();
         screen_meta.release();
+        screen_scale.release();
         screen_blist.release();
         screen_ids.release();
         d_sblock_off.release();
@@ -936,11 +949,18 @@ struct vdb_ivf {
         for (uint32_t l = 0; l < nlist; ++l)
             if (owned[l])
                 for (uint64_t b = 0; b < list_blocks(l); ++b) blist[block_off[l] + b] = l;
+        const bool i8 = want_i8();
+        if (i8 != screen_fmt_i8) {  // (a shadow of the other format: its buffers are sized for that)
+            screen_sh.release();
+            screen_scale.release();
+        }
+        screen_fmt_i8 = i8;
         try {
-            screen_sh.ensure(vdbk::screen_shadow_u4(arena_blocks, d4));
+            screen_sh.ensure(vdbk::screen_shadow_u4(arena_blocks, d4, i8));
             screen_rows.ensure((size_t)arena_blocks * 64 * dp);
             screen_meta.ensure((size_t)arena_blocks * 64);
             screen_blist.ensure(arena_blocks);
+            if (i8) screen_scale.ensure((size_t)arena_blocks * 64);
         } catch (const VdbError&) {  // no room for it: the exact scan serves
             (void)hipGetLastError();
             screen_release();
@@ -948,7 +968,7 @@ struct vdb_ivf {
         }
         HIPCHECK(hipMemcpyAsync(screen_blist.p, blist.data(), arena_blocks * 4, hipMemcpyHostToDevice, stream));
         vdbk::launch_screen_build(arena.p, arena_blocks, d4, screen_blist.p, cent_rm.p, screen_sh.p, screen_rows.p,
-                                  screen_meta.p, stream);
+                                  screen_meta.p, stream, i8 ? screen_scale.p : nullptr);
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipStreamSynchronize(stream));
         screen_ready = true;
@@ -976,8 +996,11 @@ struct vdb_ivf {
         for (uint32_t l = 0; l < nlist; ++l)
             if (owned[l] && count[l])
                 for (uint64_t b = 0; b < list_blocks(l); ++b) blist[sblock_off[l] + b] = l;
+        const bool i8 = want_i8();
+        screen_fmt_i8 = i8;
         try {
-            screen_sh.ensure(vdbk::screen_shadow_u4(nb, d4));
+            screen_sh.ensure(vdbk::screen_shadow_u4(nb, d4, i8));
+            if (i8) screen_scale.ensure((size_t)nb * 64);
             screen_meta.ensure((size_t)nb * 64);
             screen_blist.ensure(nb);
             screen_ids.ensure((size_t)(nb + 1) * 64);
@@ -991,7 +1014,7 @@ struct vdb_ivf {
         HIPCHECK(hipMemcpyAsync(d_sblock_off.p, sblock_off.data(), nlist * 8, hipMemcpyHostToDevice, stream));
         if (!file_home()) {
             vdbk::launch_screen_build(arena.p, nb, d4, screen_blist.p, cent_rm.p, screen_sh.p, nullptr, screen_meta.p,
-                                      stream);
+                                      stream, i8 ? screen_scale.p : nullptr);
             HIPCHECK(hipMemcpyAsync(screen_ids.p, arena_ids.p, nb * 64 * 8, hipMemcpyHostToDevice, stream));
         } else {
             // groups of consecutive stored lists through a device block buffer of <= 1 GiB
@@ -1008,7 +1031,8 @@ struct vdb_ivf {
                 HIPCHECK(hipMemsetAsync(tv.p, 0, (gend - g0) * d4 * 64 * sizeof(float4), stream));
                 load_lists(loads, stream, tv.p, ti.p);
                 vdbk::launch_screen_build(tv.p, gend - g0, d4, screen_blist.p + g0, cent_rm.p,
-                                          screen_sh.p + g0 * (uint64_t)d4 * 32, nullptr, screen_meta.p + g0 * 64, stream);
+                                          screen_sh.p + g0 * (uint64_t)d4 * (i8 ? 16 : 32), nullptr, screen_meta.p + g0 * 64,
+                                          stream, i8 ? screen_scale.p + g0 * 64 : nullptr);
                 HIPCHECK(hipGetLastError());
                 HIPCHECK(hipMemcpyAsync(screen_ids.p + g0 * 64, ti.p, (gend - g0) * 64 * 8, hipMemcpyDeviceToDevice,
                                         stream));
@@ -2040,7 +2064,8 @@ struct vdb_ivf {
         // batch: cfg4 shard collect 4.45 vs 4.69 ms; 16 below: cfg3 2.54 vs 2.72 ms)
         const uint32_t sg_want = screen_group ? screen_group : (screen_defer && P >= 64 ? 32u : 16u);
         const uint32_t swq = sg_want == 32 && (screen_defer || vdbk::scan_screen_fits(k, dp, 32)) ? 32u : 16u;
-        bool screened = screen_ready && (!tiered() || screen_defer) && regs_k == 1 && metric != 2 &&
+        bool screened = screen_ready && (!tiered() || screen_defer) && (screen_defer || !screen_fmt_i8) &&
+                        regs_k == 1 && metric != 2 &&
                         vdbk::scan_screen_fits(k, dp, swq);
         bool floor_retry = false;
         if (screened && !tiered() && screen_defer) {  // the run-time floor (lists in HBM only)
@@ -2081,6 +2106,7 @@ struct vdb_ivf {
         if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
         if (screened) {
             const bool defer = screen_defer;
+            const bool i8s = defer && screen_fmt_i8;  // (int8 shadow: built only for the deferred scan)
             // (the tier's file home reads the survivors' rows on the host: the batch then
             // waits for its selection, and re-runs with a larger buffer if it overflowed)
             const bool tier_file = tiered() && file_home();
@@ -2104,7 +2130,7 @@ struct vdb_ivf {
                                           slot_buf(w, w.qres, (size_t)BP * dp), slot_buf(w, w.pst, BP),
                                           slot_buf(w, w.thr4, (size_t)BP * 4), s, defer ? w.scnt.p : nullptr,
                                           defer ? w.ovf.p : nullptr, defer ? w.counters.p : nullptr,
-                                          defer ? w.ubcnt.p : nullptr);
+                                          defer ? w.ubcnt.p : nullptr, i8s ? slot_buf(w, w.qscale, BP) : nullptr);
             };
             if (defer) alloc_defer();
             pairs();
@@ -2112,6 +2138,8 @@ struct vdb_ivf {
             sa.shadow = screen_sh.p;
             sa.rows = screen_rows.p;
             sa.meta = screen_meta.p;
+            sa.sscale = i8s ? screen_scale.p : nullptr;
+            sa.qscale = i8s ? w.qscale.p : nullptr;
             sa.qres = w.qres.p;
             sa.pst = w.pst.p;
             sa.dp = dp;

@@ -134,6 +134,8 @@ struct ScanArgs {
     const float4* __restrict__ meta = nullptr;
     const uint16_t* __restrict__ qres = nullptr;
     const float4* __restrict__ pst = nullptr;
+    const float* __restrict__ sscale = nullptr;  // int8 shadow (deferred screen): per slot s_b (null: bf16)
+    const float* __restrict__ qscale = nullptr;  // ... per (query, probe) pair s_a
     uint32_t dp = 0;
     uint32_t P = 0;
     uint32_t wide_q = 16;  // queries per screened wide item at most (16 or 32)
@@ -162,14 +164,14 @@ bool scan_bounded_fits(uint32_t d4, uint32_t k);
 void launch_scan_bounded(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
 // ---- screened scan (screen.hip): L2 / IP, k <= 64, lists in HBM ----
 bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq);
-size_t screen_shadow_u4(uint64_t blocks, uint32_t d4);  // shadow size (uint4) incl. the prefetch slack
+size_t screen_shadow_u4(uint64_t blocks, uint32_t d4, bool i8 = false);  // shadow size (uint4) incl. the prefetch slack
 void launch_screen_build(const float4* arena, uint64_t blocks, uint32_t d4, const uint32_t* block_list,
-                         const float* cent_rm, uint4* shadow, float* rows, float4* meta, hipStream_t s);
+                         const float* cent_rm, uint4* shadow, float* rows, float4* meta, hipStream_t s, float* sscale = nullptr);
 // scnt / ovf / counters (the deferred scan; null for the inline one) are reset too.
 void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, const uint32_t* probes,
                          const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, uint32_t* thr4, hipStream_t s,
                          uint32_t* scnt = nullptr, uint32_t* ovf = nullptr, uint32_t* counters = nullptr,
-                         uint32_t* ubcnt = nullptr);
+                         uint32_t* ubcnt = nullptr, float* qscale = nullptr);
 void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
 // Deferred screened scan: collect (a.cand), then select (each pair's final threshold, the
 // survivors of it grouped per pair in surv with offsets soff[0 .. nvalid] and their count in

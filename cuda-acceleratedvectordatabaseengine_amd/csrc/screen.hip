@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <type_traits>
 
 #include "kernels.hpp"
 #include "scan_common.hpp"
@@ -50,6 +51,7 @@ namespace vdbk {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 constexpr float kScreenHuge = 1125899906842624.0f;  // 2^50: larger magnitudes are never screened
 constexpr int kRing = 512;                          // candidate ring entries per wave
@@ -195,6 +197,157 @@ __global__ __launch_bounds__(256) void ivf_screen_pairs(const float* __restrict_
     }
 }
 
+// ---- the int8 shadow (deferred screen, option screen_i8): per vector a scale
+// s_b = max_i |x_i - c_i| / 127 (rounded up) and q_b = rint((x - c) / s_b) in [-127, 127], so
+// b' = s_b q_b; in the B-operand order of v_mfma_i32_16x16x64_i8: per k-step s (64 dims) and
+// vector tile vt, lane l holds vector 16 vt + (l & 15), dims 64 s + 16 (l >> 4) .. + 16 (A and B
+// share the instruction's lane -> k map, so the same dims in the same slots of both make the
+// full dot product whatever that map is). Half the bf16 shadow's bytes; |b - b'| is measured
+// exactly (double) as for bf16 and is about 4.6x larger on Gaussian residuals. The integer
+// products and sums are exact (|dot| <= 127^2 dp < 2^24, also exact as a float).
+__device__ __forceinline__ float i8_scale(float mx) { return mx > 0.0f ? mx * (1.0f / 127.0f) * (1.0f + 0x1p-20f) : 0.0f; }
+__device__ __forceinline__ int i8_q(float r, float inv) { return max(-127, min(127, (int)rintf(r * inv))); }
+
+__global__ __launch_bounds__(256) void ivf_screen_build_i8(const float4* __restrict__ arena, uint64_t blocks,
+                                                           uint32_t d4, const uint32_t* __restrict__ block_list,
+                                                           const float* __restrict__ cent_rm, uint4* __restrict__ shadow,
+                                                           float* __restrict__ rows, float4* __restrict__ meta,
+                                                           float* __restrict__ sscale) {
+    const int lane = lane_id();
+    const uint32_t dp = d4 * 4, ks = dp / 64;
+    for (uint64_t b = (uint64_t)blockIdx.x * 4 + wave_index(); b < blocks; b += (uint64_t)gridDim.x * 4) {
+        const float4* blk = arena + b * d4 * 64;
+        const float4* cen = (const float4*)(cent_rm + (size_t)block_list[b] * dp);
+        const uint64_t slot = b * 64 + lane;
+        float4* row = rows ? (float4*)(rows + slot * dp) : nullptr;
+        double x2 = 0.0, b2 = 0.0;
+        float mx = 0.0f;
+        bool huge = false;
+        for (uint32_t t = 0; t < d4; ++t) {  // pass 1 (lane = vector): norms and the scale
+            const float4 x = blk[(size_t)t * 64 + lane];
+            const float4 c = cen[t];
+            if (rows) row[t] = x;
+            const float xv[4] = {x.x, x.y, x.z, x.w}, cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double bd = (double)xv[i] - (double)cv[i];
+                huge |= !(fabs(bd) <= (double)kScreenHuge) || !(fabsf(xv[i]) <= kScreenHuge);
+                x2 += (double)xv[i] * xv[i];
+                b2 += bd * bd;
+                mx = fmaxf(mx, fabsf((float)bd));
+            }
+        }
+        const float sc = huge ? 0.0f : i8_scale(mx);
+        sscale[slot] = sc;
+        // pass 2 (lane = (vector 16 vt + (l & 15), dims 16 (l >> 4) ..)): the quantized shadow and |b - b'|
+        const int vv = lane & 15, h = lane >> 4;
+        float svt[4], inv[4];
+        double e2p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int vt = 0; vt < 4; ++vt) {
+            svt[vt] = __shfl(sc, 16 * vt + vv);
+            inv[vt] = svt[vt] > 0.0f ? 1.0f / svt[vt] : 0.0f;
+        }
+        uint4* sh = shadow + b * (uint64_t)ks * 256;
+        for (uint32_t s = 0; s < ks; ++s) {
+            float4 c4[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) c4[j] = cen[16 * s + 4 * h + j];
+#pragma unroll
+            for (int vt = 0; vt < 4; ++vt) {
+                uint32_t w[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float4 x = blk[(size_t)(16 * s + 4 * h + j) * 64 + 16 * vt + vv];
+                    const float xv[4] = {x.x, x.y, x.z, x.w}, cv[4] = {c4[j].x, c4[j].y, c4[j].z, c4[j].w};
+                    uint32_t word = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const double bd = (double)xv[i] - (double)cv[i];
+                        const int qv = i8_q((float)bd, inv[vt]);
+                        const double ed = bd - (double)svt[vt] * (double)qv;
+                        e2p[vt] += ed * ed;
+                        word |= (uint32_t)(qv & 0xFF) << (8 * i);
+                    }
+                    w[j] = word;
+                }
+                sh[((size_t)s * 4 + vt) * 64 + lane] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+#pragma unroll
+        for (int vt = 0; vt < 4; ++vt) {
+            e2p[vt] += __shfl_xor(e2p[vt], 16);
+            e2p[vt] += __shfl_xor(e2p[vt], 32);
+        }
+        const int mv = lane >> 4;  // (this lane's vector 16 mv + (l & 15): its |b - b'|^2)
+        const double e2 = mv == 0 ? e2p[0] : mv == 1 ? e2p[1] : mv == 2 ? e2p[2] : e2p[3];
+        meta[slot] = huge ? make_float4(__builtin_inff(), __builtin_inff(), __builtin_inff(), __builtin_inff())
+                          : make_float4((float)b2, ru(sqrt(b2)), ru(sqrt(e2)), ru(sqrt(x2)));
+    }
+}
+
+// Per (query, probe) pair: the int8 A row (L2: a = q - c; IP: a = q) with its scale s_a, and
+// pst as for bf16 ({|a|^2 or <q, c>, |a| up, |a - a'| up, |c| up}).
+template <int M>
+__global__ __launch_bounds__(256) void ivf_screen_pairs_i8(const float* __restrict__ q, uint32_t BP, uint32_t P,
+                                                           const uint32_t* __restrict__ probes,
+                                                           const float* __restrict__ cent_rm, uint32_t dp,
+                                                           int8_t* __restrict__ qres, float* __restrict__ qscale,
+                                                           float4* __restrict__ pst, uint32_t* __restrict__ thr4,
+                                                           uint32_t* __restrict__ scnt, uint32_t* __restrict__ ovf,
+                                                           uint32_t* __restrict__ counters, uint32_t* __restrict__ ubcnt) {
+    const int lane = lane_id();
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < 4 * BP; e += gridDim.x * blockDim.x) thr4[e] = kThrInf;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < BP; e += gridDim.x * blockDim.x) {
+        scnt[e] = 0u;
+        ovf[e] = 0u;
+        ubcnt[e] = 0u;
+        if (e == 0) counters[kCtrCand] = 0u;
+    }
+    for (uint32_t i = blockIdx.x * 4 + wave_index(); i < BP; i += gridDim.x * 4) {
+        const float* qr = q + (size_t)(i / P) * dp;
+        const float* cr = cent_rm + (size_t)probes[i] * dp;
+        double a2 = 0.0, c2 = 0.0, qc = 0.0;
+        float mx = 0.0f;
+        bool huge = false;
+        for (uint32_t d = lane; d < dp; d += 64) {
+            const float qv = qr[d], cv = cr[d];
+            const double ad = M == kL2 ? (double)qv - (double)cv : (double)qv;
+            huge |= !(fabs(ad) <= (double)kScreenHuge) || !(fabsf(qv) <= kScreenHuge) || !(fabsf(cv) <= kScreenHuge);
+            a2 += ad * ad;
+            c2 += (double)cv * cv;
+            qc += (double)qv * cv;
+            mx = fmaxf(mx, fabsf((float)ad));
+        }
+        for (int m = 32; m >= 1; m >>= 1) {
+            a2 += __shfl_xor(a2, m);
+            c2 += __shfl_xor(c2, m);
+            qc += __shfl_xor(qc, m);
+            mx = fmaxf(mx, __shfl_xor(mx, m));
+        }
+        huge = __ballot(huge) != 0;
+        const float sc = huge ? 0.0f : i8_scale(mx);
+        const float inv = sc > 0.0f ? 1.0f / sc : 0.0f;
+        double f2 = 0.0;
+        for (uint32_t d = lane; d < dp; d += 64) {
+            const float qv = qr[d], cv = cr[d];
+            const double ad = M == kL2 ? (double)qv - (double)cv : (double)qv;
+            const int qi = i8_q((float)ad, inv);
+            qres[(size_t)i * dp + d] = (int8_t)qi;
+            const double fd = ad - (double)sc * (double)qi;
+            f2 += fd * fd;
+        }
+        for (int m = 32; m >= 1; m >>= 1) f2 += __shfl_xor(f2, m);
+        if (lane == 0) {
+            const float inf = __builtin_inff();
+            qscale[i] = sc;
+            if (huge) pst[i] = make_float4(inf, inf, inf, inf);
+            else if (M == kL2) pst[i] = make_float4((float)a2, ru(sqrt(a2)), ru(sqrt(f2)), 0.0f);
+            else pst[i] = make_float4((float)qc, ru(sqrt(a2)), ru(sqrt(f2)), ru(sqrt(c2)));
+        }
+    }
+}
+
 // One compare-exchange stage of a bitonic sort of 64 values held as u[v] in the 16 lanes of
 // a DPP row: element e = 4 (lane & 15) + v (strides 1, 2 within a lane, 4 .. 32 across lanes).
 template <int SIZE, int STRIDE>
@@ -242,6 +395,9 @@ __device__ __forceinline__ uint4 ld_nt_u4(const uint4* p) {
 }
 __device__ __forceinline__ bf16x8 as_bf16x8(const uint4 v) {
     return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ i32x4 as_i32x4(const uint4 v) {
+    return __builtin_bit_cast(i32x4, v);
 }
 
 // One wave: segment `seg` of list it.list against the nq (<= 16) queries of the item
@@ -691,12 +847,12 @@ __device__ __forceinline__ float row_elem(const float (&u)[4], int e) {
 // rl_lds: the wave's running lists of upper bounds (NG x 4 query rows; reset by the caller
 // per item); s_thr: the item's shared k-th (LDS); residue: the wave's quarter slot (0..3,
 // distinct per wave of an item).
-template <int M, int KD, int NG>
+template <int M, int KD, int NG, bool I8>
 __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
                                                 const uint32_t seg, float4* rl_lds, uint32_t* s_thr,
                                                 const uint32_t residue) {
     const int lane = lane_id();
-    const uint32_t dp = a.dp, ks = dp >> 5;
+    const uint32_t dp = a.dp, ks = dp >> (I8 ? 6 : 5);  // (k-steps of 64 int8 or 32 bf16 dims)
     const uint32_t count = a.count[it.list];
     const uint32_t seg_vectors = a.seg_blocks * 64;
     const uint64_t b0 = a.block_off[it.list] + (uint64_t)seg * a.seg_blocks;
@@ -716,7 +872,9 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
     const uint4* qa_row[NG];
 #pragma unroll
     for (int gg = 0; gg < NG; ++gg)
-        qa_row[gg] = (const uint4*)(a.qres + (size_t)pair_of(min(16 * gg + (lane & 15), nq - 1)) * dp) + (lane >> 4);
+        qa_row[gg] = (const uint4*)((const char*)a.qres + (size_t)pair_of(min(16 * gg + (lane & 15), nq - 1)) * dp *
+                                                              (I8 ? 1 : 2)) +
+                     (lane >> 4);
     uint32_t collected = 0;
     // the shared thresholds (list-wide k-th, quarter slots) as last read: re-read every
     // thr_every blocks (a stale value is larger, so only looser: still valid) so their
@@ -728,7 +886,7 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
         for (int r = 0; r < 4; ++r) gthr[gg][r] = gq4[gg][r] = __builtin_inff();
     const uint32_t thr_every = a.thr_every;
 
-    const uint4* sp = a.shadow + b0 * (uint64_t)dp * 8 + lane;
+    const uint4* sp = a.shadow + b0 * (uint64_t)ks * 256 + lane;
     uint4 xa[KD][4], qa[NG][KD];
 #pragma unroll
     for (int u = 0; u < KD; ++u) {
@@ -737,22 +895,31 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
 #pragma unroll
         for (int gg = 0; gg < NG; ++gg) qa[gg][u] = qa_row[gg][4 * (u % ks)];
     }
+    using AccT = std::conditional_t<I8, i32x4, f32x4>;
     for (uint32_t j = 0; j < nb; ++j) {
-        f32x4 acc[NG][4];
+        AccT acc[NG][4];
 #pragma unroll
         for (int gg = 0; gg < NG; ++gg)
 #pragma unroll
-            for (int vt = 0; vt < 4; ++vt) acc[gg][vt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            for (int vt = 0; vt < 4; ++vt) acc[gg][vt] = AccT{0, 0, 0, 0};
         for (uint32_t s0 = 0; s0 < ks; s0 += KD) {
             static_for<0, KD>([&](auto uu) {
                 constexpr int u = decltype(uu)::value;
 #pragma unroll
                 for (int gg = 0; gg < NG; ++gg) {
-                    const bf16x8 A = as_bf16x8(qa[gg][u]);
+                    if constexpr (I8) {
+                        const i32x4 A = as_i32x4(qa[gg][u]);
 #pragma unroll
-                    for (int vt = 0; vt < 4; ++vt)
-                        acc[gg][vt] =
-                            __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, as_bf16x8(xa[u][vt]), acc[gg][vt], 0, 0, 0);
+                        for (int vt = 0; vt < 4; ++vt)
+                            acc[gg][vt] =
+                                __builtin_amdgcn_mfma_i32_16x16x64_i8(A, as_i32x4(xa[u][vt]), acc[gg][vt], 0, 0, 0);
+                    } else {
+                        const bf16x8 A = as_bf16x8(qa[gg][u]);
+#pragma unroll
+                        for (int vt = 0; vt < 4; ++vt)
+                            acc[gg][vt] =
+                                __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, as_bf16x8(xa[u][vt]), acc[gg][vt], 0, 0, 0);
+                    }
                 }
                 const uint64_t nxt = (uint64_t)j * ks + s0 + u + KD;
 #pragma unroll
@@ -767,15 +934,26 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
             // lower bounds into acc, upper bounds into ubv (the inline kernel's bound)
             float ubv[4][4];
             float4 pst[4];
+            float qsc[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) pst[r] = a.pst[pair_of(min(g0 + 4 * (lane >> 4) + r, nq - 1))];
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t pi = pair_of(min(g0 + 4 * (lane >> 4) + r, nq - 1));
+                pst[r] = a.pst[pi];
+                if constexpr (I8) qsc[r] = a.qscale[pi];
+            }
 #pragma unroll
             for (int vt = 0; vt < 4; ++vt) {
                 const float4 mt = a.meta[(b0 + j) * 64 + 16 * vt + (lane & 15)];
+                float vsc = 0.0f;
+                if constexpr (I8) vsc = a.sscale[(b0 + j) * 64 + 16 * vt + (lane & 15)];
                 const bool valid = j * 64 + 16 * vt + (lane & 15) < nv;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float dot = acc[gg][vt][r];
+                    // (int8: <a', b'> = s_a s_b <q_a, q_b>, the integer sum exact; the two float
+                    // roundings are far inside the MFMA accumulation term cm below)
+                    float dot;
+                    if constexpr (I8) dot = (float)acc[gg][vt][r] * (qsc[r] * vsc);
+                    else dot = acc[gg][vt][r];
                     const float4 ps = pst[r];
                     const float approx = M == kL2 ? (ps.x + mt.x) - 2.0f * dot : -(ps.x + dot);
                     const float an = ps.y + ps.z, bn = mt.y + mt.z;
@@ -789,7 +967,8 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                     }
                     del = del * 1.001f + 1e-30f;
                     const float ub = approx + del;
-                    acc[gg][vt][r] = approx - del;
+                    if constexpr (I8) acc[gg][vt][r] = __float_as_int(approx - del);  // (the lower bound, in place)
+                    else acc[gg][vt][r] = approx - del;
                     ubv[r][vt] = valid && ub == ub ? ub : __builtin_inff();
                 }
             }
@@ -839,9 +1018,12 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
             }
             // candidates: one atomic per block and group for the wave's whole batch of them
             // (the ballots are recomputed for the writes rather than held: registers)
+            auto lbv = [&](int vt, int r) -> float {
+                if constexpr (I8) return __int_as_float(acc[gg][vt][r]);
+                else return acc[gg][vt][r];
+            };
             auto is_cand = [&](int vt, int r) {
-                return j * 64 + 16 * vt + (lane & 15) < nv && g0 + 4 * (lane >> 4) + r < nq &&
-                       !(acc[gg][vt][r] > th[r]);
+                return j * 64 + 16 * vt + (lane & 15) < nv && g0 + 4 * (lane >> 4) + r < nq && !(lbv(vt, r) > th[r]);
             };
             uint32_t tot = 0;
 #pragma unroll
@@ -865,7 +1047,7 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                             const uint32_t spi = it.pair_start + q0 + g0 + 4 * (lane >> 4) + r;
                             const uint32_t slot = (uint32_t)((b0 + j) * 64 + 16 * vt + (lane & 15));
                             if (idx < a.cand_cap)
-                                a.cand[idx] = make_uint4(spi, slot, __float_as_uint(acc[gg][vt][r]), 0u);
+                                a.cand[idx] = make_uint4(spi, slot, __float_as_uint(lbv(vt, r)), 0u);
                             else
                                 a.ovf[spi] = 1u;  // (any store of 1: idempotent)
                         }
@@ -920,7 +1102,7 @@ __device__ __forceinline__ void contribute_rl(const ScanArgs& a, const ScanItem 
 // segments dynamically; narrow items: one wave = one segment x <= 4 queries), collecting
 // instead of re-checking. W2: items of up to 32 queries (two A operands per shadow tile: the
 // registers of one workgroup per CU; otherwise two).
-template <int M, int KD, bool W2>
+template <int M, int KD, bool W2, bool I8>
 __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a) {
     __shared__ uint32_t s_next, s_seg;
     __shared__ uint32_t s_thr[32];
@@ -945,7 +1127,7 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
             if (lane < (int)it.npairs) s_thr_w[wv][lane] = a.thr[it.pair_start + lane];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             reset_rl(rl, 4);
-            collect_segment<M, KD, 1>(a, it, 0, (int)it.npairs, it.seg, rl, s_thr_w[wv], it.seg & 3u);
+            collect_segment<M, KD, 1, I8>(a, it, 0, (int)it.npairs, it.seg, rl, s_thr_w[wv], it.seg & 3u);
             contribute_rl(a, it, 0, (int)it.npairs, rl);
         }
     };
@@ -976,8 +1158,8 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
             if (lane == 0) sg = atomicAdd(&s_seg, 1u);
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
-            if (W2 && nq > 16) collect_segment<M, KD, 2>(a, it, 0, nq, sg, rl, s_thr, wv);
-            else collect_segment<M, KD, 1>(a, it, 0, nq, sg, rl, s_thr, wv);
+            if (W2 && nq > 16) collect_segment<M, KD, 2, I8>(a, it, 0, nq, sg, rl, s_thr, wv);
+            else collect_segment<M, KD, 1, I8>(a, it, 0, nq, sg, rl, s_thr, wv);
             any = true;
         }
         if (any) contribute_rl(a, it, 0, nq, rl);
@@ -1265,21 +1447,33 @@ bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq) {
            screen_item_lds(k, wq) + 4 * screen_wave_lds(k) + 256 <= kLdsBytes / 2;
 }
 
-size_t screen_shadow_u4(uint64_t blocks, uint32_t d4) { return (size_t)(blocks + 2) * d4 * 32; }
+size_t screen_shadow_u4(uint64_t blocks, uint32_t d4, bool i8) {
+    return (size_t)(blocks + 2) * d4 * (i8 ? 16 : 32);
+}
 
 void launch_screen_build(const float4* arena, uint64_t blocks, uint32_t d4, const uint32_t* block_list,
-                         const float* cent_rm, uint4* shadow, float* rows, float4* meta, hipStream_t s) {
+                         const float* cent_rm, uint4* shadow, float* rows, float4* meta, hipStream_t s, float* sscale) {
     if (!blocks) return;
     const uint32_t g = (uint32_t)std::min<uint64_t>((blocks + 3) / 4, 8192);
-    ivf_screen_build<<<g, 256, 0, s>>>(arena, blocks, d4, block_list, cent_rm, shadow, rows, meta);
+    if (sscale) ivf_screen_build_i8<<<g, 256, 0, s>>>(arena, blocks, d4, block_list, cent_rm, shadow, rows, meta, sscale);
+    else ivf_screen_build<<<g, 256, 0, s>>>(arena, blocks, d4, block_list, cent_rm, shadow, rows, meta);
 }
 
 void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, const uint32_t* probes,
                          const float* cent_rm, uint32_t dp, uint16_t* qres, float4* pst, uint32_t* thr4, hipStream_t s,
-                         uint32_t* scnt, uint32_t* ovf, uint32_t* counters, uint32_t* ubcnt) {
+                         uint32_t* scnt, uint32_t* ovf, uint32_t* counters, uint32_t* ubcnt, float* qscale) {
     const uint32_t BP = B * P;
     if (!BP) return;
     const uint32_t g = std::min<uint32_t>((BP + 3) / 4, 2048);
+    if (qscale) {  // (the int8 shadow: deferred scan only)
+        if (metric == kL2)
+            ivf_screen_pairs_i8<kL2><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, (int8_t*)qres, qscale, pst, thr4,
+                                                       scnt, ovf, counters, ubcnt);
+        else
+            ivf_screen_pairs_i8<kIP><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, (int8_t*)qres, qscale, pst, thr4,
+                                                       scnt, ovf, counters, ubcnt);
+        return;
+    }
     if (metric == kL2)
         ivf_screen_pairs<kL2><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst, thr4, scnt, ovf, counters, ubcnt);
     else
@@ -1290,23 +1484,30 @@ void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, 
     if (!grid_blocks) return;
     const bool w2 = a.wide_q > 16;
     const uint32_t g = std::min<uint32_t>(grid_blocks, w2 ? kPersistentBlocks / 2 : kPersistentBlocks);
-    const bool kd4 = (a.dp / 32) % 4 == 0, kd8 = (a.dp / 32) % 8 == 0;
-    auto go = [&](auto m_c, auto w_c) {
+    auto go = [&](auto m_c, auto w_c, auto i_c) {
         constexpr int Mm = decltype(m_c)::value;
         constexpr bool Ww = decltype(w_c)::value;
-        // (32-query items run one workgroup per CU: 8 k-steps of shadow in flight per wave
-        // keep as many bytes in flight per CU as two workgroups of 4 k-steps)
-        if (Ww && kd8) ivf_screen_collect<Mm, 8, Ww><<<g, 256, 0, s>>>(a);
-        else if (kd4) ivf_screen_collect<Mm, 4, Ww><<<g, 256, 0, s>>>(a);
-        else ivf_screen_collect<Mm, 2, Ww><<<g, 256, 0, s>>>(a);
+        constexpr bool Ii = decltype(i_c)::value;
+        // k-steps in flight per wave: a divisor of the row's k-steps (32 bf16 / 64 int8 dims
+        // each); 32-query items run one workgroup per CU, so they keep more in flight (8 bf16,
+        // 6 int8: as many bytes per CU as two workgroups of 4 bf16 k-steps, or nearly)
+        constexpr int KW = Ii ? 6 : 8;
+        const uint32_t ks = a.dp / (Ii ? 64 : 32);
+        if (Ww && ks % KW == 0) ivf_screen_collect<Mm, KW, Ww, Ii><<<g, 256, 0, s>>>(a);
+        else if (ks % 4 == 0) ivf_screen_collect<Mm, 4, Ww, Ii><<<g, 256, 0, s>>>(a);
+        else if (ks % 2 == 0) ivf_screen_collect<Mm, 2, Ww, Ii><<<g, 256, 0, s>>>(a);
+        else ivf_screen_collect<Mm, 1, Ww, Ii><<<g, 256, 0, s>>>(a);
     };
-    if (metric == kL2) {
-        if (w2) go(std::integral_constant<int, kL2>{}, std::true_type{});
-        else go(std::integral_constant<int, kL2>{}, std::false_type{});
-    } else {
-        if (w2) go(std::integral_constant<int, kIP>{}, std::true_type{});
-        else go(std::integral_constant<int, kIP>{}, std::false_type{});
-    }
+    auto go_w = [&](auto m_c, auto i_c) {
+        if (w2) go(m_c, std::true_type{}, i_c);
+        else go(m_c, std::false_type{}, i_c);
+    };
+    auto go_i = [&](auto m_c) {
+        if (a.sscale) go_w(m_c, std::true_type{});
+        else go_w(m_c, std::false_type{});
+    };
+    if (metric == kL2) go_i(std::integral_constant<int, kL2>{});
+    else go_i(std::integral_constant<int, kIP>{});
 }
 
 void launch_screen_select(const ScanArgs& a, uint32_t BP, uint32_t* scnt, uint32_t* soff, uint2* surv,

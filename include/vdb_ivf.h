@@ -328,7 +328,8 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * candidates appear), "screen_cand_cap" (collected candidates per batch, default 4M; a pair
  * beyond it is recomputed over its whole list, a file-home tier batch re-run with more),
  * "tier_row_direct" (1, default: the screened tier reads survivors' rows with O_DIRECT),
- * "tier_row_qd" (256: survivor-row reads in flight), "screen_thr_every" (0 = automatic: blocks
+ * "tier_row_qd" (256: survivor-row reads in flight), "screen_i8" (0, default: the deferred
+ * screen's shadow in bf16; 1: int8 with a per-vector scale, half the bytes, a wider bound), "screen_thr_every" (0 = automatic: blocks
  * between the collect kernel's re-reads of the shared thresholds; 4 for 32-query items, else 1),
  * "screen_floor_ppm" (50000, default: a screened batch of at least "screen_floor_min" (4M)
  * (query, vector) pairs that overflowed its candidate buffer, or whose survivors beyond k per

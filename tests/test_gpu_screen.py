@@ -74,6 +74,57 @@ def test_screen_is_taken_and_prunes(defer):
 
 
 @pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("k", [1, 10, 17, 64])
+def test_screen_int8_shadow_hub_lists(metric, k):
+    """The int8 shadow (option screen_i8): per-vector scaled residuals on
+    v_mfma_i32_16x16x64_i8, exact integer sums, |b - b'| measured per vector; hub lists,
+    16- and 32-query items, several segment sizes; and the format switches back to bf16 for
+    the inline kernel and the option 0."""
+    X, ids, lists, C, Q = hub_data(48, seed=90 + k)
+    g, o = lists_pair(X, ids, lists, C, metric)
+    g.set_option("screen_i8", 1)
+    g.set_option("screen_floor_ppm", 0)  # (at k = 64 the wider bound would trip the floor)
+    nprobe = 3 if metric == 0 else 6
+    Dr, Ir = o.search(Q, nprobe, k)
+    for sg in (16, 32):
+        g.set_option("screen_group", sg)
+        for seg in (0, 64):
+            g.set_option("seg_vectors", seg)
+            D, I, p = screen_stats(g, Q, nprobe, k, 130)
+            assert_same(D, I, Dr, Ir)
+            assert p["bounded_blocks"] > 0, p
+    g.set_option("screen_defer", 0)  # (the inline kernel: a bf16 shadow is built for it)
+    assert_same(*search_all(g, Q, nprobe, k, 130), Dr, Ir)
+    g.set_option("screen_defer", 1)
+    g.set_option("screen_i8", 0)
+    assert_same(*search_all(g, Q, nprobe, k, 130), Dr, Ir)
+
+
+@pytest.mark.parametrize("dim", [1, 3, 67, 130, 256])
+def test_screen_int8_odd_dims_and_extremes(dim):
+    """int8 shadow with dims that leave 1, 2 or 3 k-steps of 64 (every k-step pipeline),
+    plus vectors with huge, infinite and subnormal values and a zero vector."""
+    rng = np.random.default_rng(dim)
+    X = rng.standard_normal((3000, dim)).astype(np.float32)
+    X[5] = 0.0
+    X[6, 0] = 3e38
+    X[7, 0] = np.inf
+    X[8] = 1e-41
+    Q = rng.standard_normal((70, dim)).astype(np.float32)
+    ids = np.arange(3000, dtype=np.uint64)
+    for metric in (0, 1):
+        o = oracle.OracleIndex(dim, 8, metric)
+        o.centroids = rng.standard_normal((8, dim)).astype(np.float32)
+        o.add(X, ids)
+        g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, 8, vdb.Metric(metric)))
+        g.centroids = o.centroids
+        g.add(X, ids)
+        g.set_option("screen_i8", 1)
+        for k in (1, 10):
+            assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))
+
+
+@pytest.mark.parametrize("metric", [0, 1])
 def test_screen_deferred_overflow_recomputes_the_pair(metric):
     """A candidate buffer far too small for the batch: every pair whose candidates do not fit
     is marked and recomputed exactly over its whole list, one wave per planned segment (one

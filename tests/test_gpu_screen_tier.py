@@ -62,8 +62,9 @@ def test_screened_tier_host_home_mixed_k(metric):
     assert st["screen_bytes"] < 0.7 * len(X) * (dim * 4 + 8), st
 
 
+@pytest.mark.parametrize("i8", [0, 1], ids=["bf16", "int8"])
 @pytest.mark.parametrize("dim", [64, 70])
-def test_screened_tier_file_home(tmp_path, dim):
+def test_screened_tier_file_home(tmp_path, dim, i8):
     """Lists served from an index file: the shadow is built by streaming the file once;
     per batch only the survivors' rows are read (far fewer bytes than the probed lists).
     dim 70 pads the fetched rows to 128."""
@@ -75,6 +76,7 @@ def test_screened_tier_file_home(tmp_path, dim):
     g.save(path)
     del g
     h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    h.set_option("screen_i8", i8)
     h.set_option("list_cache_bytes", (need_blocks(o, Q, NPROBE) + 8) * block_bytes(dim))
     h.open_lists(path)
     Dr, Ir = o.search(Q, NPROBE, 10)
@@ -85,7 +87,7 @@ def test_screened_tier_file_home(tmp_path, dim):
     assert st["screen_resident"] == 1 and st["loads"] == 0, st
     assert 0 < st["screen_rows_fetched"] and st["screen_row_bytes"] == st["screen_rows_fetched"] * dim * 4, st
     probed = sum(o.list_count(l) for q in Q for l in o.select_nprobe(q, NPROBE))
-    assert st["screen_rows_fetched"] < 0.1 * probed * 2, st  # (two passes above)
+    assert st["screen_rows_fetched"] < (0.3 if i8 else 0.1) * probed * 2, st  # (two passes above)
     # k > 64 on the same handle: the list cache, under eviction
     Dr, Ir = o.search(Q, NPROBE, 80)
     assert_same(*h.search(Q, nprobe=NPROBE, k=80), Dr, Ir)
