@@ -55,7 +55,8 @@ class CacheStats(ctypes.Structure):
                 ("io_uring", ctypes.c_int32), ("o_direct", ctypes.c_int32),
                 ("screen_resident", ctypes.c_int32), ("reserved", ctypes.c_int32), ("screen_bytes", ctypes.c_uint64),
                 ("screen_batches", ctypes.c_uint64), ("screen_rows_fetched", ctypes.c_uint64),
-                ("screen_row_bytes", ctypes.c_uint64), ("screen_reruns", ctypes.c_uint64)]
+                ("screen_row_bytes", ctypes.c_uint64), ("screen_reruns", ctypes.c_uint64),
+                ("screen_rows_cached", ctypes.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

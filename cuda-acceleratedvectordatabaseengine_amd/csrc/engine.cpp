@@ -691,6 +691,11 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "screen_floor_skip") {
             require(value >= 1 && value < (1ll << 20), "screen_floor_skip is 1 .. 2^20");
             h->screen_floor_skip = (uint32_t)value;
+        } else if (n == "tier_row_cache") {
+            h->set_device();
+            h->quiesce();
+            h->tier_row_cache = value != 0;
+            if (h->tiered() && h->file_home() && h->screen_ready) h->fill_row_cache();
         } else if (n == "tier_row_qd") {
             require(value >= 1 && value <= 4096, "tier_row_qd is 1 .. 4096");
             h->tier_row_qd = (uint32_t)value;
@@ -771,6 +776,7 @@ int vdb_ivf_cache_stats(vdb_ivf* h, vdb_ivf_cache_stats_t* out) {
             out->screen_rows_fetched += m->screen_rows_fetched;
             out->screen_row_bytes += m->screen_row_bytes;
             out->screen_reruns += m->screen_reruns;
+            out->screen_rows_cached += m->screen_rows_cached;
         }
     });
 }

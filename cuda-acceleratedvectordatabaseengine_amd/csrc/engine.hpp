@@ -355,6 +355,10 @@ struct vdb_ivf {
     DevBuf<float> fetch_dev;           // ... on the device ([n][dim], padded into the slot's srows)
     std::vector<uint2> fetch_surv;     // ... their (slot, pair)
     uint64_t screen_rows_fetched = 0, screen_row_bytes = 0, screen_tier_batches = 0, screen_reruns = 0;
+    uint64_t screen_rows_cached = 0;   // ... survivor rows copied from the HBM cache instead
+    bool tier_row_cache = true;        // option tier_row_cache: the idle cache holds the largest lists' rows
+    DevBuf<ulonglong2> cache_src;      // ... per batch {row index, cache slot} of those survivors
+    std::vector<ulonglong2> cache_src_host;
     uint32_t tier_cand_cap = 0;        // ... a candidate capacity grown by an overflow
     // Run-time floor under the screen (lists in HBM): every deferred batch reports to
     // page-locked host memory its survivors (or an overflow of the candidate buffer), its
@@ -636,7 +640,8 @@ struct vdb_ivf {
                            d_block_off.device_bytes(), d_count_local.device_bytes(), d_count_global.device_bytes(),
                            d_nseg.device_bytes(), screen_sh.device_bytes(), screen_rows.device_bytes(),
                            screen_meta.device_bytes(), screen_blist.device_bytes(), screen_scale.device_bytes(),
-                           screen_ids.device_bytes(), d_sblock_off.device_bytes(), cache.device_bytes(),
+                           screen_ids.device_bytes(), d_sblock_off.device_bytes(), cache_src.device_bytes(),
+                           cache.device_bytes(),
                            cache_ids.device_bytes(), drows.device_bytes(), dpad.device_bytes(), drows_cs.device_bytes(),
                            dpad_cs.device_bytes(), out_d.device_bytes(), qin.device_bytes(), out_i.device_bytes(),
                            d_req.device_bytes(), stats.device_bytes()})
@@ -1053,6 +1058,33 @@ struct vdb_ivf {
         HIPCHECK(hipStreamSynchronize(stream));
         sblocks = nb;
         screen_ready = true;
+        if (file_home() && tier_row_cache) fill_row_cache();
+    }
+
+    // Screened tier, file home: the k <= 64 searches never use the list cache, so it is filled
+    // with the largest stored lists (on iid data they are also the most probed); a survivor of
+    // a list found there is copied from HBM instead of read from the file. The lists stay
+    // ordinary cached lists: a k > 64 search may evict them.
+    void fill_row_cache() {
+        if (!cache_blocks) return;
+        std::vector<uint32_t> order;
+        for (uint32_t l = 0; l < nlist; ++l)
+            if (owned[l] && count[l] && cache_off[l] == kAbsent) order.push_back(l);
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return count[x] > count[y]; });
+        std::vector<std::pair<uint32_t, uint64_t>> loads;
+        for (uint32_t l : order) {
+            const uint64_t off = cache_alloc(list_blocks(l));
+            if (off == kAbsent) continue;  // (a smaller list may still fit)
+            cache_off[l] = off;
+            ++resident_n;
+            ++cache_loads;
+            cache_bytes_in += list_blocks(l) * block_bytes(dp);
+            loads.push_back({l, off});
+        }
+        if (loads.empty()) return;
+        load_lists(loads, stream);
+        upload_scan_directory(stream);
+        HIPCHECK(hipStreamSynchronize(stream));
     }
 
     // Tier, file home: after the deferred scan's selection, read the survivors' rows of the
@@ -1094,17 +1126,29 @@ struct vdb_ivf {
         for (uint32_t i = 0; i < kQD; ++i) free_slots[i] = kQD - 1 - i;
         std::vector<uint64_t> delta(kQD);
         uint64_t bytes_read = 0;
-        // one read per distinct row (a row surviving for several queries is read once), issued
-        // in file order; the duplicates are copied from the first reader's staging row
-        std::vector<uint32_t> order(n);
-        for (uint32_t i = 0; i < n; ++i) order[i] = i;
+        // rows of lists in the HBM cache are copied from there (after the upload below); the
+        // rest: one read per distinct row (a row surviving for several queries is read once),
+        // issued in file order, the duplicates copied from the first reader's staging row
+        cache_src_host.clear();
+        std::vector<uint32_t> order;
+        order.reserve(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint64_t slot = fetch_surv[i].x;
+            const uint32_t l = sblist_host[slot >> 6];
+            if (tier_row_cache && !cache_off.empty() && cache_off[l] != kAbsent)
+                cache_src_host.push_back({(unsigned long long)i,
+                                          (unsigned long long)(cache_off[l] * 64 + (slot - sblock_off[l] * 64))});
+            else
+                order.push_back(i);
+        }
+        const uint32_t nf = (uint32_t)order.size();
         std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
             return fetch_surv[x].x != fetch_surv[y].x ? fetch_surv[x].x < fetch_surv[y].x : x < y;
         });
         std::vector<uint32_t> uniq;
         std::vector<std::pair<uint32_t, uint32_t>> dups;  // (survivor, survivor holding its row)
-        uniq.reserve(n);
-        for (uint32_t t = 0; t < n; ++t) {
+        uniq.reserve(nf);
+        for (uint32_t t = 0; t < nf; ++t) {
             if (t && fetch_surv[order[t]].x == fetch_surv[order[t - 1]].x) dups.push_back({order[t], uniq.back()});
             else uniq.push_back(order[t]);
         }
@@ -1154,6 +1198,7 @@ struct vdb_ivf {
         for (const auto& d : dups) std::memcpy(st + (size_t)d.first * dim, st + (size_t)d.second * dim, row_bytes);
         screen_rows_fetched += nu;
         screen_row_bytes += (uint64_t)nu * row_bytes;
+        screen_rows_cached += cache_src_host.size();
         file_bytes_read += bytes_read;  // (with O_DIRECT: the aligned supersets the device delivered)
         float* rows = slot_buf(w, w.srows, (size_t)std::max<uint32_t>(n, 1) * dp);
         if (n) {
@@ -1166,7 +1211,14 @@ struct vdb_ivf {
                 HIPCHECK(hipGetLastError());
             }
         }
-        HIPCHECK(hipStreamSynchronize(s));  // (the staging is reused by the next batch)
+        if (!cache_src_host.empty()) {  // (overwrites those rows' unused staging content)
+            const uint32_t nc = (uint32_t)cache_src_host.size();
+            HIPCHECK(hipMemcpyAsync(cache_src.ensure(nc), cache_src_host.data(), (size_t)nc * sizeof(ulonglong2),
+                                    hipMemcpyHostToDevice, s));
+            vdbk::launch_gather_cache_rows(cache.p, d4, cache_src.p, nc, rows, s);
+            HIPCHECK(hipGetLastError());
+        }
+        HIPCHECK(hipStreamSynchronize(s));  // (the staging and the cache's contents are reused later)
         return rows;
     }
 

@@ -1442,6 +1442,26 @@ __global__ __launch_bounds__(256) void ivf_screen_pair_topk(ScanArgs a, const ui
     if (a.mstats && lane == 0 && rechecked) atomicAdd(&a.mstats[2], rechecked);
 }
 
+// Screened tier: survivor rows whose list is in the HBM cache ({row index, cache slot}: one wave
+// each) copied from the cache's block layout into the batch's row-major rows [n][dp].
+__global__ __launch_bounds__(256) void ivf_gather_cache_rows(const float4* __restrict__ cache, uint32_t d4,
+                                                             const ulonglong2* __restrict__ src, uint32_t n,
+                                                             float4* __restrict__ rows) {
+    const int lane = lane_id();
+    for (uint32_t i = blockIdx.x * 4 + wave_index(); i < n; i += gridDim.x * 4) {
+        const ulonglong2 e = src[i];
+        const uint64_t blk = e.y >> 6, vl = e.y & 63;
+        for (uint32_t t = lane; t < d4; t += 64) rows[e.x * d4 + t] = cache[(blk * d4 + t) * 64 + vl];
+    }
+}
+
+void launch_gather_cache_rows(const float4* cache, uint32_t d4, const ulonglong2* src, uint32_t n, float* rows,
+                              hipStream_t s) {
+    if (!n) return;
+    const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(4096, (n + 3) / 4));
+    ivf_gather_cache_rows<<<g, 256, 0, s>>>(cache, d4, src, n, (float4*)rows);
+}
+
 bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq) {
     return k >= 1 && k <= 64 && dp % 64 == 0 && (wq == 16 || wq == 32) && exact_lds(dp / 4) <= kLdsBytes / 2 &&
            screen_item_lds(k, wq) + 4 * screen_wave_lds(k) + 256 <= kLdsBytes / 2;

@@ -266,6 +266,8 @@ typedef struct vdb_ivf_cache_stats_t {
     uint64_t screen_rows_fetched; /* survivors' rows read from the file home (host home: read over PCIe) */
     uint64_t screen_row_bytes;
     uint64_t screen_reruns;       /* batches re-run after overflowing the candidate buffer */
+    uint64_t screen_rows_cached;  /* survivor rows read from the HBM cache instead of the file
+                                     (option tier_row_cache: the largest lists' rows kept there) */
 } vdb_ivf_cache_stats_t;
 int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
 /* The tier's home on disk (ListPrefetcher::register_list_file / prefetch_lists,
@@ -328,7 +330,9 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * candidates appear), "screen_cand_cap" (collected candidates per batch, default 4M; a pair
  * beyond it is recomputed over its whole list, a file-home tier batch re-run with more),
  * "tier_row_direct" (1, default: the screened tier reads survivors' rows with O_DIRECT),
- * "tier_row_qd" (256: survivor-row reads in flight), "screen_i8" (0, default: the deferred
+ * "tier_row_qd" (256: survivor-row reads in flight), "tier_row_cache" (1, default: a file-home
+ * screened tier fills its idle HBM cache with the largest lists, whose survivors' rows are then
+ * copied from HBM instead of read from the file), "screen_i8" (0, default: the deferred
  * screen's shadow in bf16; 1: int8 with a per-vector scale, half the bytes, a wider bound), "screen_thr_every" (0 = automatic: blocks
  * between the collect kernel's re-reads of the shared thresholds; 4 for 32-query items, else 1),
  * "screen_floor_ppm" (50000, default: a screened batch of at least "screen_floor_min" (4M)

@@ -62,12 +62,14 @@ def test_screened_tier_host_home_mixed_k(metric):
     assert st["screen_bytes"] < 0.7 * len(X) * (dim * 4 + 8), st
 
 
+@pytest.mark.parametrize("rc", [0, 1], ids=["file_rows", "row_cache"])
 @pytest.mark.parametrize("i8", [0, 1], ids=["bf16", "int8"])
 @pytest.mark.parametrize("dim", [64, 70])
-def test_screened_tier_file_home(tmp_path, dim, i8):
+def test_screened_tier_file_home(tmp_path, dim, i8, rc):
     """Lists served from an index file: the shadow is built by streaming the file once;
-    per batch only the survivors' rows are read (far fewer bytes than the probed lists).
-    dim 70 pads the fetched rows to 128."""
+    per batch only the survivors' rows are read (far fewer bytes than the probed lists),
+    from the file, or (tier_row_cache) copied from the idle HBM cache filled with the
+    largest lists. dim 70 pads the fetched rows to 128."""
     X, Q, ids, o = data(dim, seed=9)
     g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
     g.centroids = o.centroids
@@ -77,17 +79,22 @@ def test_screened_tier_file_home(tmp_path, dim, i8):
     del g
     h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
     h.set_option("screen_i8", i8)
+    h.set_option("tier_row_cache", rc)
     h.set_option("list_cache_bytes", (need_blocks(o, Q, NPROBE) + 8) * block_bytes(dim))
     h.open_lists(path)
     Dr, Ir = o.search(Q, NPROBE, 10)
+    loads0 = None
     for batch in (256, 5):
         h.set_batch(batch)
         assert_same(*h.search(Q, nprobe=NPROBE, k=10), Dr, Ir)
+        loads0 = h.cache_stats()["loads"] if loads0 is None else loads0
     st = h.cache_stats()
-    assert st["screen_resident"] == 1 and st["loads"] == 0, st
+    assert st["screen_resident"] == 1 and st["loads"] == loads0, st  # (no per-batch loads)
+    assert (st["loads"] > 0) == bool(rc) and (st["screen_rows_cached"] > 0) == bool(rc), st
     assert 0 < st["screen_rows_fetched"] and st["screen_row_bytes"] == st["screen_rows_fetched"] * dim * 4, st
     probed = sum(o.list_count(l) for q in Q for l in o.select_nprobe(q, NPROBE))
-    assert st["screen_rows_fetched"] < (0.3 if i8 else 0.1) * probed * 2, st  # (two passes above)
+    rows = st["screen_rows_fetched"] + st["screen_rows_cached"]
+    assert rows < (0.3 if i8 else 0.1) * probed * 2, st  # (two passes above)
     # k > 64 on the same handle: the list cache, under eviction
     Dr, Ir = o.search(Q, NPROBE, 80)
     assert_same(*h.search(Q, nprobe=NPROBE, k=80), Dr, Ir)

@@ -196,9 +196,10 @@ def test_shard_files_served_per_rank(tmp_path, screen):
         st = h.cache_stats()
         assert st["file_bytes_read"] > 0
         if screen:  # the file streamed once (the shadow), then only the survivors' rows
-            assert st["screen_rows_fetched"] > 0 and st["loads"] == 0, st
+            # (the idle cache holds the largest lists: their survivors are copied from HBM)
+            assert st["screen_rows_fetched"] + st["screen_rows_cached"] > 0, st
             probed = sum(int(sizes[l]) for q in Q for l in o.select_nprobe(q, NPROBE) if owned[l])
-            assert st["screen_rows_fetched"] < 0.25 * probed, (st, probed)
+            assert st["screen_rows_fetched"] + st["screen_rows_cached"] < 0.25 * probed, (st, probed)
         with pytest.raises(vdb.VdbError):
             h.set_shard((r + 1) % world, world)  # the file holds only this rank's lists
         s = torch.cuda.Stream(dev)
