@@ -438,6 +438,8 @@ def tier_leg(vdb, idx, args, device, queries):
                                 "from the file only for the exact re-checks' survivors",
                       "screen_hbm_gb": round(s1["screen_bytes"] / 1e9, 2),
                       "survivor_rows_per_batch": round(rows / batches, 1),
+                      "survivor_rows_from_hbm_cache_per_batch": round(
+                          (s1.get("screen_rows_cached", 0) - s0.get("screen_rows_cached", 0)) / batches, 1),
                       "survivor_row_bytes_per_batch": int((s1["screen_row_bytes"] - s0["screen_row_bytes"]) / batches),
                       "screen_batches": s1["screen_batches"] - s0["screen_batches"],
                       "screen_reruns": s1["screen_reruns"] - s0["screen_reruns"],
@@ -458,6 +460,8 @@ def tier_leg(vdb, idx, args, device, queries):
             ev = time.perf_counter() - t0
             v1 = h.cache_stats()
             variants.append({"opts": vs, "value": round(nq / ev, 1),
+                             "survivor_rows_from_hbm_cache_per_batch": round(
+                                 (v1.get("screen_rows_cached", 0) - v0.get("screen_rows_cached", 0)) / batches, 1),
                              "survivor_rows_read_per_batch": round((v1["screen_rows_fetched"] - v0["screen_rows_fetched"]) / batches, 1),
                              "file_read_gbps": round((v1["file_bytes_read"] - v0["file_bytes_read"]) / ev / 1e9, 2)})
         if variants:

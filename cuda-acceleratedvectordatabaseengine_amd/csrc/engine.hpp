@@ -1212,6 +1212,9 @@ struct vdb_ivf {
             }
         }
         if (!cache_src_host.empty()) {  // (overwrites those rows' unused staging content)
+            // (a k > 64 call may have loaded lists into the cache asynchronously: its loads end
+            // before its last sub-batch, whose completion tier_call_ev marks)
+            if (tier_call_used) HIPCHECK(hipEventSynchronize(tier_call_ev));
             const uint32_t nc = (uint32_t)cache_src_host.size();
             HIPCHECK(hipMemcpyAsync(cache_src.ensure(nc), cache_src_host.data(), (size_t)nc * sizeof(ulonglong2),
                                     hipMemcpyHostToDevice, s));
