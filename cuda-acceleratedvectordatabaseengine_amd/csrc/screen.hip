@@ -987,14 +987,6 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                 const float4 rv = *rlp;
                 float rl[4] = {rv.x, rv.y, rv.z, rv.w};
                 float tw = row_elem(rl, k - 1), tq = row_elem(rl, kq - 1);
-                const float bmin = fminf(fminf(ubv[r][0], ubv[r][1]), fminf(ubv[r][2], ubv[r][3]));
-                if (__ballot(bmin < tw)) {
-                    block_sort64(ubv[r]);
-                    merge_sorted64(rl, ubv[r]);
-                    *rlp = make_float4(rl[0], rl[1], rl[2], rl[3]);
-                    tw = row_elem(rl, k - 1);
-                    tq = row_elem(rl, kq - 1);
-                }
                 uint32_t* gt = a.thr + spi;
                 uint32_t* s4 = a.thr4 + (size_t)spi * 4;
                 if (j % thr_every == 0) {
@@ -1005,6 +997,19 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                     gq4[gg][r] = ord_dec(m4);
                 }
                 const float cur = fminf(gthr[gg][r], ord_dec(s_thr[gc]));
+                // Only upper bounds below min(tw, cur) are kept: one at or above a valid shared
+                // threshold cannot lower any threshold, and the union of the contributed lists
+                // already holds k upper bounds at or below cur (those of the waves that
+                // published it), so its k-th is unchanged (ivf_screen_tfinal). A block with
+                // none skips its sort and merge.
+                const float bmin = fminf(fminf(ubv[r][0], ubv[r][1]), fminf(ubv[r][2], ubv[r][3]));
+                if (__ballot(bmin < fminf(tw, cur))) {
+                    block_sort64(ubv[r]);
+                    merge_sorted64(rl, ubv[r]);
+                    *rlp = make_float4(rl[0], rl[1], rl[2], rl[3]);
+                    tw = row_elem(rl, k - 1);
+                    tq = row_elem(rl, kq - 1);
+                }
                 if ((lane & 15) == 0 && g < nq) {
                     if (tw < cur) {
                         atomicMin(&s_thr[g], ord_enc(tw));
