@@ -847,7 +847,7 @@ __device__ __forceinline__ float row_elem(const float (&u)[4], int e) {
 // rl_lds: the wave's running lists of upper bounds (NG x 4 query rows; reset by the caller
 // per item); s_thr: the item's shared k-th (LDS); residue: the wave's quarter slot (0..3,
 // distinct per wave of an item).
-template <int M, int KD, int NG, bool I8>
+template <int M, int KD, int NG, bool I8, bool W2>
 __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
                                                 const uint32_t seg, float4* rl_lds, uint32_t* s_thr,
                                                 const uint32_t residue) {
@@ -879,12 +879,14 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
     // the shared thresholds (list-wide k-th, quarter slots) as last read: re-read every
     // thr_every blocks (a stale value is larger, so only looser: still valid) so their
     // latency is not paid by every block
+    // (kept across blocks in the one-workgroup-per-CU variant only: the two-workgroups-per-CU
+    // variant re-reads them every block, which keeps 8 registers free: 2 spills instead of 18)
     float gthr[NG][4], gq4[NG][4];  // (and this wave's quarter slot)
 #pragma unroll
     for (int gg = 0; gg < NG; ++gg)
 #pragma unroll
         for (int r = 0; r < 4; ++r) gthr[gg][r] = gq4[gg][r] = __builtin_inff();
-    const uint32_t thr_every = a.thr_every;
+    const uint32_t thr_every = W2 ? a.thr_every : 1u;
 
     const uint4* sp = a.shadow + b0 * (uint64_t)ks * 256 + lane;
     uint4 xa[KD][4], qa[NG][KD];
@@ -1132,7 +1134,7 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
             if (lane < (int)it.npairs) s_thr_w[wv][lane] = a.thr[it.pair_start + lane];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             reset_rl(rl, 4);
-            collect_segment<M, KD, 1, I8>(a, it, 0, (int)it.npairs, it.seg, rl, s_thr_w[wv], it.seg & 3u);
+            collect_segment<M, KD, 1, I8, W2>(a, it, 0, (int)it.npairs, it.seg, rl, s_thr_w[wv], it.seg & 3u);
             contribute_rl(a, it, 0, (int)it.npairs, rl);
         }
     };
@@ -1163,8 +1165,8 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
             if (lane == 0) sg = atomicAdd(&s_seg, 1u);
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
-            if (W2 && nq > 16) collect_segment<M, KD, 2, I8>(a, it, 0, nq, sg, rl, s_thr, wv);
-            else collect_segment<M, KD, 1, I8>(a, it, 0, nq, sg, rl, s_thr, wv);
+            if (W2 && nq > 16) collect_segment<M, KD, 2, I8, W2>(a, it, 0, nq, sg, rl, s_thr, wv);
+            else collect_segment<M, KD, 1, I8, W2>(a, it, 0, nq, sg, rl, s_thr, wv);
             any = true;
         }
         if (any) contribute_rl(a, it, 0, nq, rl);
