@@ -564,6 +564,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight (streams) in the timed region; 0 = 2 on one GPU (3 measured no faster, "
                          "p99 2x), 3 across ranks (1/8 shard: +6 %% over 2)")
+    ap.add_argument("--latency-batches", type=int, default=1000,
+                    help="batches per latency leg (p99 at the in-flight depth and one in flight; 0: p99 from the K steps)")
     ap.add_argument("--prof-steps", type=int, default=30,
                     help="single-stream steps timed per launch (roofline, one-in-flight latency)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -769,12 +771,23 @@ def timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, che
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         parity_multi = bool(int(flag.item()) == 1)
     lat = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    p99 = percentile(lat, 0.99)
-    lat_mean = sum(lat) / max(len(lat), 1)
+    p99_steps = percentile(lat, 0.99)
     if world > 1:
-        t = torch.tensor([elapsed, p99], dtype=torch.float64, device=ctrl)
+        t = torch.tensor([elapsed, p99_steps], dtype=torch.float64, device=ctrl)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, p99 = float(t[0]), float(t[1])
+        elapsed, p99_steps = float(t[0]), float(t[1])
+    # p99 latency from its own leg (QPS stays the K timed steps'): with K = 20 a "p99" is the
+    # second-largest sample, so the latency legs time >= 1000 batches each, at the same
+    # in-flight depth (closed loop: batch j is issued when batch j - depth completes, so its
+    # start event fires at issue) and one at a time
+    lat_legs = {}
+    if args.latency_batches > 0:
+        for depth in sorted({len(streams), 1}, reverse=True):
+            lat_legs[depth] = latency_leg(args, world, idx, rank, streams[:depth], step, ctrl)
+    if lat_legs:
+        p99, lat_mean = lat_legs[len(streams)]["p99_ms"], lat_legs[len(streams)]["mean_ms"]
+    else:
+        p99, lat_mean = p99_steps, sum(lat) / max(len(lat), 1)
 
     device_wait(args, world, idx, streams, rank)
     idx.profile_enable(True)
@@ -823,9 +836,56 @@ def timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, che
         p99_single = float(t[0])
         per_rank = [None] * world
         dist.all_gather_object(per_rank, mine)
+    if 1 in lat_legs:
+        p99_single = lat_legs[1]["p99_ms"]
     return {"elapsed": elapsed, "p99": p99, "lat_mean": lat_mean, "p99_single": p99_single, "prof": prof,
+            "p99_steps": p99_steps, "latency_legs": lat_legs,
             "parity_multi": parity_multi,
             "per_rank": per_rank, "mine": mine}
+
+
+def latency_leg(args, world, idx, rank, streams, step, ctrl):
+    """args.latency_batches batches at len(streams) in flight, closed loop: batch j is issued
+    (on streams[j % depth]) once batch j - depth has completed, so its start event fires at
+    issue and its latency is issue -> results ready (device time, including the other
+    batches in flight). Queries cycle over the bench's query set; every batch writes the
+    same results to the same output rows as its first use. p99 = sorted[floor(0.99 (n-1))]
+    (query_service.cpp:790-798), max over ranks."""
+    depth, n = len(streams), args.latency_batches
+    nq_batches = args.warmup + args.steps + args.prof_steps
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+
+    def wait(e):
+        while not e.query():
+            if world > 1 and args.exchange == "engine":
+                err = idx.comm_status()[0]
+                if err:
+                    print(json.dumps({"error": err, "rank": rank}), flush=True)
+                    os._exit(3)
+            time.sleep(0.00002)
+
+    device_wait(args, world, idx, streams, rank)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for j in range(n):
+        if j >= depth:
+            wait(ends[j - depth])
+        st = streams[j % depth]
+        starts[j].record(st)
+        step(j % nq_batches, j % depth)
+        ends[j].record(st)
+    device_wait(args, world, idx, streams, rank)
+    wall = time.perf_counter() - t0
+    lat = [s.elapsed_time(e) for s, e in zip(starts, ends)]
+    out = [percentile(lat, 0.99), sum(lat) / n, percentile(lat, 0.5), max(lat), wall]
+    if world > 1:
+        t = torch.tensor(out, dtype=torch.float64, device=ctrl)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out = [float(x) for x in t]
+    return {"inflight": depth, "samples": n, "p99_ms": round(out[0], 4), "mean_ms": round(out[1], 4),
+            "p50_ms": round(out[2], 4), "max_ms": round(out[3], 4), "qps": round(n * args.batch / out[4], 1)}
 
 
 def rank_breakdown(rank, prof, ms_per_step, step_ms_single):
@@ -1122,6 +1182,10 @@ def run(vdb, args, device, rank, world):
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "p99_ms": round(p99, 4),
         "p99_ms_one_in_flight": round(p99_single, 4),
+        # (p99 from >= 1000-batch latency legs; the K timed steps' own p99 beside it)
+        "p99_samples": args.latency_batches if res["latency_legs"] else args.steps,
+        "p99_ms_timed_steps": round(res["p99_steps"], 4),
+        "latency_legs": list(res["latency_legs"].values()),
         # with `inflight` batches in flight a batch's latency is at least inflight x ms_per_step
         # on average (Little's law); p99 / mean shows the spread around that
         "latency_mean_ms": round(res["lat_mean"], 4),

@@ -56,7 +56,7 @@ class CacheStats(ctypes.Structure):
                 ("screen_resident", ctypes.c_int32), ("reserved", ctypes.c_int32), ("screen_bytes", ctypes.c_uint64),
                 ("screen_batches", ctypes.c_uint64), ("screen_rows_fetched", ctypes.c_uint64),
                 ("screen_row_bytes", ctypes.c_uint64), ("screen_reruns", ctypes.c_uint64),
-                ("screen_rows_cached", ctypes.c_uint64)]
+                ("screen_rows_cached", ctypes.c_uint64), ("screen_fallbacks", ctypes.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

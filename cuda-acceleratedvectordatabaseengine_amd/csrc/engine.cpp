@@ -678,24 +678,27 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->set_device();
             h->quiesce();
             h->screen_cand_cap = (uint32_t)value;
+        } else if (n == "tier_cand_max") {
+            require(value >= 1024 && value <= (1ll << 31), "tier_cand_max is 1024 .. 2^31");
+            h->tier_cand_max = (uint32_t)value;
         } else if (n == "screen_floor_ppm") {
             require(value >= 0 && value <= 1000000, "screen_floor_ppm is 0 (never) .. 1000000");
-            h->screen_floor_ppm = (uint32_t)value;
-            h->screen_skip_left = h->screen_floor_streak = h->floor_probe = 0;
+            h->floor.ppm = (uint32_t)value;
+            h->floor.reset_state();
         } else if (n == "screen_floor_min") {
             require(value >= 0, "screen_floor_min is >= 0");
-            h->screen_floor_min = (uint64_t)value;
+            h->floor.min_pairs = (uint64_t)value;
         } else if (n == "screen_thr_every") {
             require(value >= 0 && value <= 1024, "screen_thr_every is 0 (automatic) .. 1024");
             h->screen_thr_every = (uint32_t)value;
         } else if (n == "screen_floor_skip") {
             require(value >= 1 && value < (1ll << 20), "screen_floor_skip is 1 .. 2^20");
-            h->screen_floor_skip = (uint32_t)value;
+            h->floor.skip = (uint32_t)value;
         } else if (n == "tier_row_cache") {
             h->set_device();
             h->quiesce();
             h->tier_row_cache = value != 0;
-            if (h->tiered() && h->file_home() && h->screen_ready) h->fill_row_cache();
+            if (h->tier_row_cache && h->tiered() && h->file_home() && h->screen_ready) h->fill_row_cache();
         } else if (n == "tier_row_qd") {
             require(value >= 1 && value <= 4096, "tier_row_qd is 1 .. 4096");
             h->tier_row_qd = (uint32_t)value;
@@ -777,6 +780,7 @@ int vdb_ivf_cache_stats(vdb_ivf* h, vdb_ivf_cache_stats_t* out) {
             out->screen_row_bytes += m->screen_row_bytes;
             out->screen_reruns += m->screen_reruns;
             out->screen_rows_cached += m->screen_rows_cached;
+            out->screen_fallbacks += m->screen_tier_fallbacks;
         }
     });
 }
@@ -830,7 +834,7 @@ int vdb_ivf_profile_reset(vdb_ivf* h) {
         p->set_device();
         HIPCHECK(hipDeviceSynchronize());
         p->events_used = 0;
-        p->screen_floor_batches = p->screen_floor_trips = 0;
+        p->floor.batches = p->floor.trips = 0;
         HIPCHECK(hipMemsetAsync(p->stats.ensure(16), 0, 128, p->stream));
         HIPCHECK(hipStreamSynchronize(p->stream));
         h->set_device();
@@ -889,8 +893,8 @@ int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
         p.exact_reranks = st[5] + st[10];
         p.bounded_blocks = st[6] + st[9];
         p.screen_collected = st[8];
-        p.screen_floor_batches = h->screen_floor_batches;
-        p.screen_floor_trips = h->screen_floor_trips;
+        p.screen_floor_batches = h->floor.batches;
+        p.screen_floor_trips = h->floor.trips;
         p.computed_vectors = st[7];
         *out = p;
         hh->set_device();

@@ -38,6 +38,7 @@
 
 #include "../../include/vdb_ivf.h"
 #include "kernels.hpp"
+#include "floor.hpp"
 #include "uring.hpp"
 
 namespace vdbe {
@@ -331,10 +332,12 @@ struct vdb_ivf {
     uint32_t screen_cand_cap = 4u << 20;  // collected candidates per batch (an overflowing pair is recomputed whole)
     // One fp32 copy of the lists in HBM: while the screen is built, the row-major copy
     // (screen_rows, slot order: what the exact re-checks read) is the only one and the
-    // interleaved arena is released (arena_dropped); whatever needs the arena (an exact-path
-    // search: k > 64 or the screen off; an add / relayout; export; save) rebuilds it from the
-    // rows first (ensure_arena: one interleave pass), and it then stays until the next
-    // screen build. Footprint while screening: rows + shadow + norms + ids ~ 1.5x the lists.
+    // interleaved arena is released (arena_dropped). Exact-path searches (k > 64, the
+    // run-time floor's batches) scan the row-major copy itself (ScanArgs::rows_layout: no
+    // rebuild, no quiesce, no second copy); what needs the interleaved layout (an add /
+    // relayout, the screen off, the opt-in bounded scan, Cosine) rebuilds it from the rows
+    // first (ensure_arena: one interleave pass). Footprint while screening: rows + shadow +
+    // norms + ids ~ 1.5x the lists, whatever k the searches ask for.
     bool arena_dropped = false;
     // The screen in the list-cache tier (an index larger than HBM, configs[4]): the shadow,
     // norms and ids of EVERY stored list stay HBM-resident (half the fp32 list bytes), packed
@@ -360,49 +363,23 @@ struct vdb_ivf {
     DevBuf<ulonglong2> cache_src;      // ... per batch {row index, cache slot} of those survivors
     std::vector<ulonglong2> cache_src_host;
     uint32_t tier_cand_cap = 0;        // ... a candidate capacity grown by an overflow
-    // Run-time floor under the screen (lists in HBM): every deferred batch reports to
-    // page-locked host memory its survivors (or an overflow of the candidate buffer), its
-    // (query, vector) pairs and k x its valid (query, list) pairs (the survivors no screen can
-    // avoid). When a completed batch of at least screen_floor_min pairs overflowed, or its
-    // survivors beyond those exceed screen_floor_ppm of its pairs (a data regime where the
-    // bound is wider than the distance spread: the exact re-checks then cost more than the
-    // exact scan saves), the next batches run the exact scan, then the screen is tried again:
-    // screen_floor_skip batches after a first trip, twice as many after each further trip in
-    // a row (at most 32x), so a dataset that never screens pays one screened batch per
-    // thousand: after a trip, the screen is retried on one batch, and the batches issued
-    // while its report is outstanding run the exact scan (the reports of batches already in
-    // flight at a trip belong to that trip). Results are the same either way; only speed changes. (Break-even at cfg3: the
-    // exact scan 4.9 ms against the screen's 2.7 ms plus ~4.6 ns per survivor, ~9 % of the
-    // batch's 5.0M pairs; 5 % leaves room for the retries.)
-    uint32_t screen_floor_ppm = 50000;  // option screen_floor_ppm (0: never fall back)
-    uint32_t screen_floor_skip = 32;    // option screen_floor_skip
-    uint64_t screen_floor_min = 1u << 22;  // option screen_floor_min (pairs of a batch the floor judges)
-    uint32_t screen_skip_left = 0, screen_floor_seq = 0, screen_floor_seen = 0, screen_floor_streak = 0;
-    uint32_t floor_probe = 0, floor_trip_seq = 0;  // (the retry batch's sequence; the last trip's)
-    uint64_t screen_floor_batches = 0, screen_floor_trips = 0;
-    DevBuf<uint4> floor_host;           // page-locked, one entry per workspace slot
-    void floor_poll() {
-        if (!floor_host.p) return;
-        for (int i = 0; i < kSlots; ++i) {
-            const volatile uint32_t* f = (const volatile uint32_t*)(floor_host.p + i);
-            const uint4 v = make_uint4(f[0], f[1], f[2], f[3]);
-            if (!v.z || (int32_t)(v.z - screen_floor_seen) <= 0) continue;
-            screen_floor_seen = v.z;
-            const bool probe = floor_probe && v.z == floor_probe;
-            if (probe) floor_probe = 0;
-            if (!screen_floor_ppm || v.y < screen_floor_min) continue;
-            if (screen_floor_trips && (int32_t)(v.z - floor_trip_seq) <= 0) continue;  // (in flight at the trip)
-            const uint64_t excess = v.x > v.w ? (uint64_t)v.x - v.w : 0;
-            if (v.x == ~0u || excess * 1000000ull > (uint64_t)screen_floor_ppm * v.y) {
-                screen_skip_left = screen_floor_skip << std::min<uint32_t>(screen_floor_streak, 5);
-                ++screen_floor_streak;
-                ++screen_floor_trips;
-                floor_trip_seq = screen_floor_seq;
-            } else if (probe) {
-                screen_floor_streak = 0;
-            }
-        }
-    }
+    // ... at most this many candidates per batch (option tier_cand_max; never below
+    // screen_cand_cap): a batch that needs more is served by the exact list-cache path
+    uint32_t tier_cand_max = 32u << 20;
+    uint64_t screen_tier_fallbacks = 0;
+    bool force_exact = false;          // (that path's batches: never screened)
+    // Run-time floor under the screen (lists in HBM; floor.hpp): every deferred batch reports
+    // its survivors (or an overflow of its candidate buffer), its (query, vector) pairs and k x
+    // its valid (query, list) pairs into a ring of page-locked host memory, read without
+    // synchronisation when a later batch is planned. A batch whose survivors beyond those
+    // exceed screen_floor_ppm of its pairs (a regime where the bound is wider than the
+    // distance spread) sends the next batches to the exact scan, with backoff, then one
+    // probe batch retries the screen. (Break-even at cfg3: the exact scan 4.9 ms against the
+    // screen's 2.7 ms plus ~4.6 ns per survivor, ~9 % of the batch's 5.0M pairs; 5 % leaves
+    // room for the retries.) Results are the same either way; only speed changes.
+    ScreenFloor floor;
+    DevBuf<uint4> floor_host;  // page-locked: ScreenFloor::kRing report entries
+    const volatile uint32_t* floor_entry(uint32_t i) const { return (const volatile uint32_t*)(floor_host.p + i); }
     DevBuf<uint4> screen_sh;
     DevBuf<float> screen_rows;
     DevBuf<float4> screen_meta;
@@ -962,7 +939,8 @@ struct vdb_ivf {
         screen_fmt_i8 = i8;
         try {
             screen_sh.ensure(vdbk::screen_shadow_u4(arena_blocks, d4, i8));
-            screen_rows.ensure((size_t)arena_blocks * 64 * dp);
+            // (+ one slack block: the exact scans' tile pipeline reads one block past a segment)
+            screen_rows.ensure((size_t)(arena_blocks + 1) * 64 * dp);
             screen_meta.ensure((size_t)arena_blocks * 64);
             screen_blist.ensure(arena_blocks);
             if (i8) screen_scale.ensure((size_t)arena_blocks * 64);
@@ -972,6 +950,7 @@ struct vdb_ivf {
             return;
         }
         HIPCHECK(hipMemcpyAsync(screen_blist.p, blist.data(), arena_blocks * 4, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipMemsetAsync(screen_rows.p + (size_t)arena_blocks * 64 * dp, 0, (size_t)64 * dp * 4, stream));
         vdbk::launch_screen_build(arena.p, arena_blocks, d4, screen_blist.p, cent_rm.p, screen_sh.p, screen_rows.p,
                                   screen_meta.p, stream, i8 ? screen_scale.p : nullptr);
         HIPCHECK(hipGetLastError());
@@ -1989,7 +1968,7 @@ struct vdb_ivf {
         if (n == 0 || P == 0) return;
         quiesce();
         SearchSlot w;
-        const uint32_t bmax = batch_cap(P);
+        const uint32_t bmax = batch_cap(P, 1);
         ensure_workspace(w, (uint32_t)std::min<uint64_t>(bmax, n), P, 1);
         DevBuf<uint32_t> d_counts;
         HIPCHECK(hipMemsetAsync(d_counts.ensure(nlist), 0, nlist * 4, stream));
@@ -2092,7 +2071,10 @@ struct vdb_ivf {
     // Probe inversion, fine scan (search_list_cpu, cpp:339-384) and merges
     // (merge_results, cpp:474-518) of a batch whose padded queries are in w.qpad and
     // probes in w.probes.
-    void scan_batch(SearchSlot& w, uint32_t B, uint32_t P, uint32_t k, float* out_d_, uint64_t* out_i_, hipStream_t s,
+    // Returns false (nothing merged) only for a screened batch of the tier's file home whose
+    // candidates would need a buffer above tier_cand_max: the caller serves it through the
+    // exact list-cache path instead (run_batch).
+    bool scan_batch(SearchSlot& w, uint32_t B, uint32_t P, uint32_t k, float* out_d_, uint64_t* out_i_, hipStream_t s,
                     const uint32_t* req_start, uint32_t b0, EventSet* ev) {
         const int regs_k = vdbk::topk_regs(k);
         const uint32_t group = (uint32_t)vdbk::scan_group(regs_k);
@@ -2103,41 +2085,30 @@ struct vdb_ivf {
         if (tiered() && tier_ev_used) HIPCHECK(hipStreamWaitEvent(s, tier_ev, 0));
         const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
         const uint64_t max_wide = max_items / 4 + BP + 1;
-        const int waves = wide_group == 32 ? 8 : 4;  // workgroup shape of the wide scan
+        if (screen_stale) screen_update();
+        // the screened scan (default, L2 / IP, k <= 64): items of swq queries
+        const uint32_t swq = screen_width(k, P);
+        bool screened = swq != 0 && !force_exact;
+        uint32_t floor_seq = 0;
+        if (screened && !tiered() && screen_defer)  // the run-time floor (lists in HBM only)
+            screened = floor.plan([this](uint32_t i) { return floor_entry(i); }, &floor_seq);
+        // Exact scans on lists in HBM whose interleaved arena was released read the row-major
+        // copy (4-wave items); the opt-in bounded scan needs the interleaved layout back.
+        bool rows_l = !screened && arena_dropped && !tiered();
+        if (rows_l && scan_mfma_min && regs_k == 1 && wide_scan && metric != 2) {
+            ensure_arena();
+            rows_l = false;
+        }
+        const int waves = wide_group == 32 && !rows_l ? 8 : 4;  // workgroup shape of the wide scan
         // (Cosine: every CPU-path distance is 0.0f, A5; its lists scan as narrow items only)
         const bool wide = regs_k == 1 && wide_scan && metric != 2 && vdbk::scan_wide_fits(d4, k, waves);
         // segments per item: one per wave (more adds tail latency, no throughput)
         const uint32_t segs_item = segs_item_opt ? segs_item_opt : (uint32_t)waves;
         // wide items of many queries: bounded on the matrix cores (L2 / IP, 16-query items)
-        // the screened scan (default): its items are the exact scan's 16-query wide items
-        // and narrow items
-        if (screen_stale) screen_update();
-        // 32-query items (option screen_group) where their shared lists fit the LDS
-        // 32-query items (option screen_group): the deferred kernel feeds each shadow tile to two
-        // A operands; the inline kernel splits its waves in two halves
-        // (0 = automatic: 32 from nprobe 64 up, where hub lists are probed by many queries of a
-        // batch: cfg4 shard collect 4.45 vs 4.69 ms; 16 below: cfg3 2.54 vs 2.72 ms)
-        const uint32_t sg_want = screen_group ? screen_group : (screen_defer && P >= 64 ? 32u : 16u);
-        const uint32_t swq = sg_want == 32 && (screen_defer || vdbk::scan_screen_fits(k, dp, 32)) ? 32u : 16u;
-        bool screened = screen_ready && (!tiered() || screen_defer) && (screen_defer || !screen_fmt_i8) &&
-                        regs_k == 1 && metric != 2 &&
-                        vdbk::scan_screen_fits(k, dp, swq);
-        bool floor_retry = false;
-        if (screened && !tiered() && screen_defer) {  // the run-time floor (lists in HBM only)
-            floor_poll();
-            if (screen_skip_left || floor_probe) {
-                if (screen_skip_left) --screen_skip_left;
-                ++screen_floor_batches;
-                screened = false;
-            } else {
-                floor_retry = screen_floor_streak > 0;
-            }
-        }
-        if (!screened && arena_dropped) ensure_arena();  // (the exact scans read the arena)
-        const uint32_t mfma_min = !screened && wide && waves == 4 && metric != 2 && !(VDB_SCAN_DIAG & 2) &&
+        const uint32_t mfma_min = !screened && !rows_l && wide && waves == 4 && metric != 2 && !(VDB_SCAN_DIAG & 2) &&
                                           vdbk::scan_bounded_fits(d4, k)
                                       ? scan_mfma_min : 0u;
-        const int plan_wide = screened ? (int)swq : (wide ? (int)wide_group : 0);
+        const int plan_wide = screened ? (int)swq : (wide ? 4 * waves : 0);
         // (screened items: segs_per_item segments, default 4; a wave's top-k carries across
         // the segments it takes from one item)
         const uint32_t segs_screen = segs_item_opt ? segs_item_opt : screen_segs_auto;
@@ -2153,10 +2124,12 @@ struct vdb_ivf {
             if (prev.scan_done) HIPCHECK(hipStreamWaitEvent(s, prev.scan_done, 0));
         }
         if (ev) HIPCHECK(hipEventRecord(ev->scan_begin, s));
-        vdbk::ScanArgs sa{tiered() ? cache.p : arena.p, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.q, w.items.p, w.items_w.p,
+        const float4* lists = tiered() ? cache.p : rows_l ? (const float4*)screen_rows.p : arena.p;
+        vdbk::ScanArgs sa{lists, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.q, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
                                 wide_stride, w.counters.p + 4, seg_blocks, segs_item, 0, w.thr.p,
                                 mfma_min, bounded_stats ? stats.p + 5 : nullptr};
+        sa.rows_layout = rows_l ? 1u : 0u;
         // the bounded items first (the batch's most-probed lists), on the same stream
         if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
         if (screened) {
@@ -2228,15 +2201,13 @@ struct vdb_ivf {
                     sa.ovf = w.ovf.p;
                     sa.ublist = w.ublist.p;
                     sa.ubcnt = w.ubcnt.p;
-                    if (!tiered()) {
+                    if (floor_seq) {  // (its own ring entry, whatever slot or stream runs it)
                         if (!floor_host.p) {
                             floor_host.host = true;
-                            std::memset(floor_host.ensure(kSlots), 0, kSlots * sizeof(uint4));
+                            std::memset(floor_host.ensure(ScreenFloor::kRing), 0, ScreenFloor::kRing * sizeof(uint4));
                         }
-                        sa.floor_out = floor_host.p + (in_ring ? (&w - slots) : 0);
-                        if (!++screen_floor_seq) ++screen_floor_seq;  // (0: never written)
-                        sa.floor_seq = screen_floor_seq;
-                        if (floor_retry) floor_probe = screen_floor_seq;
+                        sa.floor_out = floor_host.p + floor_seq % ScreenFloor::kRing;
+                        sa.floor_seq = floor_seq;
                     }
                     sa.mstats = bounded_stats && !pass ? stats.p + 8 : nullptr;
                     if (ev) HIPCHECK(hipEventRecord(ev->collect_begin, s));
@@ -2250,7 +2221,14 @@ struct vdb_ivf {
                     uint32_t need = 0;
                     fetched = fetch_survivor_rows(w, ccap, need, s);
                     if (fetched) break;
-                    ccap = std::max<uint32_t>(need + need / 2, ccap + 1024);
+                    const uint64_t grow = std::max<uint64_t>((uint64_t)need + need / 2, (uint64_t)ccap + 1024);
+                    if (grow > std::max<uint64_t>(tier_cand_max, screen_cand_cap)) {
+                        // (a regime where the bound is wider than the distance spread: the
+                        // survivors' rows would cost more than the lists)
+                        ++screen_tier_fallbacks;
+                        return false;
+                    }
+                    ccap = (uint32_t)grow;
                     tier_cand_cap = ccap;  // (kept for the next batches)
                     ++screen_reruns;
                 }
@@ -2299,7 +2277,7 @@ struct vdb_ivf {
             if (stale) w.carry_sel ^= 1u;
             if (ev) HIPCHECK(hipEventRecord(ev->end, s));
             HIPCHECK(hipGetLastError());
-            return;
+            return true;
         }
         vdbk::launch_merge_partials(regs_k, (uint32_t)max_l1, w.probes.p, d_count_global.p, w.nseg_qp.p, w.pbqp.p, w.l1base.p,
                                     w.l1_items.p, w.counters.p, w.part_d.p, w.part_i.p, k, w.l1_d.p, w.l1_i.p, s);
@@ -2312,6 +2290,7 @@ struct vdb_ivf {
                                w.carry_i.p, s);
         if (ev) HIPCHECK(hipEventRecord(ev->end, s));
         HIPCHECK(hipGetLastError());
+        return true;
     }
 
     // One batch, every list HBM-resident (or the tier with every stored list cached).
@@ -2321,7 +2300,17 @@ struct vdb_ivf {
         if (ev) HIPCHECK(hipEventRecord(ev->begin, s));
         coarse_batch(w, d_q, B, P, s);
         if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
-        scan_batch(w, B, P, k, out_d_, out_i_, s, req_start, b0, ev);
+        if (!scan_batch(w, B, P, k, out_d_, out_i_, s, req_start, b0, ev)) {
+            // the screened tier could not serve it (tier_cand_max): the exact list-cache path
+            force_exact = true;
+            try {
+                search_tiered(w, d_q, B, P, k, out_d_, out_i_, s, req_start, b0);
+            } catch (...) {
+                force_exact = false;
+                throw;
+            }
+            force_exact = false;
+        }
         return true;
     }
 
@@ -2338,10 +2327,11 @@ struct vdb_ivf {
     //  * a victim is the cached list whose next use in the call is furthest away (not
     //    used again: first), then the least recently used; sub-batch i's lists (and i+1's)
     //    are never evicted while i runs.
+    // (qbase: the call-global index of d_q's first query, for the stale-slot semantics)
     void search_tiered(SearchSlot& w, const float* d_q, uint32_t n, uint32_t P, uint32_t k, float* d_dist,
-                       uint64_t* d_ids, hipStream_t s, const uint32_t* req_start) {
+                       uint64_t* d_ids, hipStream_t s, const uint32_t* req_start, uint32_t qbase = 0) {
         if (tier_call_used) HIPCHECK(hipEventSynchronize(tier_call_ev));  // probe_stage is reused
-        const uint32_t bmax = batch_cap(P);
+        const uint32_t bmax = batch_cap(P, k);
         // 1. probes of the whole call
         probe_stage.host = true;
         uint32_t* hp = probe_stage.ensure((size_t)n * P);
@@ -2429,7 +2419,8 @@ struct vdb_ivf {
             stage_queries(w, d_q + (size_t)b0 * dim, B, s);
             HIPCHECK(hipMemcpyAsync(w.probes.p, hp + (size_t)b0 * P, (size_t)B * P * 4, hipMemcpyHostToDevice, s));
             if (ev) HIPCHECK(hipEventRecord(ev->coarse_end, s));
-            scan_batch(w, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s, req_start, b0, ev);
+            require(scan_batch(w, B, P, k, d_dist + (size_t)b0 * k, d_ids + (size_t)b0 * k, s, req_start, qbase + b0, ev),
+                    "tier sub-batch not served", VDB_ERR_STATE);
             HIPCHECK(hipEventRecord(sb_done[b & 1], s));
             ++tier_subbatches;
             prefetched = false;
@@ -2456,16 +2447,40 @@ struct vdb_ivf {
         tier_call_used = true;
     }
 
-    // The screen serves a search with this k (the tier: the deferred scan with its shadow
-    // resident; built lazily, so a stale screen is rebuilt first).
-    bool screen_serves(uint32_t k) {
+    // The screened scan's item width for a search (16 or 32 queries), or 0 when the screen
+    // does not serve it. ONE decision for scan_batch and for the tier's routing
+    // (screen_serves): a search the tier sends past its list cache is always screened.
+    // 32-query items (option screen_group; 0 = automatic: 32 from nprobe 64 up, where hub
+    // lists are probed by many queries of a batch: cfg4 shard collect 4.45 vs 4.69 ms; 16
+    // below: cfg3 2.54 vs 2.72 ms): the deferred kernel feeds each shadow tile to two A
+    // operands (its LDS is static: any k <= 64); the inline kernel splits its waves in two
+    // halves where the item's lists fit its LDS, else it runs 16-query items.
+    uint32_t screen_width(uint32_t k, uint32_t P) const {
+        if (!screen_ready || metric == 2 || vdbk::topk_regs(k) != 1) return 0;
+        if (tiered() && !screen_defer) return 0;    // (the tier's screen is the deferred one)
+        if (!screen_defer && screen_fmt_i8) return 0;  // (the inline kernel reads a bf16 shadow)
+        const uint32_t want = screen_group ? screen_group : (screen_defer && P >= 64 ? 32u : 16u);
+        if (want == 32 && vdbk::scan_screen_fits(k, dp, 32, screen_defer)) return 32;
+        return vdbk::scan_screen_fits(k, dp, 16, screen_defer) ? 16 : 0;
+    }
+    // The screen serves a search with this k and nprobe (the tier: the deferred scan with its
+    // shadow resident; built lazily, so a stale screen is rebuilt first).
+    bool screen_serves(uint32_t k, uint32_t P) {
         if (screen_stale) screen_update();
-        return screen_ready && (!tiered() || screen_defer) && vdbk::topk_regs(k) == 1 && metric != 2 &&
-               vdbk::scan_screen_fits(k, dp, 16);
+        return screen_width(k, P) != 0;
     }
 
-    uint32_t batch_cap(uint32_t P) const {
-        return std::max<uint32_t>(1, std::min<uint32_t>(batch, vdbk::kPlanMaxPairs / P));
+    // Queries per internal batch: the option `batch`, bounded so that batch x nprobe fits the
+    // plan kernel (8192 pairs) and so that one slot's per-segment partials (B x the segments
+    // of the P largest lists x k x 12 bytes) stay within kPartialBytes: the exact path at
+    // k = 1000 on the 10M x 768 index would otherwise hold 1.5 GB of partials per slot.
+    // Results never depend on batch boundaries.
+    static constexpr uint64_t kPartialBytes = 256ull << 20;
+    uint32_t batch_cap(uint32_t P, uint32_t k) const {
+        uint32_t b = std::max<uint32_t>(1, std::min<uint32_t>(batch, vdbk::kPlanMaxPairs / P));
+        const uint64_t per_query = (P < nseg_prefix.size() ? nseg_prefix[P] : 0) * (uint64_t)k * 12;
+        if (per_query) b = std::max<uint32_t>(1, (uint32_t)std::min<uint64_t>(b, kPartialBytes / per_query));
+        return b;
     }
 
     // Grow a slot-owned buffer; a buffer still read by the slot's previous call is
@@ -2486,7 +2501,7 @@ struct vdb_ivf {
         }
         SearchSlot& w = slots[next_slot];
         next_slot = (next_slot + 1) % kSlots;
-        const uint32_t B = std::min(batch_cap(P), n);
+        const uint32_t B = std::min(batch_cap(P, k), n);
         ensure_workspace(w, B, P, k);
         if (xworld) {
             const uint64_t rb = vdb_rank_record_bytes(B, k);
@@ -2566,12 +2581,12 @@ struct vdb_ivf {
             end_call(w, s);
             return;
         }
-        if (tiered() && resident_n < storable_n && !screen_serves(k)) {  // (every stored list cached: the plain path)
+        if (tiered() && resident_n < storable_n && !screen_serves(k, P)) {  // (every stored list cached: the plain path)
             search_tiered(w, d_q, n, P, k, d_dist, d_ids, s, req_start);
             end_call(w, s);
             return;
         }
-        const uint32_t bmax = batch_cap(P);
+        const uint32_t bmax = batch_cap(P, k);
         for (uint32_t b0 = 0, B = std::min(bmax, n); b0 < n; b0 += B, B = std::min(B, n - b0)) {
             float* od = xchg ? rec_dist(w) : d_dist + (size_t)b0 * k;
             uint64_t* oi = xchg ? rec_ids(w, B, k) : d_ids + (size_t)b0 * k;
@@ -2588,11 +2603,11 @@ struct vdb_ivf {
         slot_buf(w, w.xrec, vdb_rank_record_bytes(n, k));
         float* rd = rec_dist(w);
         uint64_t* ri = rec_ids(w, n, k);
-        if (tiered() && resident_n < storable_n && !screen_serves(k)) {
+        if (tiered() && resident_n < storable_n && !screen_serves(k, P)) {
             search_tiered(w, d_q, n, P, k, rd, ri, s, req_start);
             return;
         }
-        const uint32_t bmax = batch_cap(P);
+        const uint32_t bmax = batch_cap(P, k);
         for (uint32_t b0 = 0, B = std::min(bmax, n); b0 < n; b0 += B, B = std::min(B, n - b0))
             run_batch(w, d_q + (size_t)b0 * dim, B, P, k, rd + (size_t)b0 * k, ri + (size_t)b0 * k, s, req_start,
                       b0);

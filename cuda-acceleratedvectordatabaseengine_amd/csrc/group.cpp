@@ -358,7 +358,8 @@ void vdb_ivf::group_search_device(const float* d_q, uint32_t n, uint32_t P, uint
         for_members(this, [&](size_t m) { members[m]->call_to_record(*w[m], qm[m], n, P, k, ms[m], rm[m]); });
         exchange(n, d_dist, d_ids);
     } else {
-        const uint32_t bmax = members[0]->batch_cap(P);
+        uint32_t bmax = members[0]->batch_cap(P, k);  // (the smallest member cap: partial bytes per member)
+        for (auto& mb : members) bmax = std::min(bmax, mb->batch_cap(P, k));
         for (uint32_t b0 = 0, B = std::min(bmax, n); b0 < n; b0 += B, B = std::min(B, n - b0)) {
             for (uint32_t m = 0; m < M; ++m) {
                 vdb_ivf& mb = *members[m];

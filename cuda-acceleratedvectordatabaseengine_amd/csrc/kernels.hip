@@ -1025,24 +1025,44 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
 //   compute(x, t): consume tile t (0 <= t < d4) of the current block
 //   finish(j, id): block j done; id = this lane's id slot in block j
 
-template <int T, class Compute, class Finish>
+//
+// ROWS: the same segment read from the lists' row-major fp32 copy ([slot][dp], the screen's
+// rows, then the lists' only fp32 copy; one slack block past the last list) instead of the
+// interleaved arena: lane = vector still, tile t of block j at base + 64 d4 j + t, so one
+// wave-load touches 64 rows (16 B each) and the row's next tiles are the same lines (plain
+// loads, which keep them in the L1/L2 for those tiles). Exact-path searches on an index
+// whose arena was released (k > 64, the run-time floor) run on it without rebuilding it.
+template <bool ROWS>
+__device__ __forceinline__ const float4* lane_base(const float4* lists, uint64_t b0, uint32_t d4, int lane) {
+    return ROWS ? lists + (b0 * 64 + (uint64_t)lane) * d4 : lists + b0 * d4 * 64 + lane;
+}
+
+template <int T, bool ROWS = false, class Compute, class Finish>
 __device__ __forceinline__ void stream_blocks(const float4* __restrict__ base, const uint64_t* __restrict__ ids,
                                               uint32_t d4, uint32_t nb, Compute&& compute, Finish&& finish) {
+    constexpr size_t TS = ROWS ? 1 : 64;  // float4 between a lane's consecutive tiles
+    auto ld = [](const float4* q) -> float4 {
+        if constexpr (ROWS) return *q;
+        else return load_nt(q);
+    };
     float4 x[T];
     const float4* p = base;
 #pragma unroll
-    for (int t = 0; t < T; ++t) x[t] = load_nt(p + (size_t)t * 64);
+    for (int t = 0; t < T; ++t) x[t] = ld(p + (size_t)t * TS);
     uint64_t id_next = __builtin_nontemporal_load(ids);
     for (uint32_t j = 0; j < nb; ++j) {
         const uint64_t id = id_next;
         id_next = __builtin_nontemporal_load(ids + (size_t)(j + 1) * 64);
         for (uint32_t t0 = 0; t0 < d4; t0 += T) {
+            // the next round's first tile (row-major: past the row's end, the next block's row)
+            const float4* pn = p + (size_t)T * TS;
+            if (ROWS && t0 + T == d4) pn += (size_t)63 * d4;
             static_for<0, T>([&](auto u) {
                 constexpr int t = decltype(u)::value;
                 compute(x[t], t0 + t, u);
-                if (!(VDB_SCAN_DIAG & 32)) x[t] = load_nt(p + (size_t)(T + t) * 64);  // (DIAGNOSTIC 32: no list reads)
+                if (!(VDB_SCAN_DIAG & 32)) x[t] = ld(pn + (size_t)t * TS);  // (DIAGNOSTIC 32: no list reads)
             });
-            p += (size_t)T * 64;
+            p = pn;
         }
         finish(j, id);
     }
@@ -1050,7 +1070,7 @@ __device__ __forceinline__ void stream_blocks(const float4* __restrict__ base, c
 
 // One narrow wave-item: one segment of a small list against G <= 4 queries whose
 // dims are wave-uniform scalar loads; each query's top-k lives in registers.
-template <int R, int G, int M>
+template <int R, int G, int M, bool ROWS>
 __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) {
     const int lane = lane_id();
     const uint32_t count = a.count[it.list];
@@ -1107,7 +1127,9 @@ __device__ __forceinline__ void scan_item(const ScanArgs& a, const ScanItem it) 
 #pragma unroll
         for (int g = 0; g < G; ++g) acc[g] = 0.0f;
     };
-    stream_blocks<kTilePipeNarrow>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
+    // (row-major: 8 tiles, half a row's 128-byte line pair, in flight per lane)
+    stream_blocks<ROWS ? 8 : kTilePipeNarrow, ROWS>(lane_base<ROWS>(a.arena, b0, d4, lane), a.ids + b0 * 64 + lane, d4,
+                                                    nb, compute, finish);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
         if (g >= np) break;
@@ -1186,7 +1208,7 @@ constexpr bool kBigGroupPrefetch = VDB_BIG_GROUP_PREFETCH != 0;
 #define VDB_ODD_PAIRS 1
 #endif
 constexpr bool kOddPairs = VDB_ODD_PAIRS != 0;
-template <int GP, int M, bool SPLIT, bool ODD>
+template <int GP, int M, bool SPLIT, bool ODD, bool ROWS>
 __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem it, const float4* qlds,
                                                const uint32_t pstride_rt, const int q0, const int np, float* tk_d,
                                                uint64_t* tk_i, uint32_t* s_thr, const uint32_t seg) {
@@ -1325,7 +1347,7 @@ __device__ __forceinline__ void scan_wide_wave(const ScanArgs& a, const ScanItem
     };
     // more than 8 pairs: fewer tiles in flight (the pairs' query registers take the rest)
     constexpr int T = GP <= 8 ? kTilePipe : (kBigGroupPrefetch ? kTilePipe / 4 : kTilePipe / 2);
-    stream_blocks<T>(a.arena + b0 * d4 * 64 + lane, a.ids + b0 * 64 + lane, d4, nb, compute, finish);
+    stream_blocks<T, ROWS>(lane_base<ROWS>(a.arena, b0, d4, lane), a.ids + b0 * 64 + lane, d4, nb, compute, finish);
     // the segment's k-th distances lower the list-wide thresholds for later items
 #pragma unroll
     for (int g = 0; g < G; ++g)
@@ -1539,14 +1561,14 @@ __device__ __forceinline__ void scan_wide_wave_mfma(const ScanArgs& a, const Sca
 }
 
 // One wave-item of a narrow list (<= 4 pairs of one segment).
-template <int R, int M>
+template <int R, int M, bool ROWS>
 __device__ __forceinline__ void scan_narrow(const ScanArgs& a, const ScanItem it) {
     constexpr int GMAX = scan_group_max(R);
     switch (it.npairs) {
-        case 1: scan_item<R, 1, M>(a, it); break;
-        case 2: if constexpr (GMAX >= 2) scan_item<R, 2, M>(a, it); break;
-        case 3: if constexpr (GMAX >= 3) scan_item<R, 3, M>(a, it); break;
-        case 4: if constexpr (GMAX >= 4) scan_item<R, 4, M>(a, it); break;
+        case 1: scan_item<R, 1, M, ROWS>(a, it); break;
+        case 2: if constexpr (GMAX >= 2) scan_item<R, 2, M, ROWS>(a, it); break;
+        case 3: if constexpr (GMAX >= 3) scan_item<R, 3, M, ROWS>(a, it); break;
+        case 4: if constexpr (GMAX >= 4) scan_item<R, 4, M, ROWS>(a, it); break;
         default: break;
     }
 }
@@ -1554,7 +1576,7 @@ __device__ __forceinline__ void scan_narrow(const ScanArgs& a, const ScanItem it
 // ivf_scan_narrow: the fine scan (search_list_cpu, cpp:347-370) of the batch's small
 // lists: each wave takes one narrow item (one segment x <= 4 queries, queries via
 // scalar loads, top-k in registers).
-template <int R, int M>
+template <int R, int M, bool ROWS>
 // Persistent: a grid sized to the machine, each wave pulling items from a queue
 // (one device-scope atomic per item) until the batch's items run out.
 __global__ __launch_bounds__(256) void ivf_scan_narrow(ScanArgs a) {
@@ -1564,13 +1586,13 @@ __global__ __launch_bounds__(256) void ivf_scan_narrow(ScanArgs a) {
         if (lane_id() == 0) idx = atomicAdd(&a.work[0], 1u);
         idx = __builtin_amdgcn_readfirstlane(idx);
         if (idx >= n_narrow) break;
-        scan_narrow<R, M>(a, a.items[idx]);
+        scan_narrow<R, M, ROWS>(a, a.items[idx]);
     }
 }
 
 // Narrow items pulled by one wave until the queue is empty (the fused wide scan).
 // (Inlined at both call sites: a real call would spill the wide path's registers.)
-template <int M>
+template <int M, bool ROWS>
 __device__ __forceinline__ void drain_narrow(const ScanArgs& a) {
     const uint32_t n_narrow = a.counters[0];
     for (;;) {
@@ -1578,7 +1600,7 @@ __device__ __forceinline__ void drain_narrow(const ScanArgs& a) {
         if (lane_id() == 0) idx = atomicAdd(&a.work[0], 1u);
         idx = __builtin_amdgcn_readfirstlane(idx);
         if (idx >= n_narrow) break;
-        scan_narrow<1, M>(a, a.items[idx]);
+        scan_narrow<1, M, ROWS>(a, a.items[idx]);
     }
 }
 
@@ -1593,7 +1615,7 @@ __device__ __forceinline__ void drain_narrow(const ScanArgs& a) {
 //    its half of the queries: the two waves streaming one segment run side by side on
 //    the CU, so the second read is served on-chip, and every wave keeps at most 8 query
 //    pairs in registers (the code path that does not spill).
-template <int M, int W>
+template <int M, int W, bool ROWS>
 __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
     constexpr int GW = 4 * W;  // queries per item at most
     // Dynamic LDS: [d4][gpv][2] float4 of staged query pairs (tile-major), then per wave
@@ -1614,7 +1636,7 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
     // Fused launch: narrow items (HBM-bound) run beside the wide ones (often VALU-bound)
     // inside this one persistent grid, no second stream: the last a.fused workgroups
     // start on the narrow queue, and every wave drains it once the wide queue is empty.
-    if (a.fused && blockIdx.x + a.fused >= gridDim.x) drain_narrow<M>(a);
+    if (a.fused && blockIdx.x + a.fused >= gridDim.x) drain_narrow<M, ROWS>(a);
     __shared__ uint32_t s_next;
     __shared__ uint32_t s_seg[2];   // next segment of the current item (per query half)
     __shared__ uint32_t s_thr[GW];  // per query of the item: the best k-th distance reached
@@ -1666,23 +1688,23 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
             if (sg >= seg1) break;
 #define VDB_WW(GPN)                                                                       \
     case GPN:                                                                             \
-        if (W == 8 && split) scan_wide_wave<GPN, M, true, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg); \
-        else if (kOddPairs && (nq & 1)) scan_wide_wave<GPN, M, false, true>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);  \
-        else scan_wide_wave<GPN, M, false, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);            \
+        if (W == 8 && split) scan_wide_wave<GPN, M, true, false, ROWS>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg); \
+        else if (kOddPairs && (nq & 1)) scan_wide_wave<GPN, M, false, true, ROWS>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);  \
+        else scan_wide_wave<GPN, M, false, false, ROWS>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);            \
         break;
             switch (gw) {
                 VDB_WW(1) VDB_WW(2) VDB_WW(3) VDB_WW(4) VDB_WW(5) VDB_WW(6) VDB_WW(7)
                 default:
-                    if (W == 8 && split) scan_wide_wave<8, M, true, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
-                    else if (kOddPairs && (nq & 1)) scan_wide_wave<8, M, false, true>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
-                    else scan_wide_wave<8, M, false, false>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
+                    if (W == 8 && split) scan_wide_wave<8, M, true, false, ROWS>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
+                    else if (kOddPairs && (nq & 1)) scan_wide_wave<8, M, false, true, ROWS>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
+                    else scan_wide_wave<8, M, false, false, ROWS>(a, it, qw, gpv, q0, nq, tk_d, tk_i, s_thr + q0, sg);
                     break;
             }
 #undef VDB_WW
         }
         __syncthreads();  // qlds is restaged by the next wide item
     }
-    if (a.fused) drain_narrow<M>(a);
+    if (a.fused) drain_narrow<M, ROWS>(a);
 }
 
 // ivf_scan_bounded: the wide items of >= a.mfma_min queries (items_w[counters[3] ..
@@ -2557,11 +2579,14 @@ bool scan_wide_fits(uint32_t d4, uint32_t k, int waves) {
 void launch_scan_narrow(int metric, int regs, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
     if (!grid_blocks) return;
     const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
-#define VDB_SN(R)                                                             \
-    do {                                                                      \
-        if (metric == kL2) ivf_scan_narrow<R, kL2><<<g, 256, 0, s>>>(a);      \
-        else if (metric == kIP) ivf_scan_narrow<R, kIP><<<g, 256, 0, s>>>(a); \
-        else ivf_scan_narrow<R, kCos><<<g, 256, 0, s>>>(a);                   \
+    // (row-major lists exist only beside the screen: L2 / IP)
+#define VDB_SN(R)                                                                                    \
+    do {                                                                                             \
+        if (a.rows_layout && metric == kL2) ivf_scan_narrow<R, kL2, true><<<g, 256, 0, s>>>(a);      \
+        else if (a.rows_layout && metric == kIP) ivf_scan_narrow<R, kIP, true><<<g, 256, 0, s>>>(a); \
+        else if (metric == kL2) ivf_scan_narrow<R, kL2, false><<<g, 256, 0, s>>>(a);                 \
+        else if (metric == kIP) ivf_scan_narrow<R, kIP, false><<<g, 256, 0, s>>>(a);                 \
+        else ivf_scan_narrow<R, kCos, false><<<g, 256, 0, s>>>(a);                                   \
     } while (0)
     switch (regs) {
         case 1: VDB_SN(1); break;
@@ -2601,8 +2626,9 @@ void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipSt
     if (!grid_blocks) return;
     static const bool raised = [] {
         // wide items stage up to 16 (32) queries in LDS: allow the whole 160 KB of a CU
-        const void* f4[] = {(const void*)ivf_scan_wide<kL2, 4>, (const void*)ivf_scan_wide<kIP, 4>};
-        const void* f8[] = {(const void*)ivf_scan_wide<kL2, 8>, (const void*)ivf_scan_wide<kIP, 8>};
+        const void* f4[] = {(const void*)ivf_scan_wide<kL2, 4, false>, (const void*)ivf_scan_wide<kIP, 4, false>,
+                            (const void*)ivf_scan_wide<kL2, 4, true>, (const void*)ivf_scan_wide<kIP, 4, true>};
+        const void* f8[] = {(const void*)ivf_scan_wide<kL2, 8, false>, (const void*)ivf_scan_wide<kIP, 8, false>};
         for (const void* f : f4)
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes - wide_static_lds(4)));
         for (const void* f : f8)
@@ -2611,16 +2637,22 @@ void launch_scan_wide(int metric, uint32_t grid_blocks, const ScanArgs& a, hipSt
         return true;
     }();
     (void)raised;
+    // (row-major lists: 4-wave items only; the engine plans 16-query items for them)
     const size_t lds = scan_wide_lds(a.d4, a.k, waves);
-    if (waves == 8) {  // one 8-wave workgroup per CU
+    if (waves == 8 && !a.rows_layout) {  // one 8-wave workgroup per CU
         const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks / 2);
-        if (metric == kL2) ivf_scan_wide<kL2, 8><<<g, 512, lds, s>>>(a);
-        else ivf_scan_wide<kIP, 8><<<g, 512, lds, s>>>(a);
+        if (metric == kL2) ivf_scan_wide<kL2, 8, false><<<g, 512, lds, s>>>(a);
+        else ivf_scan_wide<kIP, 8, false><<<g, 512, lds, s>>>(a);
         return;
     }
     const uint32_t g = std::min<uint32_t>(grid_blocks, kPersistentBlocks);
-    if (metric == kL2) ivf_scan_wide<kL2, 4><<<g, 256, lds, s>>>(a);
-    else ivf_scan_wide<kIP, 4><<<g, 256, lds, s>>>(a);
+    if (a.rows_layout) {
+        if (metric == kL2) ivf_scan_wide<kL2, 4, true><<<g, 256, lds, s>>>(a);
+        else ivf_scan_wide<kIP, 4, true><<<g, 256, lds, s>>>(a);
+        return;
+    }
+    if (metric == kL2) ivf_scan_wide<kL2, 4, false><<<g, 256, lds, s>>>(a);
+    else ivf_scan_wide<kIP, 4, false><<<g, 256, lds, s>>>(a);
 }
 
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global, const uint32_t* nseg_qp,

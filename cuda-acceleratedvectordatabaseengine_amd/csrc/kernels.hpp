@@ -151,6 +151,10 @@ struct ScanArgs {
     uint32_t floor_seq = 0;
     float* ublist = nullptr;    // per sorted pair kUbLists lists of k upper bounds (the waves' running lists)
     uint32_t* ubcnt = nullptr;  // ... and how many were offered
+    // The exact scans (ivf_scan_narrow / ivf_scan_wide, 4-wave items) read `arena` as the
+    // lists' row-major fp32 copy ([slot][dp], one slack block) instead of the interleaved
+    // layout: the arena released while the screen serves (one fp32 copy in HBM).
+    uint32_t rows_layout = 0;
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);
@@ -163,7 +167,7 @@ size_t scan_bounded_lds(uint32_t d4, uint32_t k);
 bool scan_bounded_fits(uint32_t d4, uint32_t k);
 void launch_scan_bounded(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
 // ---- screened scan (screen.hip): L2 / IP, k <= 64, lists in HBM ----
-bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq);
+bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq, bool deferred);
 void launch_gather_cache_rows(const float4* cache, uint32_t d4, const ulonglong2* src, uint32_t n, float* rows,
                               hipStream_t s);
 size_t screen_shadow_u4(uint64_t blocks, uint32_t d4, bool i8 = false);  // shadow size (uint4) incl. the prefetch slack

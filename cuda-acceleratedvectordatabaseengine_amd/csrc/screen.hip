@@ -1251,11 +1251,18 @@ __global__ __launch_bounds__(1024) void ivf_screen_offsets(const uint32_t* __res
     if (threadIdx.x == 0) {
         soff[n] = total;
         counters[kCtrSurv] = total;
-        // (the run-time floor's feedback, one 16-byte vector store to page-locked host memory:
-        // {survivors or ~0 after an overflow, (query, vector) pairs, sequence, k x valid pairs})
-        if (floor_out)
-            *floor_out = make_uint4(counters[kCtrCand] > cap ? ~0u : total, counters[kCtrPairs], floor_seq,
-                                    (uint32_t)min(0xFFFFFFFFull, (unsigned long long)k * n));
+        // (the run-time floor's report into its ring entry of page-locked host memory:
+        // {survivors or ~0 after an overflow, (query, vector) pairs, sequence, k x valid pairs}.
+        // The counts first, then a system-scope release fence, then the sequence number: the
+        // host reads the sequence before and after the counts and keeps only a match (floor.hpp))
+        if (floor_out) {
+            volatile uint32_t* f = (volatile uint32_t*)floor_out;
+            f[0] = counters[kCtrCand] > cap ? ~0u : total;
+            f[1] = counters[kCtrPairs];
+            f[3] = (uint32_t)min(0xFFFFFFFFull, (unsigned long long)k * n);
+            __threadfence_system();
+            f[2] = floor_seq;
+        }
     }
 }
 
@@ -1469,9 +1476,12 @@ void launch_gather_cache_rows(const float4* cache, uint32_t d4, const ulonglong2
     ivf_gather_cache_rows<<<g, 256, 0, s>>>(cache, d4, src, n, (float4*)rows);
 }
 
-bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq) {
+bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq, bool deferred) {
+    // (the deferred collect kernel's LDS is static and independent of k and the item width:
+    // only the exact re-check's row staging counts; the inline kernel stages the item's
+    // queries and its waves' top-k lists)
     return k >= 1 && k <= 64 && dp % 64 == 0 && (wq == 16 || wq == 32) && exact_lds(dp / 4) <= kLdsBytes / 2 &&
-           screen_item_lds(k, wq) + 4 * screen_wave_lds(k) + 256 <= kLdsBytes / 2;
+           (deferred || screen_item_lds(k, wq) + 4 * screen_wave_lds(k) + 256 <= kLdsBytes / 2);
 }
 
 size_t screen_shadow_u4(uint64_t blocks, uint32_t d4, bool i8) {

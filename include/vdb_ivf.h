@@ -268,6 +268,8 @@ typedef struct vdb_ivf_cache_stats_t {
     uint64_t screen_reruns;       /* batches re-run after overflowing the candidate buffer */
     uint64_t screen_rows_cached;  /* survivor rows read from the HBM cache instead of the file
                                      (option tier_row_cache: the largest lists' rows kept there) */
+    uint64_t screen_fallbacks;    /* batches whose candidates would exceed "tier_cand_max": served
+                                     by the exact list-cache path instead */
 } vdb_ivf_cache_stats_t;
 int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
 /* The tier's home on disk (ListPrefetcher::register_list_file / prefetch_lists,
@@ -321,14 +323,16 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * items; 0: narrow items on a second stream), "screen" (1, default: the screened scan — bf16
  * matrix-core distance bounds from a shadow of the lists, exact fp32 sums only for pairs that can
  * reach a list's top-k; L2/IP, k <= 64; the lists are then held as a row-major fp32 copy plus the
- * bf16 shadow and norms, ~1.5x the list bytes; in the list-cache tier the shadow alone stays
+ * bf16 shadow and norms, ~1.5x the list bytes, for every k: exact-path searches, k > 64, scan
+ * the row-major copy; in the list-cache tier the shadow alone stays
  * in HBM and the rows at home; 0: the exact VALU scan of every pair), "screen_group" (16,
  * default, or 32: queries per screened wide item; with the deferred scan every shadow tile
  * then feeds two 16-query A operands, inline: two wave halves), "screen_defer" (1, default:
  * the screen collects candidates against upper-bound thresholds and re-checks afterwards only
  * the survivors of each (query, list) pair's final threshold; 0: re-checks inline as
  * candidates appear), "screen_cand_cap" (collected candidates per batch, default 4M; a pair
- * beyond it is recomputed over its whole list, a file-home tier batch re-run with more),
+ * beyond it is recomputed over its whole list, a file-home tier batch re-run with more, up to
+ * "tier_cand_max" (32M: beyond it that batch is served by the exact list-cache path)),
  * "tier_row_direct" (1, default: the screened tier reads survivors' rows with O_DIRECT),
  * "tier_row_qd" (256: survivor-row reads in flight), "tier_row_cache" (1, default: a file-home
  * screened tier fills its idle HBM cache with the largest lists, whose survivors' rows are then

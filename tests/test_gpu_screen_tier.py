@@ -176,3 +176,76 @@ def test_screened_tier_attach_comm_world1_file_home(tmp_path):
     st = h.cache_stats()
     assert st["screen_batches"] > 0 and st["evictions"] > 0, st
     h.detach_comm()
+
+
+@pytest.mark.parametrize("home", ["host", "file"])
+def test_screened_tier_k64_32_query_items(tmp_path, home):
+    """k = 64 with nprobe >= 64 (32-query items chosen automatically) and with screen_group =
+    32: the tier's routing and the batch agree that the screen serves them, so no batch
+    falls to the exact scan over a cache that does not hold its lists."""
+    from test_gpu_bounded import lists_pair
+    dim, nlist = 64, 80
+    rng = np.random.default_rng(64)
+    X = rng.standard_normal((16000, dim)).astype(np.float32)
+    Q = rng.standard_normal((130, dim)).astype(np.float32)
+    ids = np.arange(len(X), dtype=np.uint64)
+    C = rng.standard_normal((nlist, dim)).astype(np.float32)
+    lists = rng.integers(0, nlist, len(X))
+    g, o = lists_pair(X, ids, lists, C, 0)
+    cache = 24 * block_bytes(dim)  # (a fraction of the lists: the exact path would need the cache)
+    if home == "host":
+        h = g
+        h.set_option("list_cache_bytes", cache)
+    else:
+        path = str(tmp_path / "k64.vdb")
+        g.save(path)
+        del g
+        h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist))
+        h.set_option("list_cache_bytes", cache)
+        h.open_lists(path)
+    for nprobe, sg in ((64, 0), (70, 0), (8, 32), (64, 32), (8, 16)):
+        h.set_option("screen_group", sg)
+        Dr, Ir = o.search(Q, nprobe, 64)
+        b0 = h.cache_stats()["screen_batches"]
+        for batch in (128, 37):
+            h.set_batch(batch)
+            assert_same(*h.search(Q, nprobe=nprobe, k=64), Dr, Ir)
+        assert h.cache_stats()["screen_batches"] > b0, (nprobe, sg)
+
+
+def test_screened_tier_cancellation_falls_back_to_the_list_cache(tmp_path):
+    """File home, the cancellation regime (the bound wider than the whole distance spread:
+    every pair a candidate): a batch whose candidates would need a buffer above
+    tier_cand_max is served by the exact list-cache path instead of growing the buffer
+    without bound; results stay bit-identical."""
+    from test_gpu_bounded import lists_pair
+    rng = np.random.default_rng(11)
+    dim = 64
+    c = (100.0 / np.sqrt(dim)) * np.ones(dim, np.float32)
+    X = (c + 0.01 * rng.standard_normal((12000, dim))).astype(np.float32)
+    Q = (c + 0.01 * rng.standard_normal((96, dim))).astype(np.float32)
+    lists = (rng.random(12000) >= 0.8).astype(np.int64)
+    ids = np.arange(12000, dtype=np.uint64)
+    C = np.stack([np.zeros_like(c), -c]).astype(np.float32)
+    g, o = lists_pair(X, ids, lists, C, 0)
+    path = str(tmp_path / "cancel.vdb")
+    g.save(path)
+    del g
+    h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, 2))
+    h.set_option("list_cache_bytes", 200 * block_bytes(dim))
+    h.open_lists(path)
+    h.set_option("tier_row_cache", 0)
+    h.set_option("screen_cand_cap", 1024)
+    h.set_option("tier_cand_max", 4096)
+    Dr, Ir = o.search(Q, 2, 10)
+    for batch in (96, 40):
+        h.set_batch(batch)
+        assert_same(*h.search(Q, nprobe=2, k=10), Dr, Ir)
+    st = h.cache_stats()
+    assert st["screen_fallbacks"] > 0 and st["subbatches"] > 0, st
+    # a cap the batch fits under: re-run with a larger buffer instead
+    h.set_option("tier_cand_max", 1 << 24)
+    f0 = st["screen_fallbacks"]
+    assert_same(*h.search(Q, nprobe=2, k=10), Dr, Ir)
+    st = h.cache_stats()
+    assert st["screen_fallbacks"] == f0 and st["screen_reruns"] > 0, st

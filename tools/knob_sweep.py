@@ -54,28 +54,33 @@ def main():
         B, steps = 64, 12
         q = torch.empty((steps * B, 768), dtype=torch.float32, device=dev)
         bench.fill_rows(vdb, args, q, 0, steps * B, 12346, st.cuda_stream)
-        od = torch.empty((B, 10), dtype=torch.float32, device=dev)
-        oi = torch.empty((B, 10), dtype=torch.int64, device=dev)
+        od = torch.empty((B, 1024), dtype=torch.float32, device=dev)
+        oi = torch.empty((B, 1024), dtype=torch.int64, device=dev)
         for s in sets:
             opts = [o.split("=") for o in s.split(",") if o]
+            kk = 10  # ("k=N" in a set: the search's k, not an engine option)
             for n, v in opts:
-                idx.set_option(n, int(v))
+                if n == "k":
+                    kk = int(v)
+                else:
+                    idx.set_option(n, int(v))
+            opts = [(n, v) for n, v in opts if n != "k"]
             for j in range(2):
-                idx.search_device(q[j * B:].data_ptr(), B, args.nprobe, 10, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
+                idx.search_device(q[j * B:].data_ptr(), B, args.nprobe, kk, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
             torch.cuda.synchronize()
             idx.profile_enable(True)
             idx.set_option("bounded_stats", 1)  # statistics only
             idx.profile_reset()
             t0 = time.perf_counter()
             for j in range(steps):
-                idx.search_device(q[j * B:].data_ptr(), B, args.nprobe, 10, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
+                idx.search_device(q[j * B:].data_ptr(), B, args.nprobe, kk, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
             torch.cuda.synchronize()
             wall = (time.perf_counter() - t0) / steps * 1e3
             p = idx.profile_read()
             idx.profile_enable(False)
             n = max(p["scan_launches"], 1)
             alg = p["scan_bytes"] / max(p["batches"], 1)
-            print(json.dumps({"workload": wl, "opts": s, "scan_ms": round(p["scan_ms"] / n, 3),
+            print(json.dumps({"workload": wl, "opts": s, "gpu_bytes": idx.gpu_bytes_allocated(), "scan_ms": round(p["scan_ms"] / n, 3),
                               "search_ms": round(p["total_ms"] / n, 3), "wall_ms": round(wall, 3),
                               "alg_GB": round(alg / 1e9, 2),
                               "pairs_M": round(p["pair_vectors"] / max(p["batches"], 1) / 1e6, 2),
