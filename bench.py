@@ -613,6 +613,8 @@ def main():
     ap.add_argument("--host-calls", type=int, default=400, help="host-API calls of --batch queries each")
     ap.add_argument("--host-coalesce", type=int, default=64, help="max queries per coalesced device batch")
     ap.add_argument("--asg-file", default="", help=argparse.SUPPRESS)  # (a child of --emulate-rank all)
+    ap.add_argument("--no-emulate-exchange", action="store_true",
+                    help="--emulate-rank all: leave out the emulated all-gather + W-record merge per batch")
     ap.add_argument("--ranks-in-process", action="store_true",
                     help="--emulate-rank all in this one process (round 3's form) instead of a process per rank")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
@@ -994,7 +996,10 @@ def run_emulated_ranks_procs(args):
         "shard_lists": lists, "shard_vectors": vecs,
         "predicted_8gpu_qps_from_max_rank_step": round(args.batch * 1e3 / max(r["ms_per_step"] for r in ranks), 1),
         "build": info, "process_per_rank": True,
-        "note": "partial (per-rank) results; exchange excluded; each rank's search timed alone, in its own process",
+        "exchange": ("excluded" if args.no_emulate_exchange else
+                     f"on every batch: an RCCL all-gather of {W} records' bytes (communicator of world 1: a "
+                     f"local copy, not the xGMI latency) and the on-device merge of {W} records"),
+        "note": "per-rank results; each rank's search timed alone, in its own process",
     }), flush=True)
     return 0
 
@@ -1027,6 +1032,11 @@ def emulated_rank(vdb, args, device, r):
     for o in args.opt:
         name, val = o.split("=", 1)
         idx.set_option(name, int(val))
+    if not args.no_emulate_exchange:
+        # every batch also carries what a W-GPU node adds per rank: the all-gather (an RCCL
+        # communicator of world 1 gathering W records' bytes) and the W-record rank merge
+        idx.set_option("exchange_emulate_world", W)
+        idx.attach_comm(vdb.comm_unique_id(), 0, 1)
     res = timed_region(vdb, idx, args, device, 0, 1, queries, out_d, out_i)
     row = dict(res["mine"], rank=r, qps=round(args.steps * args.batch / res["elapsed"], 1),
                p99_ms=round(res["p99"], 4), latency_mean_ms=round(res["lat_mean"], 4),

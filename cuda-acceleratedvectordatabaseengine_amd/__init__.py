@@ -141,6 +141,8 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int64]),
         "vdb_ivf_coalesce_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "vdb_ivf_cache_stats": (ctypes.c_int, [vp, ctypes.POINTER(CacheStats)]),
+        "vdb_ivf_collect_stamps": (ctypes.c_int, [vp, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                                  ctypes.POINTER(ctypes.c_uint64)]),
         "vdb_ivf_open_lists": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "vdb_ivf_profile_enable": (ctypes.c_int, [vp, i32]),
         "vdb_ivf_profile_reset": (ctypes.c_int, [vp]),
@@ -489,6 +491,16 @@ class IVFFlatIndex:
         st = CacheStats()
         _check(lib().vdb_ivf_cache_stats(self._h, ctypes.byref(st)))
         return st.as_dict()
+
+    def collect_stamps(self):
+        """(option collect_stamps) the collect kernel's item timeline: (records [n, 4] uint64,
+        wall clock Hz); resets the buffer."""
+        n, hz = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(lib().vdb_ivf_collect_stamps(self._h, None, 0, ctypes.byref(n), ctypes.byref(hz)))
+        out = np.zeros((n.value, 4), dtype=np.uint64)
+        if n.value:
+            _check(lib().vdb_ivf_collect_stamps(self._h, out.ctypes.data, n.value, ctypes.byref(n), ctypes.byref(hz)))
+        return out, hz.value
 
     def profile_enable(self, on: bool = True):
         _check(lib().vdb_ivf_profile_enable(self._h, int(on)))

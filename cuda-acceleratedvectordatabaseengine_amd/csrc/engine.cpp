@@ -678,6 +678,23 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->set_device();
             h->quiesce();
             h->screen_cand_cap = (uint32_t)value;
+        } else if (n == "exchange_emulate_world") {  // (diagnostics: see engine.hpp xchg_emulate)
+            require(value >= 0 && value <= 64, "exchange_emulate_world is 0 .. 64");
+            h->set_device();
+            h->quiesce();
+            h->xchg_emulate = (uint32_t)value;
+        } else if (n == "collect_stamps") {  // (diagnostics: records of the collect kernel's items)
+            require(value >= 0 && value <= (1ll << 24), "collect_stamps is 0 .. 2^24 records");
+            h->set_device();
+            h->quiesce();
+            h->stamps_cap = (uint32_t)value;
+            if (value) {
+                h->stamps_buf.ensure((size_t)value * 4 + 2);
+                HIPCHECK(hipMemset(h->stamps_buf.p, 0, 16));
+            } else {
+                h->stamps_buf.release();
+            }
+            h->stamp_batch = 0;
         } else if (n == "tier_cand_max") {
             require(value >= 1024 && value <= (1ll << 31), "tier_cand_max is 1024 .. 2^31");
             h->tier_cand_max = (uint32_t)value;
@@ -782,6 +799,29 @@ int vdb_ivf_cache_stats(vdb_ivf* h, vdb_ivf_cache_stats_t* out) {
             out->screen_rows_cached += m->screen_rows_cached;
             out->screen_fallbacks += m->screen_tier_fallbacks;
         }
+    });
+}
+
+int vdb_ivf_collect_stamps(vdb_ivf* h, uint64_t* out, uint64_t cap, uint64_t* n, uint64_t* clock_hz) {
+    return guarded([&] {
+        require(h && n && clock_hz, "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        no_group(h, "collect_stamps");
+        h->set_device();
+        *n = 0;
+        int hz = 0;
+        HIPCHECK(hipDeviceGetAttribute(&hz, hipDeviceAttributeWallClockRate, h->device));
+        *clock_hz = (uint64_t)hz * 1000;  // (the attribute is in kHz)
+        if (!h->stamps_cap) return;
+        h->quiesce();
+        HIPCHECK(hipStreamSynchronize(h->stream));
+        uint32_t cnt = 0;
+        HIPCHECK(hipMemcpy(&cnt, h->stamps_buf.p, 4, hipMemcpyDeviceToHost));
+        *n = std::min<uint64_t>(cnt, h->stamps_cap);
+        if (!out) return;  // (the count only)
+        if (cap) HIPCHECK(hipMemcpy(out, h->stamps_buf.p + 2, std::min(cap, *n) * 32, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemset(h->stamps_buf.p, 0, 16));
+        h->stamp_batch = 0;
     });
 }
 

@@ -366,6 +366,9 @@ struct vdb_ivf {
     // ... at most this many candidates per batch (option tier_cand_max; never below
     // screen_cand_cap): a batch that needs more is served by the exact list-cache path
     uint32_t tier_cand_max = 32u << 20;
+    // (option collect_stamps, diagnostics) timeline records of the collect kernel's items
+    DevBuf<unsigned long long> stamps_buf;
+    uint32_t stamps_cap = 0, stamp_batch = 0;
     uint64_t screen_tier_fallbacks = 0;
     bool force_exact = false;          // (that path's batches: never screened)
     // Run-time floor under the screen (lists in HBM; floor.hpp): every deferred batch reports
@@ -449,6 +452,7 @@ struct vdb_ivf {
         DevBuf<float> qpad{true}, cd{true}, cdelta{true}, part_d{true}, slot_d{true}, carry_d{true}, carry2_d{true};
         DevBuf<uint64_t> part_i{true}, slot_i{true}, carry_i{true}, carry2_i{true};
         uint32_t carry_sel = 0;  // fused merge: the carry buffer the call's next batch reads (ping-pong)
+        uint32_t xfill = 0;      // (exchange_emulate_world) records placed in the other ranks' places
         const float* q = nullptr;  // the batch's zero-padded queries: qpad, or the caller's rows when dim == dp
         DevBuf<uint32_t> probes{true}, nseg_qp{true}, pbqp{true}, sorted_pair{true}, pbs{true}, counters{true},
             l1base{true}, cand{true}, thr{true};
@@ -506,6 +510,12 @@ struct vdb_ivf {
     ncclComm_t comm = nullptr;
     bool comm_owned = false;
     uint32_t comm_rank = 0, comm_world = 1;
+    // (option exchange_emulate_world, diagnostics) a communicator of world 1 exchanges records
+    // the size of W ranks' (the batch's record plus W - 1 earlier records of the same slot) and
+    // merges W records: the per-batch cost of an 8-GPU node's exchange and rank merge on one
+    // rank's timeline (one GPU cannot hold 8 ranks: RCCL refuses two ranks on one device)
+    uint32_t xchg_emulate = 0;
+    uint32_t xchg_records() const { return comm_world > 1 ? comm_world : std::max<uint32_t>(1, xchg_emulate); }
     // Every collective of the communicator runs on this one stream, fenced by events
     // against the search stream that produced / consumes its buffers: with several
     // batches in flight on several streams, every rank then executes its collectives in
@@ -2210,6 +2220,11 @@ struct vdb_ivf {
                         sa.floor_seq = floor_seq;
                     }
                     sa.mstats = bounded_stats && !pass ? stats.p + 8 : nullptr;
+                    if (stamps_cap) {
+                        sa.stamps = stamps_buf.p;
+                        sa.stamps_cap = stamps_cap;
+                        sa.stamp_batch = stamp_batch++;
+                    }
                     if (ev) HIPCHECK(hipEventRecord(ev->collect_begin, s));
                     vdbk::launch_screen_collect(metric, grid, sa, s);
                     if (ev) {
@@ -2475,7 +2490,7 @@ struct vdb_ivf {
     // of the P largest lists x k x 12 bytes) stay within kPartialBytes: the exact path at
     // k = 1000 on the 10M x 768 index would otherwise hold 1.5 GB of partials per slot.
     // Results never depend on batch boundaries.
-    static constexpr uint64_t kPartialBytes = 256ull << 20;
+    static constexpr uint64_t kPartialBytes = 384ull << 20;
     uint32_t batch_cap(uint32_t P, uint32_t k) const {
         uint32_t b = std::max<uint32_t>(1, std::min<uint32_t>(batch, vdbk::kPlanMaxPairs / P));
         const uint64_t per_query = (P < nseg_prefix.size() ? nseg_prefix[P] : 0) * (uint64_t)k * 12;
@@ -2505,6 +2520,12 @@ struct vdb_ivf {
         ensure_workspace(w, B, P, k);
         if (xworld) {
             const uint64_t rb = vdb_rank_record_bytes(B, k);
+            // (emulated exchange: W records are sent; the others hold earlier batches' records)
+            if (comm_world == 1 && xchg_emulate > 1 && w.xrec.cap < rb * xworld) {
+                slot_buf(w, w.xrec, rb * xworld);
+                w.xfill = 0;
+                HIPCHECK(hipMemsetAsync(w.xrec.p, 0xFF, rb * xworld, s));  // (empty entries until filled)
+            }
             slot_buf(w, w.xrec, rb);
             slot_buf(w, w.xgat, rb * xworld);
         }
@@ -2565,9 +2586,9 @@ struct vdb_ivf {
         }
         const bool xchg = comm != nullptr;
         if (xchg)
-            require(comm_world == world && comm_rank == rank,
+            require((comm_world == world && comm_rank == rank) || (comm_world == 1 && xchg_emulate == world),
                     "the attached communicator's (rank, world) differs from the handle's shard", VDB_ERR_STATE);
-        SearchSlot& w = begin_call(n, P, k, s, xchg ? comm_world : 0);
+        SearchSlot& w = begin_call(n, P, k, s, xchg ? xchg_records() : 0);
         if (xchg && (tiered() || comm_world > 1)) {
             // The exchange is per CALL at world > 1: the whole call's partials in one record,
             // ONE all-gather, one merge. A rank's own state (its tier, switched on by its own
@@ -2620,13 +2641,21 @@ struct vdb_ivf {
     void exchange(SearchSlot& w, uint32_t B, uint32_t k, float* od, uint64_t* oi, hipStream_t s) {
         if (comm_failed()) throw VdbError(VDB_ERR_DEVICE, comm_error_msg());
         EventSet* ev = prof && events_used ? &events[events_used - 1] : nullptr;  // (the call's last batch)
+        const uint32_t nrec = xchg_records();
+        if (comm_world == 1 && nrec > 1 && w.xfill < nrec - 1) {
+            // (emulation: the slot's first W - 1 records fill the other ranks' places once)
+            const uint64_t rb = vdb_rank_record_bytes(B, k);
+            HIPCHECK(hipMemcpyAsync(w.xrec.p + rb * (1 + w.xfill), w.xrec.p, rb, hipMemcpyDeviceToDevice, s));
+            ++w.xfill;
+        }
         const hipStream_t cs = comm_enter(w, s);
-        nccl_settle(ncclAllGather(w.xrec.p, w.xgat.p, vdb_rank_record_bytes(B, k), ncclUint8, comm, cs),
+        nccl_settle(ncclAllGather(w.xrec.p, w.xgat.p, vdb_rank_record_bytes(B, k) * (comm_world == 1 ? nrec : 1), ncclUint8,
+                                  comm, cs),
                     "ncclAllGather");
         if (ev) HIPCHECK(hipEventRecord(ev->x_end, cs));
         watch_exchange(cs);
         comm_leave(w, s);
-        merge_gathered(w, comm_world, B, k, od, oi, s);
+        merge_gathered(w, nrec, B, k, od, oi, s);
         if (ev) {
             HIPCHECK(hipEventRecord(ev->m_end, s));
             ev->xchg = true;

@@ -461,7 +461,10 @@ int vdb_ivf_attach_comm(vdb_ivf* h, const void* id, uint32_t rank, uint32_t worl
         require(h && id && world > 0 && rank < world, "invalid argument");
         require(!h->is_group(), "a group handle owns its communicators", VDB_ERR_STATE);
         std::lock_guard<std::mutex> g(h->mu);
-        require(h->rank == rank && h->world == world,
+        // (exchange_emulate_world: a shard's handle times its exchange on a communicator of
+        // world 1, records of W ranks' size; diagnostics of one rank's timeline)
+        const bool emulated = world == 1 && h->xchg_emulate > 1 && h->world == h->xchg_emulate;
+        require((h->rank == rank && h->world == world) || emulated,
                 "attach_comm after set_shard / plan_shard with the same (rank, world)", VDB_ERR_STATE);
         h->set_device();
         h->quiesce();
@@ -533,6 +536,7 @@ int vdb_ivf_attach_comm(vdb_ivf* h, const void* id, uint32_t rank, uint32_t worl
                     twice |= any & b;
                     any |= b;
                 }
+                if (emulated) break;  // (one shard of W: it holds only its own lists)
                 uint64_t nonempty = 0;
                 for (uint32_t l = wd * 64; l < std::min(h->nlist, (wd + 1) * 64); ++l)
                     if (h->count[l]) nonempty |= 1ull << (l % 64);

@@ -155,6 +155,13 @@ struct ScanArgs {
     // lists' row-major fp32 copy ([slot][dp], one slack block) instead of the interleaved
     // layout: the arena released while the screen serves (one fp32 copy in HBM).
     uint32_t rows_layout = 0;
+    // (option collect_stamps, diagnostics) per collect item a record of 4 u64 {batch << 40 |
+    // item << 16 | workgroup, wall clock at its start, at its end, nq | segments << 8 | kind
+    // << 16 | list << 32} (kind 0 wide item, 1 narrow item, 2 workgroup start); stamps[0]
+    // counts records, stamps_cap bounds them
+    unsigned long long* stamps = nullptr;
+    uint32_t stamps_cap = 0;
+    uint32_t stamp_batch = 0;
 };
 size_t scan_wide_lds(uint32_t d4, uint32_t k, int waves);   // dynamic LDS of a wide-item block
 bool scan_wide_fits(uint32_t d4, uint32_t k, int waves);

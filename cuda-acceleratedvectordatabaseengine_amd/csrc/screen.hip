@@ -1104,6 +1104,18 @@ __device__ __forceinline__ void contribute_rl(const ScanArgs& a, const ScanItem 
     }
 }
 
+// (option collect_stamps) one timeline record of the collect kernel
+__device__ __forceinline__ void put_stamp(const ScanArgs& a, uint64_t w0, uint64_t t0, uint64_t w3) {
+    const uint32_t i = atomicAdd((unsigned int*)a.stamps, 1u);
+    if (i < a.stamps_cap) {
+        unsigned long long* r = a.stamps + 2 + (size_t)i * 4;
+        r[0] = ((uint64_t)a.stamp_batch << 40) | w0;
+        r[1] = t0;
+        r[2] = wall_clock64();
+        r[3] = w3;
+    }
+}
+
 // ivf_screen_collect: the persistent grid of ivf_scan_screen over the same queues (wide
 // items: a list's segments x <= a.wide_q (16 or 32) queries, the 4 waves taking the
 // segments dynamically; narrow items: one wave = one segment x <= 4 queries), collecting
@@ -1133,19 +1145,24 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
             it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
             if (lane < (int)it.npairs) s_thr_w[wv][lane] = a.thr[it.pair_start + lane];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            const uint64_t t0 = a.stamps ? wall_clock64() : 0;
             reset_rl(rl, 4);
             collect_segment<M, KD, 1, I8, W2>(a, it, 0, (int)it.npairs, it.seg, rl, s_thr_w[wv], it.seg & 3u);
             contribute_rl(a, it, 0, (int)it.npairs, rl);
+            if (a.stamps && lane == 0)
+                put_stamp(a, ((uint64_t)idx << 16) | blockIdx.x, t0, it.npairs | (1u << 8) | (1u << 16) | ((uint64_t)it.list << 32));
         }
     };
 
     const uint32_t n_wide = a.counters[3];
+    if (a.stamps && threadIdx.x == 0) put_stamp(a, blockIdx.x, wall_clock64(), 2u << 16);
     if (a.fused && blockIdx.x + a.fused >= gridDim.x) drain_narrow();
     for (;;) {
         if (threadIdx.x == 0) s_next = atomicAdd(&a.work[1], 1u);
         __syncthreads();
         const uint32_t b = s_next;
         if (b >= n_wide) break;
+        const uint64_t t_item = a.stamps ? wall_clock64() : 0;
         ScanItem it = a.items_w[b];
         it.list = __builtin_amdgcn_readfirstlane(it.list);
         it.seg = __builtin_amdgcn_readfirstlane(it.seg);
@@ -1171,6 +1188,8 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
         }
         if (any) contribute_rl(a, it, 0, nq, rl);
         __syncthreads();  // (s_thr and s_seg are reset by the next item only after every wave is done)
+        if (a.stamps && threadIdx.x == 0)
+            put_stamp(a, ((uint64_t)b << 16) | blockIdx.x, t_item, (uint32_t)nq | ((seg1 - seg0) << 8) | ((uint64_t)it.list << 32));
     }
     if (a.fused) drain_narrow();
 }
@@ -1373,6 +1392,76 @@ __global__ __launch_bounds__(64) void ivf_screen_exact(ScanArgs a, const uint2* 
     }
 }
 
+// The same exact distances, 64 survivors per wave (one lane each: the reference's
+// sequential sum needs one lane per (query, row) pair), for rows in HBM (SRC 0: the
+// row-major copy by slot; SRC 1: the tier's fetched rows [survivor][dp]). The rows stream
+// through the wave's LDS tile a 64-dim chunk at a time with coalesced loads (instruction j
+// loads rows 4 j .. 4 j + 3, 256 B each) while the previous chunk is summed, so every lane is
+// busy and a wave keeps 16 KB of rows in flight; each lane's query chunk (a few distinct
+// queries per wave: the survivors are grouped per pair) comes through the cache. The
+// 16-row kernel above keeps 48 of its 64 lanes idle in the sums and waits on a global
+// query load per 8 dims (1.2-1.5 TB/s of survivor rows).
+#ifndef VDB_EXACT64
+#define VDB_EXACT64 1
+#endif
+constexpr bool kExact64 = VDB_EXACT64 != 0;  // (A/B builds: 0 = the 16-row kernel for HBM rows too)
+constexpr int kExact64Pad = 17;  // float4 per LDS tile row (16 + 1: the lanes' rows on distinct banks)
+template <int M, int SRC>
+__global__ __launch_bounds__(256) void ivf_screen_exact64(ScanArgs a, const uint2* __restrict__ surv,
+                                                          const float* __restrict__ fetched,
+                                                          float* __restrict__ sdist) {
+    __shared__ float4 tile[4][64 * kExact64Pad];
+    const int lane = lane_id();
+    const uint32_t wv = wave_index();
+    float4* T = tile[wv];
+    const uint32_t total = a.counters[kCtrSurv];
+    const uint32_t d4 = a.d4, nchunk = d4 / 16;  // (d4 is a multiple of 16 for the screen)
+    const float4* src = SRC == 1 ? (const float4*)fetched : (const float4*)a.rows;
+    const int rsub = lane >> 4, col = lane & 15;
+    for (uint32_t g0 = (blockIdx.x * 4 + wv) * 64; g0 < total; g0 += gridDim.x * 256) {
+        const uint32_t n = min(64u, total - g0);
+        const uint32_t mi = g0 + min((uint32_t)lane, n - 1);
+        const uint2 my = surv[mi];
+        const uint64_t myrow = SRC == 1 ? (uint64_t)mi : (uint64_t)my.x;
+        const float4* qr = (const float4*)(a.qpad + (size_t)(a.sorted_pair[my.y] >> 16) * a.dp);
+        // this lane's share of the coalesced loads: float4 `col` of rows 4 j + rsub
+        const float4* rp[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t r = __shfl(myrow, 4 * j + rsub);
+            rp[j] = src + r * d4 + col;
+        }
+        float4 v[16], qv[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = rp[j][0];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) qv[t] = qr[t];
+        float acc = 0.0f;
+        for (uint32_t c = 0; c < nchunk; ++c) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) T[(4 * j + rsub) * kExact64Pad + col] = v[j];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            float4 qc[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) qc[t] = qv[t];
+            if (c + 1 < nchunk) {  // the next chunk in flight while this one is summed
+#pragma unroll
+                for (int j = 0; j < 16; ++j) v[j] = rp[j][(c + 1) * 16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) qv[t] = qr[(c + 1) * 16 + t];
+            }
+#pragma unroll
+            for (int t = 0; t < 16; ++t) acc = acc4<M>(acc, qc[t], T[lane * kExact64Pad + t]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();  // (every lane has read the tile before it is rewritten)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (lane < (int)n) sdist[g0 + lane] = dist_finish<M>(acc);
+    }
+}
+
 // One wave per valid sorted (query, list) pair: the exact top-k of its survivors' distances,
 // written as the pair's only partial. A pair that overflowed the candidate buffer keeps its
 // planned segments instead: one wave per (pair, segment) recomputes the segment lane =
@@ -1571,14 +1660,21 @@ void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uin
         return true;
     }();
     (void)raised;
-    const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>(16384, (max_surv + kExactRows - 1) / kExactRows));
+    // (a grid-stride loop: 2048 workgroups of one wave cover 32K survivors per pass; a grid
+    // sized to the buffer's capacity launched 16384, nearly all of which found nothing to do)
+    const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>(2048, (max_surv + kExactRows - 1) / kExactRows));
     const size_t lds = exact_lds(a.d4);
     // (a wave per pair, and at least 2048 waves for the (pair, segment) tasks of overflowed pairs)
     const uint32_t gp = std::max<uint32_t>(512, std::min<uint32_t>(2048, (BP + 3) / 4));
     const int src = fetched ? 1 : (a.rows ? 0 : 2);
+    // (rows in HBM: 64 survivors per wave, 4 waves per workgroup; the host arena over PCIe:
+    // 16 rows per workgroup)
+    const uint32_t g64 = std::max<uint32_t>(1, std::min<uint32_t>(1024, (max_surv + 255) / 256));
     auto exact = [&](auto m_c) {
         constexpr int Mm = decltype(m_c)::value;
-        if (src == 0) ivf_screen_exact<Mm, 0><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
+        if (src == 0 && kExact64) ivf_screen_exact64<Mm, 0><<<g64, 256, 0, s>>>(a, surv, fetched, sdist);
+        else if (src == 1 && kExact64) ivf_screen_exact64<Mm, 1><<<g64, 256, 0, s>>>(a, surv, fetched, sdist);
+        else if (src == 0) ivf_screen_exact<Mm, 0><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
         else if (src == 1) ivf_screen_exact<Mm, 1><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
         else ivf_screen_exact<Mm, 2><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
         ivf_screen_pair_topk<Mm><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, sdist, ovf, smax);

@@ -272,6 +272,12 @@ typedef struct vdb_ivf_cache_stats_t {
                                      by the exact list-cache path instead */
 } vdb_ivf_cache_stats_t;
 int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
+/* Diagnostics (option "collect_stamps" = N records): the screened collect kernel's timeline,
+ * 4 x u64 per record {batch << 40 | item << 16 | workgroup, start, end (wall clock ticks),
+ * queries | segments << 8 | kind << 16 (0 wide item, 1 narrow item, 2 workgroup start) |
+ * list << 32}; copies min(cap, *n) records, *clock_hz = the wall clock's rate, and resets the
+ * buffer. Synchronises the handle. */
+int vdb_ivf_collect_stamps(vdb_ivf* index, uint64_t* out, uint64_t cap, uint64_t* n, uint64_t* clock_hz);
 /* The tier's home on disk (ListPrefetcher::register_list_file / prefetch_lists,
  * engine/prefetcher.h:139-183; list files of format/storage.h): serve this handle's lists
  * from an index file written by vdb_ivf_save, without reading them into memory.

@@ -26,7 +26,8 @@ import bench  # noqa: E402
 
 DEFAULTS = {"seg_vectors": 0, "segs_per_item": 0, "wide_stride": 1, "fused_scan": 1, "narrow_blocks": 64,
             "wide_group": 16, "fused_merge": 1, "scan_window": 0, "screen": 1, "bounded_stats": 0, "screen_group": 0,
-            "screen_defer": 1, "screen_cand_cap": 4 << 20, "screen_floor_ppm": 50000, "screen_thr_every": 0, "screen_i8": 0}
+            "screen_defer": 1, "screen_cand_cap": 4 << 20, "screen_floor_ppm": 50000, "screen_thr_every": 0, "screen_i8": 0,
+            "collect_stamps": 0}
 
 
 def main():
@@ -51,20 +52,23 @@ def main():
             if wl == "s8":
                 idx.set_shard(0, 8)
         st = torch.cuda.current_stream()
-        B, steps = 64, 12
-        q = torch.empty((steps * B, 768), dtype=torch.float32, device=dev)
-        bench.fill_rows(vdb, args, q, 0, steps * B, 12346, st.cuda_stream)
+        B, steps, nqb = 64, 12, 128  # (nqb distinct query batches for the in-flight timing)
+        q = torch.empty((nqb * B, 768), dtype=torch.float32, device=dev)
+        bench.fill_rows(vdb, args, q, 0, nqb * B, 12346, st.cuda_stream)
         od = torch.empty((B, 1024), dtype=torch.float32, device=dev)
         oi = torch.empty((B, 1024), dtype=torch.int64, device=dev)
         for s in sets:
             opts = [o.split("=") for o in s.split(",") if o]
-            kk = 10  # ("k=N" in a set: the search's k, not an engine option)
+            kk, infl = 10, 1  # ("k=N", "inflight=N" in a set: the search's k, batches in flight; not engine options)
             for n, v in opts:
                 if n == "k":
                     kk = int(v)
+                elif n == "inflight":
+                    infl = int(v)
                 else:
                     idx.set_option(n, int(v))
-            opts = [(n, v) for n, v in opts if n != "k"]
+            opts = [(n, v) for n, v in opts if n not in ("k", "inflight")]
+            stamps = any(n == "collect_stamps" for n, _ in opts)
             for j in range(2):
                 idx.search_device(q[j * B:].data_ptr(), B, args.nprobe, kk, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
             torch.cuda.synchronize()
@@ -78,6 +82,9 @@ def main():
             wall = (time.perf_counter() - t0) / steps * 1e3
             p = idx.profile_read()
             idx.profile_enable(False)
+            if stamps:
+                rec, hz = idx.collect_stamps()
+                print(json.dumps(dict(stamp_summary(rec, hz), workload=wl, opts=s)), flush=True)
             n = max(p["scan_launches"], 1)
             alg = p["scan_bytes"] / max(p["batches"], 1)
             print(json.dumps({"workload": wl, "opts": s, "gpu_bytes": idx.gpu_bytes_allocated(), "scan_ms": round(p["scan_ms"] / n, 3),
@@ -90,8 +97,61 @@ def main():
                               "collect_ms": round(p.get("collect_ms", 0) / n, 3),
                               "recheck_ms": round(p.get("recheck_ms", 0) / n, 3)}),
                   flush=True)
+            if infl > 1:  # the step at `infl` batches in flight (round-robin streams, as bench.py)
+                idx.set_option("bounded_stats", 0)
+                streams = [st] + [torch.cuda.Stream(dev) for _ in range(infl - 1)]
+                nb = 100
+                for j in range(nb + 6):
+                    if j == 6:
+                        torch.cuda.synchronize()
+                        t0 = time.perf_counter()
+                    s_ = streams[j % infl]
+                    idx.search_device(q[(j % nqb) * B:].data_ptr(), B, args.nprobe, kk, od.data_ptr(), oi.data_ptr(),
+                                      s_.cuda_stream)
+                torch.cuda.synchronize()
+                print(json.dumps({"workload": wl, "opts": s, "inflight": infl,
+                                  "step_ms": round((time.perf_counter() - t0) / nb * 1e3, 4)}), flush=True)
             for n_, _ in opts:  # back to defaults
                 idx.set_option(n_, DEFAULTS[n_])
+
+
+def stamp_summary(rec, hz):
+    """The collect kernel's timeline (option collect_stamps) per batch: the workgroups' start
+    ramp, the span, the wide items' share of the workgroup-time, the tail after the last
+    item started, and the slowest items."""
+    import numpy as np
+    if not len(rec):
+        return {"stamps": 0}
+    us = 1e6 / hz
+    batch = (rec[:, 0] >> np.uint64(40)).astype(np.int64)
+    kind = ((rec[:, 3] >> np.uint64(16)) & np.uint64(0xFF)).astype(np.int64)
+    nq = (rec[:, 3] & np.uint64(0xFF)).astype(np.int64)
+    segs = ((rec[:, 3] >> np.uint64(8)) & np.uint64(0xFF)).astype(np.int64)
+    t0 = rec[:, 1].astype(np.float64)
+    t1 = rec[:, 2].astype(np.float64)
+    out = []
+    for b in np.unique(batch)[1:]:  # (the first batch warms up)
+        m = batch == b
+        st, wi, na = m & (kind == 2), m & (kind == 0), m & (kind == 1)
+        if not st.any() or not wi.any():
+            continue
+        first, last_start = t0[st].min(), t0[st].max()
+        end = max(t1[wi].max(), t1[na].max() if na.any() else 0)
+        span = end - first
+        dur = t1[wi] - t0[wi]
+        nwg = int(st.sum())
+        top = np.argsort(-dur)[:3]
+        out.append({"span_us": span * us, "wg_start_ramp_us": (last_start - first) * us,
+                    "last_wide_item_start_us": (t0[wi].max() - first) * us,
+                    "tail_after_last_start_us": (end - t0[wi].max()) * us,
+                    "wide_items": int(wi.sum()), "narrow_items": int(na.sum()), "workgroups": nwg,
+                    "wide_busy_frac": float(dur.sum() / (nwg * span)),
+                    "item_us_mean": float(dur.mean() * us), "item_us_max": float(dur.max() * us),
+                    "slowest": [[int(nq[wi][i]), int(segs[wi][i]), round(float(dur[i] * us), 1)] for i in top],
+                    "narrow_us_sum": float((t1[na] - t0[na]).sum() * us) if na.any() else 0.0})
+    keys = [k for k in out[0] if k != "slowest"] if out else []
+    return {"stamp_batches": len(out), **{k: round(float(np.mean([o[k] for o in out])), 2) for k in keys},
+            "slowest_items_of_first_batch[nq,segs,us]": out[0]["slowest"] if out else None}
 
 
 def cancel(vdb, dev, sets):
