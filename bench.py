@@ -1153,8 +1153,9 @@ def run(vdb, args, device, rank, world):
     deferred = screened and prof.get("collect_ms", 0) > 0
     dp = -(-args.dim // 64) * 64
     collect_ms = prof.get("collect_ms", 0.0) / launches
-    # the deferred screen's shadow: bf16 (default), or int8 + a 4 B scale per vector (option screen_i8=1)
-    shadow_i8 = deferred and "screen_i8=1" in args.opt
+    # the deferred screen's shadow: bf16, or int8 + a 4 B scale per vector (option screen_i8: the
+    # engine chooses by default, profile field screen_shadow says which it built)
+    shadow_i8 = deferred and prof.get("screen_shadow", 1) == 2
     shadow_b = dp + 4 if shadow_i8 else 2 * dp
     if deferred:
         # the dominant kernel is the deferred screen's collect pass: it streams the shadow and

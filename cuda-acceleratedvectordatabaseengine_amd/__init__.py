@@ -72,7 +72,8 @@ class Profile(ctypes.Structure):
                 ("exchanges", ctypes.c_uint64), ("exchange_ms", ctypes.c_double), ("rank_merge_ms", ctypes.c_double),
                 ("screen_collected", ctypes.c_uint64), ("collect_ms", ctypes.c_double),
                 ("recheck_ms", ctypes.c_double), ("screen_floor_batches", ctypes.c_uint64),
-                ("screen_floor_trips", ctypes.c_uint64)]
+                ("screen_floor_trips", ctypes.c_uint64), ("screen_shadow", ctypes.c_uint32),
+                ("reserved0", ctypes.c_uint32)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

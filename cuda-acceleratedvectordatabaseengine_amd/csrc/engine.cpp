@@ -671,7 +671,8 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
         } else if (n == "screen_i8") {
             h->set_device();
             h->quiesce();
-            h->screen_i8 = value != 0;
+            h->screen_i8 = (int)value;
+            h->i8_vetoed = false;
             h->screen_update();
         } else if (n == "screen_cand_cap") {
             require(value >= 1024 && value <= (1ll << 30), "screen_cand_cap is 1024 .. 2^30");
@@ -935,6 +936,7 @@ int vdb_ivf_profile_read(vdb_ivf* h, vdb_ivf_profile* out) {
         p.screen_collected = st[8];
         p.screen_floor_batches = h->floor.batches;
         p.screen_floor_trips = h->floor.trips;
+        p.screen_shadow = h->screen_ready ? (h->screen_fmt_i8 ? 2u : 1u) : 0u;
         p.computed_vectors = st[7];
         *out = p;
         hh->set_device();

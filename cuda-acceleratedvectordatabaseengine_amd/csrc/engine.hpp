@@ -321,8 +321,22 @@ struct vdb_ivf {
     // bytes): cfg3 collect 2.12 vs 2.49 ms but 6.3x the re-checks (0.58 vs 0.17 ms), scan 2.72
     // vs 2.67 ms; cfg4 shard 4.29 vs 4.09 ms; 1/8 shard 0.523 vs 0.560 ms. The inline kernel
     // (screen_defer 0) always uses bf16.
-    bool screen_i8 = false;
-    bool want_i8() const { return screen_i8 && screen_defer; }
+    // 2 (default) = automatic: int8 for lists in HBM searched with 16-query items (the build's
+    // triggering search has nprobe < 64), kept unless the calibration batch at the build vetoes
+    // it (screen_calibrate: survivors beyond k per pair above 1.5 % of the pairs, a regime
+    // where its wider bound re-checks more than its half-size stream saves); bf16 for
+    // 32-query items (VALU-bound there: cfg4 rank 0 of 8, 4.39 vs 4.10 ms per batch) and in
+    // the tier (each survivor is a row read from the home). Bench lines with the hybrid exact
+    // kernel: headline 27,321 vs 25,304 QPS, 1/8 shard at 3 in flight 173.3K vs 151.3K,
+    // mixture 44.4K vs 52.2K (calibration sends it to bf16).
+    int screen_i8 = 2;
+    bool i8_vetoed = false;  // (automatic: the calibration vetoed int8 for this handle)
+    uint32_t last_P = 0;     // the nprobe of the search that triggers a screen build
+    bool want_i8() const {
+        if (!screen_defer) return false;
+        if (screen_i8 != 2) return screen_i8 == 1;
+        return !tiered() && !i8_vetoed && last_P < 64;
+    }
     uint32_t screen_thr_every = 0;  // deferred collect: blocks between re-reads of the shared thresholds, 0 = automatic (option screen_thr_every)
     // Deferred re-checks (option screen_defer, default 1): the scan only collects candidates
     // against upper-bound thresholds; survivors of each pair's final threshold are re-checked
@@ -941,35 +955,90 @@ struct vdb_ivf {
         for (uint32_t l = 0; l < nlist; ++l)
             if (owned[l])
                 for (uint64_t b = 0; b < list_blocks(l); ++b) blist[block_off[l] + b] = l;
-        const bool i8 = want_i8();
-        if (i8 != screen_fmt_i8) {  // (a shadow of the other format: its buffers are sized for that)
-            screen_sh.release();
-            screen_scale.release();
+        for (bool i8 = want_i8();; i8 = false) {
+            if (i8 != screen_fmt_i8) {  // (a shadow of the other format: its buffers are sized for that)
+                screen_sh.release();
+                screen_scale.release();
+            }
+            screen_fmt_i8 = i8;
+            try {
+                screen_sh.ensure(vdbk::screen_shadow_u4(arena_blocks, d4, i8));
+                // (+ one slack block: the exact scans' tile pipeline reads one block past a segment)
+                screen_rows.ensure((size_t)(arena_blocks + 1) * 64 * dp);
+                screen_meta.ensure((size_t)arena_blocks * 64);
+                screen_blist.ensure(arena_blocks);
+                if (i8) screen_scale.ensure((size_t)arena_blocks * 64);
+            } catch (const VdbError&) {  // no room for it: the exact scan serves
+                (void)hipGetLastError();
+                screen_release();
+                return;
+            }
+            HIPCHECK(hipMemcpyAsync(screen_blist.p, blist.data(), arena_blocks * 4, hipMemcpyHostToDevice, stream));
+            HIPCHECK(hipMemsetAsync(screen_rows.p + (size_t)arena_blocks * 64 * dp, 0, (size_t)64 * dp * 4, stream));
+            vdbk::launch_screen_build(arena.p, arena_blocks, d4, screen_blist.p, cent_rm.p, screen_sh.p, screen_rows.p,
+                                      screen_meta.p, stream, i8 ? screen_scale.p : nullptr);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipStreamSynchronize(stream));
+            screen_ready = true;
+            floor.reset_state();  // (trips of a previous shadow say nothing about this one)
+            if (!i8 || screen_i8 != 2 || screen_calibrate()) break;
+            i8_vetoed = true;  // (the automatic format: int8 re-checks too much here, bf16 instead)
         }
-        screen_fmt_i8 = i8;
-        try {
-            screen_sh.ensure(vdbk::screen_shadow_u4(arena_blocks, d4, i8));
-            // (+ one slack block: the exact scans' tile pipeline reads one block past a segment)
-            screen_rows.ensure((size_t)(arena_blocks + 1) * 64 * dp);
-            screen_meta.ensure((size_t)arena_blocks * 64);
-            screen_blist.ensure(arena_blocks);
-            if (i8) screen_scale.ensure((size_t)arena_blocks * 64);
-        } catch (const VdbError&) {  // no room for it: the exact scan serves
-            (void)hipGetLastError();
-            screen_release();
-            return;
-        }
-        HIPCHECK(hipMemcpyAsync(screen_blist.p, blist.data(), arena_blocks * 4, hipMemcpyHostToDevice, stream));
-        HIPCHECK(hipMemsetAsync(screen_rows.p + (size_t)arena_blocks * 64 * dp, 0, (size_t)64 * dp * 4, stream));
-        vdbk::launch_screen_build(arena.p, arena_blocks, d4, screen_blist.p, cent_rm.p, screen_sh.p, screen_rows.p,
-                                  screen_meta.p, stream, i8 ? screen_scale.p : nullptr);
-        HIPCHECK(hipGetLastError());
-        HIPCHECK(hipStreamSynchronize(stream));
-        screen_ready = true;
         // the row-major copy is now the lists' fp32 copy: release the arena
         arena.release();
         arena_dropped = true;
     }
+
+    // The automatic shadow format's calibration (option screen_i8 = 2), at the build: one
+    // screened batch of 64 of the index's own vectors (one from each of 64 blocks spread over
+    // the lists) as queries, at the nprobe of the search that triggered the build and k = 10.
+    // int8 stays unless its survivors beyond k per valid (query, list) pair exceed
+    // kCalibPpm of the (query, vector) pairs, or the candidates overflowed: a regime where
+    // its ~5x wider bound re-checks more rows than its half-size stream saves (the two-level
+    // mixture: 6.2 % and 44.4K vs 52.2K QPS; iid data: 0.3 %, 27.3K vs 25.3K).
+    static constexpr uint64_t kCalibPpm = 15000;
+    bool screen_calibrate() {
+        const uint32_t P = std::min<uint32_t>(nlist, last_P ? last_P : 32), k = 10, B = 64;
+        if (!arena_blocks || vdbk::topk_regs(k) != 1) return true;
+        DevBuf<float> q, od;
+        DevBuf<uint64_t> oi;
+        q.ensure((size_t)B * dim);
+        od.ensure((size_t)B * k);
+        oi.ensure((size_t)B * k);
+        for (uint32_t j = 0; j < B; ++j) {  // (slot 0 of a block always holds a vector)
+            const uint64_t slot = (uint64_t)(j * arena_blocks / B) * 64;
+            HIPCHECK(hipMemcpyAsync(q.p + (size_t)j * dim, screen_rows.p + slot * dp, (size_t)dim * 4,
+                                    hipMemcpyDeviceToDevice, stream));
+        }
+        SearchSlot w;
+        ensure_workspace(w, B, P, k);
+        if (!stats.p) {
+            stats.ensure(16);
+            HIPCHECK(hipMemsetAsync(stats.p, 0, 128, stream));
+        }
+        HIPCHECK(hipMemsetAsync(w.carry_i.p, 0xFF, (size_t)P * k * 8, stream));
+        const bool prof0 = prof;
+        prof = false;
+        calibrating = true;  // (no floor report: the calibration batch never trips the floor)
+        try {
+            run_batch(w, q.p, B, P, k, od.p, oi.p, stream, nullptr, 0);
+        } catch (...) {
+            prof = prof0;
+            calibrating = false;
+            throw;
+        }
+        prof = prof0;
+        calibrating = false;
+        uint32_t hc[vdbk::kCounters];
+        HIPCHECK(hipMemcpyAsync(hc, w.counters.p, sizeof(hc), hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        const uint64_t surv = hc[vdbk::kCtrSurv], pairs = hc[vdbk::kCtrPairs], kvalid = (uint64_t)k * hc[vdbk::kCtrValid];
+        const bool overflow = hc[vdbk::kCtrCand] > screen_cand_cap;
+        calib_excess_ppm = pairs ? (surv > kvalid ? surv - kvalid : 0) * 1000000ull / pairs : 0;
+        return !overflow && calib_excess_ppm <= kCalibPpm;
+    }
+    uint64_t calib_excess_ppm = 0;
+    bool calibrating = false;
 
     // The tier's screen: shadow + norms + ids of every stored list in HBM (the deferred scan
     // only: its re-checks read the survivors' rows from the home). Host home: built from the
@@ -2095,12 +2164,13 @@ struct vdb_ivf {
         if (tiered() && tier_ev_used) HIPCHECK(hipStreamWaitEvent(s, tier_ev, 0));
         const uint64_t max_l1 = max_items / vdbk::kMergeFan + BP;
         const uint64_t max_wide = max_items / 4 + BP + 1;
+        last_P = P;
         if (screen_stale) screen_update();
         // the screened scan (default, L2 / IP, k <= 64): items of swq queries
         const uint32_t swq = screen_width(k, P);
         bool screened = swq != 0 && !force_exact;
         uint32_t floor_seq = 0;
-        if (screened && !tiered() && screen_defer)  // the run-time floor (lists in HBM only)
+        if (screened && !tiered() && screen_defer && !calibrating)  // the run-time floor (lists in HBM only)
             screened = floor.plan([this](uint32_t i) { return floor_entry(i); }, &floor_seq);
         // Exact scans on lists in HBM whose interleaved arena was released read the row-major
         // copy (4-wave items); the opt-in bounded scan needs the interleaved layout back.
@@ -2481,6 +2551,7 @@ struct vdb_ivf {
     // The screen serves a search with this k and nprobe (the tier: the deferred scan with its
     // shadow resident; built lazily, so a stale screen is rebuilt first).
     bool screen_serves(uint32_t k, uint32_t P) {
+        last_P = P;
         if (screen_stale) screen_update();
         return screen_width(k, P) != 0;
     }

@@ -1340,6 +1340,11 @@ __device__ __forceinline__ float exact_dist(const float4* __restrict__ src, uint
 // tier's host home, read over PCIe);
 // then one lane per row runs the reference's sequential sum over its LDS row (row stride
 // d4 + 1 float4: the lanes' rows fall on distinct banks) against its pair's query.
+#ifndef VDB_EXACT_LANE
+#define VDB_EXACT_LANE 1
+#endif
+constexpr bool kExactLane = VDB_EXACT_LANE != 0;  // (A/B builds: 0 = the LDS-staged kernel for HBM rows too)
+constexpr uint32_t kExactLaneMin = 16384;
 constexpr int kExactRows = 16;
 constexpr int kExactChunks = 3;  // 64-float4 chunks of a row loaded per pass (768 dims)
 __host__ __device__ constexpr size_t exact_lds(uint32_t d4) { return ((size_t)kExactRows * (d4 + 1) + 64) * 16; }
@@ -1351,6 +1356,7 @@ __global__ __launch_bounds__(64) void ivf_screen_exact(ScanArgs a, const uint2* 
     extern __shared__ __attribute__((aligned(16))) float4 rlds[];
     const int lane = lane_id();
     const uint32_t total = a.counters[kCtrSurv];
+    if (SRC != 2 && kExactLane && total >= kExactLaneMin) return;  // (ivf_screen_exact_lane's)
     const uint32_t d4 = a.d4, rs = d4 + 1;
     const float4* src = SRC == 1 ? (const float4*)fetched : SRC == 0 ? (const float4*)a.rows : a.arena;
     for (uint32_t base = blockIdx.x * kExactRows; base < total; base += gridDim.x * kExactRows) {
@@ -1392,73 +1398,48 @@ __global__ __launch_bounds__(64) void ivf_screen_exact(ScanArgs a, const uint2* 
     }
 }
 
-// The same exact distances, 64 survivors per wave (one lane each: the reference's
-// sequential sum needs one lane per (query, row) pair), for rows in HBM (SRC 0: the
-// row-major copy by slot; SRC 1: the tier's fetched rows [survivor][dp]). The rows stream
-// through the wave's LDS tile a 64-dim chunk at a time with coalesced loads (instruction j
-// loads rows 4 j .. 4 j + 3, 256 B each) while the previous chunk is summed, so every lane is
-// busy and a wave keeps 16 KB of rows in flight; each lane's query chunk (a few distinct
-// queries per wave: the survivors are grouped per pair) comes through the cache. The
-// 16-row kernel above keeps 48 of its 64 lanes idle in the sums and waits on a global
-// query load per 8 dims (1.2-1.5 TB/s of survivor rows).
-#ifndef VDB_EXACT64
-#define VDB_EXACT64 1
-#endif
-constexpr bool kExact64 = VDB_EXACT64 != 0;  // (A/B builds: 0 = the 16-row kernel for HBM rows too)
-constexpr int kExact64Pad = 17;  // float4 per LDS tile row (16 + 1: the lanes' rows on distinct banks)
+// The same exact distances for rows in HBM (SRC 0: the row-major copy by slot; SRC 1: the
+// tier's fetched rows [survivor][dp]) when a batch has many survivors (at least
+// kExactLaneMin: the LDS-staged kernel, one round trip per 16 rows, is faster for a few
+// thousand), 64 survivors per wave, one lane each (the reference's
+// sequential sum needs one lane per (query, row) pair): every lane streams its own row and
+// its query (a few distinct queries per wave: the survivors are grouped per pair, so those
+// loads are mostly one address) kLaneRowPipe float4 ahead of its sum, without LDS. All 64
+// lanes sum (the LDS-staged kernel above keeps 48 idle and holds 50 KB of LDS per 16 rows).
+constexpr int kLaneRowPipe = 16;                  // (d4 is a multiple of 16 for the screen)
 template <int M, int SRC>
-__global__ __launch_bounds__(256) void ivf_screen_exact64(ScanArgs a, const uint2* __restrict__ surv,
-                                                          const float* __restrict__ fetched,
-                                                          float* __restrict__ sdist) {
-    __shared__ float4 tile[4][64 * kExact64Pad];
+__global__ __launch_bounds__(256) void ivf_screen_exact_lane(ScanArgs a, const uint2* __restrict__ surv,
+                                                             const float* __restrict__ fetched,
+                                                             float* __restrict__ sdist) {
     const int lane = lane_id();
-    const uint32_t wv = wave_index();
-    float4* T = tile[wv];
     const uint32_t total = a.counters[kCtrSurv];
-    const uint32_t d4 = a.d4, nchunk = d4 / 16;  // (d4 is a multiple of 16 for the screen)
+    if (total < kExactLaneMin) return;  // (ivf_screen_exact's)
+    const uint32_t d4 = a.d4;
     const float4* src = SRC == 1 ? (const float4*)fetched : (const float4*)a.rows;
-    const int rsub = lane >> 4, col = lane & 15;
-    for (uint32_t g0 = (blockIdx.x * 4 + wv) * 64; g0 < total; g0 += gridDim.x * 256) {
-        const uint32_t n = min(64u, total - g0);
-        const uint32_t mi = g0 + min((uint32_t)lane, n - 1);
-        const uint2 my = surv[mi];
-        const uint64_t myrow = SRC == 1 ? (uint64_t)mi : (uint64_t)my.x;
+    for (uint32_t i0 = (blockIdx.x * 4 + wave_index()) * 64; i0 < total; i0 += gridDim.x * 256) {
+        const uint32_t i = min(i0 + (uint32_t)lane, total - 1);
+        const uint2 my = surv[i];
+        const float4* xr = src + (SRC == 1 ? (uint64_t)i : (uint64_t)my.x) * d4;
         const float4* qr = (const float4*)(a.qpad + (size_t)(a.sorted_pair[my.y] >> 16) * a.dp);
-        // this lane's share of the coalesced loads: float4 `col` of rows 4 j + rsub
-        const float4* rp[16];
+        float4 xb[kLaneRowPipe], qb[kLaneRowPipe];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint64_t r = __shfl(myrow, 4 * j + rsub);
-            rp[j] = src + r * d4 + col;
+        for (int p = 0; p < kLaneRowPipe; ++p) {
+            xb[p] = xr[p];
+            qb[p] = qr[p];
         }
-        float4 v[16], qv[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = rp[j][0];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) qv[t] = qr[t];
         float acc = 0.0f;
-        for (uint32_t c = 0; c < nchunk; ++c) {
+        for (uint32_t t0 = 0; t0 < d4; t0 += kLaneRowPipe) {
+            const bool more = t0 + kLaneRowPipe < d4;  // (wave-uniform)
 #pragma unroll
-            for (int j = 0; j < 16; ++j) T[(4 * j + rsub) * kExact64Pad + col] = v[j];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            float4 qc[16];
-#pragma unroll
-            for (int t = 0; t < 16; ++t) qc[t] = qv[t];
-            if (c + 1 < nchunk) {  // the next chunk in flight while this one is summed
-#pragma unroll
-                for (int j = 0; j < 16; ++j) v[j] = rp[j][(c + 1) * 16];
-#pragma unroll
-                for (int t = 0; t < 16; ++t) qv[t] = qr[(c + 1) * 16 + t];
+            for (int p = 0; p < kLaneRowPipe; ++p) {
+                acc = acc4<M>(acc, qb[p], xb[p]);
+                if (more) {
+                    xb[p] = xr[t0 + kLaneRowPipe + p];
+                    qb[p] = qr[t0 + kLaneRowPipe + p];
+                }
             }
-#pragma unroll
-            for (int t = 0; t < 16; ++t) acc = acc4<M>(acc, qc[t], T[lane * kExact64Pad + t]);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();  // (every lane has read the tile before it is rewritten)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        if (lane < (int)n) sdist[g0 + lane] = dist_finish<M>(acc);
+        if (i0 + (uint32_t)lane < total) sdist[i0 + lane] = dist_finish<M>(acc);
     }
 }
 
@@ -1669,12 +1650,16 @@ void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uin
     const int src = fetched ? 1 : (a.rows ? 0 : 2);
     // (rows in HBM: 64 survivors per wave, 4 waves per workgroup; the host arena over PCIe:
     // 16 rows per workgroup)
-    const uint32_t g64 = std::max<uint32_t>(1, std::min<uint32_t>(1024, (max_surv + 255) / 256));
+    const uint32_t gl = std::max<uint32_t>(1, std::min<uint32_t>(2048, (max_surv + 255) / 256));
     auto exact = [&](auto m_c) {
         constexpr int Mm = decltype(m_c)::value;
-        if (src == 0 && kExact64) ivf_screen_exact64<Mm, 0><<<g64, 256, 0, s>>>(a, surv, fetched, sdist);
-        else if (src == 1 && kExact64) ivf_screen_exact64<Mm, 1><<<g64, 256, 0, s>>>(a, surv, fetched, sdist);
-        else if (src == 0) ivf_screen_exact<Mm, 0><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
+        // (both kernels for rows in HBM: each serves the batch whose survivor count is its
+        // regime and returns at once otherwise; the count is known only on the device)
+        if (src == 0 && kExactLane && max_surv >= kExactLaneMin)
+            ivf_screen_exact_lane<Mm, 0><<<gl, 256, 0, s>>>(a, surv, fetched, sdist);
+        else if (src == 1 && kExactLane && max_surv >= kExactLaneMin)
+            ivf_screen_exact_lane<Mm, 1><<<gl, 256, 0, s>>>(a, surv, fetched, sdist);
+        if (src == 0) ivf_screen_exact<Mm, 0><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
         else if (src == 1) ivf_screen_exact<Mm, 1><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
         else ivf_screen_exact<Mm, 2><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
         ivf_screen_pair_topk<Mm><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, sdist, ovf, smax);

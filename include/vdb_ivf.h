@@ -102,6 +102,8 @@ typedef struct vdb_ivf_profile {
     double recheck_ms;         /* ... and of the final thresholds, selection and exact re-checks after it */
     uint64_t screen_floor_batches; /* batches the run-time floor ran on the exact scan */
     uint64_t screen_floor_trips;   /* screened batches that tripped the floor */
+    uint32_t screen_shadow;        /* the screen's shadow now: 0 none, 1 bf16, 2 int8 (option screen_i8) */
+    uint32_t reserved0;
 } vdb_ivf_profile;
 
 const char* vdb_last_error(void);
