@@ -464,6 +464,28 @@ def tier_leg(vdb, idx, args, device, queries):
                                  (v1.get("screen_rows_cached", 0) - v0.get("screen_rows_cached", 0)) / batches, 1),
                              "survivor_rows_read_per_batch": round((v1["screen_rows_fetched"] - v0["screen_rows_fetched"]) / batches, 1),
                              "file_read_gbps": round((v1["file_bytes_read"] - v0["file_bytes_read"]) / ev / 1e9, 2)})
+        if args.tier_census > 0 and s1["screen_resident"]:
+            # the row cache refilled by probes per vector from a census of query-like rows (the
+            # queries' generator, another seed), then the same timed calls again
+            cq = torch.empty((args.tier_census, args.dim), dtype=torch.float32, device=device)
+            fill_rows(vdb, args, cq, 1 << 41, args.tier_census, 999, st.cuda_stream)
+            torch.cuda.synchronize()
+            counts = h.probe_census(cq.data_ptr(), args.tier_census, args.nprobe)
+            del cq
+            h.fill_row_cache(counts)
+            v0 = h.cache_stats()
+            t0 = time.perf_counter()
+            for j in range(1, calls):
+                h.search_device(queries[j * call:].data_ptr(), call, args.nprobe, args.k, od.data_ptr(), oi.data_ptr(),
+                                st.cuda_stream)
+            torch.cuda.synchronize()
+            ev = time.perf_counter() - t0
+            v1 = h.cache_stats()
+            variants.append({"opts": f"row cache by census ({args.tier_census} rows)", "value": round(nq / ev, 1),
+                             "survivor_rows_from_hbm_cache_per_batch": round(
+                                 (v1.get("screen_rows_cached", 0) - v0.get("screen_rows_cached", 0)) / batches, 1),
+                             "survivor_rows_read_per_batch": round((v1["screen_rows_fetched"] - v0["screen_rows_fetched"]) / batches, 1),
+                             "file_read_gbps": round((v1["file_bytes_read"] - v0["file_bytes_read"]) / ev / 1e9, 2)})
         if variants:
             screen["variants"] = variants
         return {"value": round(nq / el, 1), "unit": "queries/s", "calls": calls - 1, "queries_per_call": call, **screen,
@@ -606,6 +628,8 @@ def main():
     ap.add_argument("--tier-calls", type=int, default=8)
     ap.add_argument("--tier-variant", action="append", default=[], metavar="NAME=V[,NAME=V]",
                     help="tier leg: time the same calls again with these engine options (repeatable)")
+    ap.add_argument("--tier-census", type=int, default=0,
+                    help="tier leg: also time the row cache filled by a probe census of this many query-like rows")
     ap.add_argument("--tier-dir", default="", help="directory for the tier leg's index file (default: TMPDIR)")
     ap.add_argument("--host-api", action="store_true",
                     help="also time the host API (vdb_ivf_search) from --host-threads caller threads")

@@ -142,6 +142,7 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_set_option": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int64]),
         "vdb_ivf_coalesce_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "vdb_ivf_cache_stats": (ctypes.c_int, [vp, ctypes.POINTER(CacheStats)]),
+        "vdb_ivf_fill_row_cache": (ctypes.c_int, [vp, vp]),
         "vdb_ivf_collect_stamps": (ctypes.c_int, [vp, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                                   ctypes.POINTER(ctypes.c_uint64)]),
         "vdb_ivf_open_lists": (ctypes.c_int, [vp, ctypes.c_char_p]),
@@ -492,6 +493,17 @@ class IVFFlatIndex:
         st = CacheStats()
         _check(lib().vdb_ivf_cache_stats(self._h, ctypes.byref(st)))
         return st.as_dict()
+
+    def fill_row_cache(self, probe_counts=None):
+        """Screened tier, file home: refill the row cache by probes per vector (probe_counts
+        from probe_census) or by list size (None)."""
+        if probe_counts is None:
+            _check(lib().vdb_ivf_fill_row_cache(self._h, None))
+        else:
+            c = np.ascontiguousarray(probe_counts, dtype=np.uint64)
+            if c.shape != (self.config.nlist,):
+                raise ValueError("probe_counts needs one entry per list")
+            _check(lib().vdb_ivf_fill_row_cache(self._h, _ptr(c)))
 
     def collect_stamps(self):
         """(option collect_stamps) the collect kernel's item timeline: (records [n, 4] uint64,

@@ -826,6 +826,24 @@ int vdb_ivf_collect_stamps(vdb_ivf* h, uint64_t* out, uint64_t cap, uint64_t* n,
     });
 }
 
+int vdb_ivf_fill_row_cache(vdb_ivf* h, const uint64_t* probe_counts) {
+    return guarded([&] {
+        require(h, "null handle");
+        std::lock_guard<std::mutex> g(h->mu);
+        no_group(h, "fill_row_cache");
+        h->set_device();
+        h->quiesce();
+        if (h->tier_call_used) HIPCHECK(hipEventSynchronize(h->tier_call_ev));
+        if (probe_counts) h->row_cache_weight.assign(probe_counts, probe_counts + h->nlist);
+        else h->row_cache_weight.clear();
+        if (!(h->tiered() && h->file_home() && h->tier_row_cache)) return;
+        if (h->screen_stale) h->screen_update();  // (its build fills the cache itself)
+        if (!h->screen_ready) return;
+        h->cache_reset();  // (refilled in the new order)
+        h->fill_row_cache();
+    });
+}
+
 int vdb_ivf_open_lists(vdb_ivf* h, const char* path) {
     return guarded([&] {
         require(h && path, "null argument");

@@ -1120,15 +1120,25 @@ struct vdb_ivf {
     }
 
     // Screened tier, file home: the k <= 64 searches never use the list cache, so it is filled
-    // with the largest stored lists (on iid data they are also the most probed); a survivor of
-    // a list found there is copied from HBM instead of read from the file. The lists stay
+    // with lists whose survivors' rows are then copied from HBM instead of read from the
+    // file: by default the largest stored lists (on iid data also the most probed); with a
+    // probe census (vdb_ivf_fill_row_cache: per list how many of a query-like sample probe
+    // it) the lists that save the most row reads per cached byte, i.e. by probes per vector
+    // (a (query, list) pair's survivors are ~k whatever the list's length). The lists stay
     // ordinary cached lists: a k > 64 search may evict them.
+    std::vector<double> row_cache_weight;  // (empty: by size)
     void fill_row_cache() {
         if (!cache_blocks) return;
         std::vector<uint32_t> order;
         for (uint32_t l = 0; l < nlist; ++l)
             if (owned[l] && count[l] && cache_off[l] == kAbsent) order.push_back(l);
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return count[x] > count[y]; });
+        if (row_cache_weight.size() == nlist)
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+                const double wx = row_cache_weight[x] / (double)count[x], wy = row_cache_weight[y] / (double)count[y];
+                return wx != wy ? wx > wy : count[x] > count[y];
+            });
+        else
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return count[x] > count[y]; });
         std::vector<std::pair<uint32_t, uint64_t>> loads;
         for (uint32_t l : order) {
             const uint64_t off = cache_alloc(list_blocks(l));
@@ -2266,7 +2276,12 @@ struct vdb_ivf {
             }
             sa.fused = std::max<uint32_t>(1, std::min<uint32_t>(narrow_blocks, vdbk::kPersistentBlocks / 2));
             const uint64_t want = std::max<uint64_t>(max_wide, (max_items + 3) / 4);
-            const uint32_t grid = (uint32_t)(scan_blocks ? std::min<uint64_t>(want, scan_blocks) : want);
+            // (the persistent collect grid of 16-query items: 320 workgroups, 1.25 per CU, not 2:
+            // the CU slots left over run the other batches in flight; measured on one box,
+            // 320 / 352 / 384 / 512: headline 28.5K / 28.2K / 28.1K / 27.4K QPS, mixture 53.6K /
+            // 53.9K / 54.0K / 52.0K, 1/8 shard at 3 in flight 184.5K / 182.7K / 181.8K / 174.4K)
+            const uint64_t cap = scan_blocks ? scan_blocks : (swq == 32 ? vdbk::kPersistentBlocks / 2 : kCollectBlocks);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>(want, cap);
             if (defer) {
                 const float* fetched = nullptr;
                 for (int pass = 0;; ++pass) {
@@ -2550,6 +2565,7 @@ struct vdb_ivf {
     }
     // The screen serves a search with this k and nprobe (the tier: the deferred scan with its
     // shadow resident; built lazily, so a stale screen is rebuilt first).
+    static constexpr uint32_t kCollectBlocks = 320;
     bool screen_serves(uint32_t k, uint32_t P) {
         last_P = P;
         if (screen_stale) screen_update();

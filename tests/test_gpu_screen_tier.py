@@ -249,3 +249,33 @@ def test_screened_tier_cancellation_falls_back_to_the_list_cache(tmp_path):
     assert_same(*h.search(Q, nprobe=2, k=10), Dr, Ir)
     st = h.cache_stats()
     assert st["screen_fallbacks"] == f0 and st["screen_reruns"] > 0, st
+
+
+def test_screened_tier_row_cache_by_census(tmp_path):
+    """The row cache refilled by probes per vector from a probe census of query-like rows
+    (vdb_ivf_fill_row_cache), and back to the size order: results unchanged, survivor rows
+    served from the cache."""
+    import torch
+    dim = 64
+    X, Q, ids, o = data(dim, seed=17)
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    g.centroids = o.centroids
+    g.add(X, ids)
+    path = str(tmp_path / "census.vdb")
+    g.save(path)
+    del g
+    h = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, NLIST))
+    h.set_option("list_cache_bytes", (need_blocks(o, Q, NPROBE) + 8) * block_bytes(dim))
+    h.open_lists(path)
+    Dr, Ir = o.search(Q, NPROBE, 10)
+    assert_same(*h.search(Q, nprobe=NPROBE, k=10), Dr, Ir)
+    qd = torch.from_numpy(np.ascontiguousarray(Q)).to("cuda:0")
+    counts = h.probe_census(qd.data_ptr(), len(Q), NPROBE)
+    torch.cuda.synchronize()
+    assert counts.sum() == len(Q) * NPROBE
+    for c in (counts, None):
+        h.fill_row_cache(c)
+        s0 = h.cache_stats()
+        assert_same(*h.search(Q, nprobe=NPROBE, k=10), Dr, Ir)
+        s1 = h.cache_stats()
+        assert s1["screen_rows_cached"] > s0["screen_rows_cached"], (s0, s1)

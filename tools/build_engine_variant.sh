@@ -1,0 +1,18 @@
+#!/bin/bash
+# A/B library build: the engine (engine.cpp, group.cpp) compiled with extra -D flags, linked
+# with the in-tree kernel objects into _variants/<name>/libvdb_ivf.so (select it with VDB_IVF_LIB).
+#   usage: bash tools/build_engine_variant.sh <name> [-DMACRO=value ...]
+set -e
+N=$1; shift
+R=$(cd "$(dirname "$0")/.." && pwd)
+P=$R/cuda-acceleratedvectordatabaseengine_amd
+[ -n "$NOMAKE" ] || make -s -C "$P" >/dev/null
+O=$R/_variants/$N
+mkdir -p "$O"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wall -I$R/include"
+/opt/rocm/bin/hipcc $F "$@" -DVDB_BUILD_ID='"variant"' -c "$P/csrc/engine.cpp" -o "$O/engine.o"
+/opt/rocm/bin/hipcc $F "$@" -c "$P/csrc/group.cpp" -o "$O/group.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libvdb_ivf.so" "$P/build/kernels.o" "$P/build/screen.o" \
+    "$O/engine.o" "$O/group.o" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+rm -f "$O/engine.o" "$O/group.o"
+echo "$O/libvdb_ivf.so"

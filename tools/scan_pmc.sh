@@ -14,7 +14,7 @@ i=0
 for P in "$A" "$B"; do
     i=$((i+1))
     echo "[$(date +%T)] $NAME pass $i"
-    timeout -k 10 500 rocprofv3 --pmc $P --kernel-include-regex ivf_scan_ -d "$O/${NAME}_p$i" -o p -f csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --prof-steps 2 "$@" > "$O/${NAME}_p$i.log" 2>&1 || { tail -20 "$O/${NAME}_p$i.log"; exit 1; }
+    timeout -k 10 500 rocprofv3 --pmc $P --kernel-include-regex ${KRE:-ivf_scan_} -d "$O/${NAME}_p$i" -o p -f csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu --prof-steps 2 "$@" > "$O/${NAME}_p$i.log" 2>&1 || { tail -20 "$O/${NAME}_p$i.log"; exit 1; }
 done
 python3 - "$O" "$NAME" <<'PY'
 import csv, glob, os, sys, collections
