@@ -464,15 +464,20 @@ def tier_leg(vdb, idx, args, device, queries):
                                  (v1.get("screen_rows_cached", 0) - v0.get("screen_rows_cached", 0)) / batches, 1),
                              "survivor_rows_read_per_batch": round((v1["screen_rows_fetched"] - v0["screen_rows_fetched"]) / batches, 1),
                              "file_read_gbps": round((v1["file_bytes_read"] - v0["file_bytes_read"]) / ev / 1e9, 2)})
-        if args.tier_census > 0 and s1["screen_resident"]:
-            # the row cache refilled by probes per vector from a census of query-like rows (the
-            # queries' generator, another seed), then the same timed calls again
-            cq = torch.empty((args.tier_census, args.dim), dtype=torch.float32, device=device)
-            fill_rows(vdb, args, cq, 1 << 41, args.tier_census, 999, st.cuda_stream)
+        if args.tier_adapt > 0 and s1["screen_resident"]:
+            # the row cache refilled by the survivor rows that other queries (the queries'
+            # generator, another seed: tier_adapt of them, served in calls) needed per list
+            # (vdb_ivf_survivor_histogram: the rows per cached byte it would have saved), then
+            # the same timed calls again
+            aq = torch.empty((args.tier_adapt, args.dim), dtype=torch.float32, device=device)
+            fill_rows(vdb, args, aq, 1 << 41, args.tier_adapt, 999, st.cuda_stream)
+            h0 = h.survivor_histogram()
+            for j in range(0, args.tier_adapt, call):
+                n_ = min(call, args.tier_adapt - j)
+                h.search_device(aq[j:].data_ptr(), n_, args.nprobe, args.k, od.data_ptr(), oi.data_ptr(), st.cuda_stream)
             torch.cuda.synchronize()
-            counts = h.probe_census(cq.data_ptr(), args.tier_census, args.nprobe)
-            del cq
-            h.fill_row_cache(counts)
+            del aq
+            h.fill_row_cache(h.survivor_histogram() - h0)
             v0 = h.cache_stats()
             t0 = time.perf_counter()
             for j in range(1, calls):
@@ -481,7 +486,7 @@ def tier_leg(vdb, idx, args, device, queries):
             torch.cuda.synchronize()
             ev = time.perf_counter() - t0
             v1 = h.cache_stats()
-            variants.append({"opts": f"row cache by census ({args.tier_census} rows)", "value": round(nq / ev, 1),
+            variants.append({"opts": f"row cache by the survivor histogram of {args.tier_adapt} other queries", "value": round(nq / ev, 1),
                              "survivor_rows_from_hbm_cache_per_batch": round(
                                  (v1.get("screen_rows_cached", 0) - v0.get("screen_rows_cached", 0)) / batches, 1),
                              "survivor_rows_read_per_batch": round((v1["screen_rows_fetched"] - v0["screen_rows_fetched"]) / batches, 1),
@@ -628,8 +633,8 @@ def main():
     ap.add_argument("--tier-calls", type=int, default=8)
     ap.add_argument("--tier-variant", action="append", default=[], metavar="NAME=V[,NAME=V]",
                     help="tier leg: time the same calls again with these engine options (repeatable)")
-    ap.add_argument("--tier-census", type=int, default=0,
-                    help="tier leg: also time the row cache filled by a probe census of this many query-like rows")
+    ap.add_argument("--tier-adapt", type=int, default=0, metavar="Q",
+                    help="tier leg: also time the row cache refilled by the survivor histogram of Q other queries")
     ap.add_argument("--tier-dir", default="", help="directory for the tier leg's index file (default: TMPDIR)")
     ap.add_argument("--host-api", action="store_true",
                     help="also time the host API (vdb_ivf_search) from --host-threads caller threads")
@@ -637,6 +642,8 @@ def main():
     ap.add_argument("--host-calls", type=int, default=400, help="host-API calls of --batch queries each")
     ap.add_argument("--host-coalesce", type=int, default=64, help="max queries per coalesced device batch")
     ap.add_argument("--asg-file", default="", help=argparse.SUPPRESS)  # (a child of --emulate-rank all)
+    ap.add_argument("--emulate-exchange", action="store_true",
+                    help="--emulate-shard W: every batch also exchanges W records (world-1 all-gather) and merges them")
     ap.add_argument("--no-emulate-exchange", action="store_true",
                     help="--emulate-rank all: leave out the emulated all-gather + W-record merge per batch")
     ap.add_argument("--ranks-in-process", action="store_true",
@@ -1162,6 +1169,11 @@ def run(vdb, args, device, rank, world):
         idx.set_shard(rank, world, owners=shard_owners(vdb, args, idx.list_sizes(), world))
     if world > 1 and args.exchange == "engine":
         attach_engine_comm(vdb, idx, args, rank, world)
+    if world == 1 and args.emulate_shard > 1 and args.emulate_exchange:
+        # (this rank's timeline with the per-batch exchange of a W-GPU node: an all-gather of W
+        # records' bytes on a communicator of world 1 and the W-record merge)
+        idx.set_option("exchange_emulate_world", args.emulate_shard)
+        idx.attach_comm(vdb.comm_unique_id(), 0, 1)
     res = timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, check)
     elapsed, p99, p99_single, prof = res["elapsed"], res["p99"], res["p99_single"], res["prof"]
     parity_multi = res["parity_multi"]

@@ -143,6 +143,7 @@ def lib() -> ctypes.CDLL:
         "vdb_ivf_coalesce_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "vdb_ivf_cache_stats": (ctypes.c_int, [vp, ctypes.POINTER(CacheStats)]),
         "vdb_ivf_fill_row_cache": (ctypes.c_int, [vp, vp]),
+        "vdb_ivf_survivor_histogram": (ctypes.c_int, [vp, vp]),
         "vdb_ivf_collect_stamps": (ctypes.c_int, [vp, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                                   ctypes.POINTER(ctypes.c_uint64)]),
         "vdb_ivf_open_lists": (ctypes.c_int, [vp, ctypes.c_char_p]),
@@ -494,16 +495,22 @@ class IVFFlatIndex:
         _check(lib().vdb_ivf_cache_stats(self._h, ctypes.byref(st)))
         return st.as_dict()
 
-    def fill_row_cache(self, probe_counts=None):
-        """Screened tier, file home: refill the row cache by probes per vector (probe_counts
-        from probe_census) or by list size (None)."""
-        if probe_counts is None:
+    def fill_row_cache(self, weights=None):
+        """Screened tier, file home: refill the row cache by expected survivor rows per vector
+        (weights per list, e.g. survivor_histogram()) or by list size (None)."""
+        if weights is None:
             _check(lib().vdb_ivf_fill_row_cache(self._h, None))
         else:
-            c = np.ascontiguousarray(probe_counts, dtype=np.uint64)
+            c = np.ascontiguousarray(weights, dtype=np.uint64)
             if c.shape != (self.config.nlist,):
-                raise ValueError("probe_counts needs one entry per list")
+                raise ValueError("weights needs one entry per list")
             _check(lib().vdb_ivf_fill_row_cache(self._h, _ptr(c)))
+
+    def survivor_histogram(self) -> np.ndarray:
+        """Per list: the survivor rows the screened tier's batches needed so far."""
+        out = np.zeros(self.config.nlist, dtype=np.uint64)
+        _check(lib().vdb_ivf_survivor_histogram(self._h, _ptr(out)))
+        return out
 
     def collect_stamps(self):
         """(option collect_stamps) the collect kernel's item timeline: (records [n, 4] uint64,

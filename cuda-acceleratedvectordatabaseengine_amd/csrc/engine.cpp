@@ -826,7 +826,16 @@ int vdb_ivf_collect_stamps(vdb_ivf* h, uint64_t* out, uint64_t cap, uint64_t* n,
     });
 }
 
-int vdb_ivf_fill_row_cache(vdb_ivf* h, const uint64_t* probe_counts) {
+int vdb_ivf_survivor_histogram(vdb_ivf* h, uint64_t* out) {
+    return guarded([&] {
+        require(h && out, "null argument");
+        std::lock_guard<std::mutex> g(h->mu);
+        no_group(h, "survivor_histogram");
+        for (uint32_t l = 0; l < h->nlist; ++l) out[l] = l < h->surv_hist.size() ? h->surv_hist[l] : 0;
+    });
+}
+
+int vdb_ivf_fill_row_cache(vdb_ivf* h, const uint64_t* weights) {
     return guarded([&] {
         require(h, "null handle");
         std::lock_guard<std::mutex> g(h->mu);
@@ -834,7 +843,7 @@ int vdb_ivf_fill_row_cache(vdb_ivf* h, const uint64_t* probe_counts) {
         h->set_device();
         h->quiesce();
         if (h->tier_call_used) HIPCHECK(hipEventSynchronize(h->tier_call_ev));
-        if (probe_counts) h->row_cache_weight.assign(probe_counts, probe_counts + h->nlist);
+        if (weights) h->row_cache_weight.assign(weights, weights + h->nlist);
         else h->row_cache_weight.clear();
         if (!(h->tiered() && h->file_home() && h->tier_row_cache)) return;
         if (h->screen_stale) h->screen_update();  // (its build fills the cache itself)

@@ -1121,12 +1121,13 @@ struct vdb_ivf {
 
     // Screened tier, file home: the k <= 64 searches never use the list cache, so it is filled
     // with lists whose survivors' rows are then copied from HBM instead of read from the
-    // file: by default the largest stored lists (on iid data also the most probed); with a
-    // probe census (vdb_ivf_fill_row_cache: per list how many of a query-like sample probe
-    // it) the lists that save the most row reads per cached byte, i.e. by probes per vector
-    // (a (query, list) pair's survivors are ~k whatever the list's length). The lists stay
-    // ordinary cached lists: a k > 64 search may evict them.
+    // file: by default the largest stored lists (on iid data also the most probed); with
+    // weights (vdb_ivf_fill_row_cache: per list its expected survivor rows, e.g. the
+    // histogram of the batches served so far, vdb_ivf_survivor_histogram) the lists that save
+    // the most row reads per cached byte, by weight / length. The lists stay ordinary cached
+    // lists: a k > 64 search may evict them.
     std::vector<double> row_cache_weight;  // (empty: by size)
+    std::vector<uint64_t> surv_hist;       // per list: survivor rows of the tier's screened batches
     void fill_row_cache() {
         if (!cache_blocks) return;
         std::vector<uint32_t> order;
@@ -1200,9 +1201,11 @@ struct vdb_ivf {
         cache_src_host.clear();
         std::vector<uint32_t> order;
         order.reserve(n);
+        if (surv_hist.size() != nlist) surv_hist.assign(nlist, 0);
         for (uint32_t i = 0; i < n; ++i) {
             const uint64_t slot = fetch_surv[i].x;
             const uint32_t l = sblist_host[slot >> 6];
+            ++surv_hist[l];
             if (tier_row_cache && !cache_off.empty() && cache_off[l] != kAbsent)
                 cache_src_host.push_back({(unsigned long long)i,
                                           (unsigned long long)(cache_off[l] * 64 + (slot - sblock_off[l] * 64))});

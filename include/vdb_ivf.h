@@ -276,10 +276,12 @@ typedef struct vdb_ivf_cache_stats_t {
 int vdb_ivf_cache_stats(vdb_ivf* index, vdb_ivf_cache_stats_t* out);
 /* The screened tier's row cache (file home, option tier_row_cache): refill the HBM list
  * cache with the lists that save the most survivor-row reads per cached byte, by
- * probe_counts[l] / count[l] (per list how many of a query-like sample probe it, e.g. from
- * vdb_ivf_probe_census), or by list size when probe_counts is null (the default). The order
- * is kept for later fills (a rebuilt screen). */
-int vdb_ivf_fill_row_cache(vdb_ivf* index, const uint64_t* probe_counts);
+ * weights[l] / count[l] (weights: per list its expected survivor rows, e.g. the histogram of
+ * the batches served so far from vdb_ivf_survivor_histogram), or by list size when weights is
+ * null (the default). The order is kept for later fills (a rebuilt screen). */
+int vdb_ivf_fill_row_cache(vdb_ivf* index, const uint64_t* weights);
+/* Per list (nlist entries): the survivor rows the screened tier's batches needed so far. */
+int vdb_ivf_survivor_histogram(vdb_ivf* index, uint64_t* out);
 /* Diagnostics (option "collect_stamps" = N records): the screened collect kernel's timeline,
  * 4 x u64 per record {batch << 40 | item << 16 | workgroup, start, end (wall clock ticks),
  * queries | segments << 8 | kind << 16 (0 wide item, 1 narrow item, 2 workgroup start) |

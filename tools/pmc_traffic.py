@@ -40,6 +40,7 @@ def summarise(d, batches, key):
         sys.exit(f"no counter_collection.csv under {d}")
     per_kernel = defaultdict(float)
     dispatches = defaultdict(set)
+    per_dispatch = defaultdict(float)  # (collect kernel, dispatch) -> KiB
     for f in files:
         for row in csv.DictReader(open(f)):
             if row.get("Counter_Name") != "FETCH_SIZE":
@@ -47,18 +48,26 @@ def summarise(d, batches, key):
             name = row["Kernel_Name"].split("(")[0].replace("void ", "")
             per_kernel[name] += float(row["Counter_Value"])
             dispatches[name].add(row.get("Dispatch_Id", ""))
+            if "ivf_screen_collect" in name:
+                per_dispatch[(name, row.get("Dispatch_Id", ""))] += float(row["Counter_Value"])
     scan = {k: v for k, v in per_kernel.items() if "ivf_scan" in k or "ivf_screen_collect" in k}
     kib = sum(scan.values())
-    # the deferred screen: one collect dispatch per batch, whatever else the command ran
+    # the deferred screen: one collect dispatch per batch, whatever else the command ran; the
+    # median dispatch (a screen build's calibration batch of the index's own vectors, and any
+    # other odd one, stays out of it)
     ncol = sum(len(v) for k, v in dispatches.items() if "ivf_screen_collect" in k)
     if ncol:
         batches = ncol
+        vals = sorted(per_dispatch.values())
+        kib_launch = vals[len(vals) // 2]
+    else:
+        kib_launch = kib / batches
     return {
         "workload": key,
         "build_id": build_id(),
-        "hbm_bytes_per_scan_launch": int(kib * 1024.0 * 2.0 / batches),
-        "source": "rocprofv3 --pmc FETCH_SIZE (KiB, x2 gfx950 correction) summed over the ivf_scan_* "
-                  f"and ivf_screen_collect dispatches of {batches} batches",
+        "hbm_bytes_per_scan_launch": int(kib_launch * 1024.0 * 2.0),
+        "source": "rocprofv3 --pmc FETCH_SIZE (KiB, x2 gfx950 correction) of the ivf_screen_collect dispatches "
+                  f"(median of {batches}), else summed over the ivf_scan_* dispatches of {batches} batches",
         "per_kernel_bytes_per_batch": {k: int(v * 2048 / batches) for k, v in scan.items()},
         "dispatches": {k: len(v) for k, v in dispatches.items() if "ivf_scan" in k or "ivf_screen_collect" in k},
     }

@@ -30,7 +30,7 @@ run() {  # run <name> <seconds> <cmd...>
     echo "[$(date +%T)] $name rc=$rc"
     if [ $rc -ne 0 ]; then tail -30 "$O/$name.log"; exit $rc; fi
 }
-SHORT="--steps 5 --warmup 1 --no-cpu --prof-steps 2"
+SHORT="--steps 5 --warmup 1 --no-cpu --prof-steps 2 --latency-batches 0"
 # the bench lines read this call's PMC traffic, or the committed file when no traffic step ran
 TJ="$O/traffic.json"
 [[ ",$STEPS," == *",traffic"* ]] || TJ="$R/profiles/traffic.json"
@@ -46,7 +46,7 @@ if has traffic8; then
     python3 tools/pmc_traffic.py "$O/traffic.json" "$O/pmc_emu8" 8 "10000000x768/4096/32/64/10/N1/shard0of8" | tail -3
 fi
 if has traffic4; then
-    run pmc_cfg4 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ivf_scan_|ivf_screen_collect" -d "$O/pmc_cfg4" -o f -f csv -- python3 bench.py $CFG4 --steps 5 --warmup 1 --prof-steps 2
+    run pmc_cfg4 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ivf_scan_|ivf_screen_collect" -d "$O/pmc_cfg4" -o f -f csv -- python3 bench.py $CFG4 --steps 5 --warmup 1 --prof-steps 2 --latency-batches 0
     python3 tools/pmc_traffic.py "$O/traffic.json" "$O/pmc_cfg4" 8 "100000000x768/16384/64/64/10/N1/shard0of8" | tail -3
 fi
 if has mfma; then
@@ -65,11 +65,11 @@ if has bench; then
 fi
 if has trace; then
     for inf in 1 2; do
-        run trace_inflight$inf 300 rocprofv3 --kernel-trace --stats -d "$O/trace_inflight$inf" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight $inf
+        run trace_inflight$inf 300 rocprofv3 --kernel-trace --stats -d "$O/trace_inflight$inf" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight $inf --latency-batches 0
         find "$O/trace_inflight$inf" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_inflight$inf.csv" \;
         head -6 "$O/kernel_stats_inflight$inf.csv"
     done
-    run trace_mix 300 rocprofv3 --kernel-trace --stats -d "$O/trace_mix" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight 1 --data mixture
+    run trace_mix 300 rocprofv3 --kernel-trace --stats -d "$O/trace_mix" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight 1 --data mixture --latency-batches 0
     find "$O/trace_mix" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_mixture.csv" \;
     head -6 "$O/kernel_stats_mixture.csv"
 fi
@@ -83,7 +83,7 @@ if has emu8; then
     grep '^{' "$O/emu8.log" > "$O/emu8.json" && cut -c 1-300 "$O/emu8.json"
 fi
 if has emu8trace; then
-    run trace_emu8 600 rocprofv3 --kernel-trace --stats -d "$O/trace_emu8" -o k -f csv -- python3 bench.py --emulate-shard 8 --steps 40 --warmup 4 --no-cpu --inflight 1 --prof-steps 4
+    run trace_emu8 600 rocprofv3 --kernel-trace --stats -d "$O/trace_emu8" -o k -f csv -- python3 bench.py --emulate-shard 8 --steps 40 --warmup 4 --no-cpu --inflight 1 --prof-steps 4 --latency-batches 0
     find "$O/trace_emu8" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_emu8.csv" \;
     head -14 "$O/kernel_stats_emu8.csv" | cut -c 1-160
 fi
@@ -94,7 +94,7 @@ if has tier5; then
     grep '^{' "$O/tier5.log" > "$O/tier5.json" && python3 -c "import json; d=json.load(open('$O/tier5.json')); print(json.dumps(d.get('tier')))"
 fi
 if has shardtrace; then
-    run trace_cfg4 600 rocprofv3 --kernel-trace --stats -d "$O/trace_cfg4" -o k -f csv -- python3 bench.py $CFG4 --steps 20 --warmup 2 --inflight 1
+    run trace_cfg4 600 rocprofv3 --kernel-trace --stats -d "$O/trace_cfg4" -o k -f csv -- python3 bench.py $CFG4 --steps 20 --warmup 2 --inflight 1 --latency-batches 0
     find "$O/trace_cfg4" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_cfg4_shard.csv" \;
     head -6 "$O/kernel_stats_cfg4_shard.csv"
 fi
