@@ -1218,20 +1218,41 @@ __global__ __launch_bounds__(256) void ivf_screen_tfinal(ScanArgs a) {
 }
 
 // Per collected pair: keep it if its lower bound is not above its pair's final threshold;
-// its rank among its pair's survivors into .w (~0: dropped).
+// its rank among its pair's survivors into .w (~0: dropped). The collect kernel appends a
+// ballot's candidates in lane order, so consecutive entries come in runs of one pair (up to
+// 16): each wave takes 64 consecutive entries and does one atomic per run (segmented by equal
+// pairs across its lanes) instead of one per survivor on the pair's counter.
 __global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ cand, const uint32_t* __restrict__ counters,
                                                          uint32_t cap, const uint32_t* __restrict__ thr,
                                                          const uint32_t* __restrict__ thr4,
                                                          const uint32_t* __restrict__ ovf, uint32_t* __restrict__ scnt) {
     const uint32_t n = min(counters[kCtrCand], cap);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint4 c = cand[i];
+    const int lane = lane_id();
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; i0 < n; i0 += gridDim.x * blockDim.x) {
+        const uint32_t i = i0 + (uint32_t)lane;
+        const bool act = i < n;
+        const uint4 c = act ? cand[i] : make_uint4(~0u, 0u, 0u, 0u);
         const uint32_t sp = c.x;
-        const uint4 t4 = *(const uint4*)(thr4 + (size_t)sp * 4);
-        const float T = fminf(ord_dec(thr[sp]),
-                              fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w))));
-        const bool keep = !ovf[sp] && !(__uint_as_float(c.z) > T);
-        cand[i].w = keep ? atomicAdd(&scnt[sp], 1u) : ~0u;
+        bool keep = false;
+        if (act) {
+            const uint4 t4 = *(const uint4*)(thr4 + (size_t)sp * 4);
+            const float T = fminf(ord_dec(thr[sp]),
+                                  fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w))));
+            keep = !ovf[sp] && !(__uint_as_float(c.z) > T);
+        }
+        // runs of equal pairs: a run starts where the previous lane's pair differs
+        const uint32_t prev = __shfl_up(sp, 1);
+        const uint64_t heads = __ballot(lane == 0 || prev != sp);
+        const uint64_t keeps = __ballot(keep);
+        const int start = 63 - __builtin_clzll(heads & (below | (1ull << lane)));  // this lane's run start
+        const uint64_t after = heads & ~(below | (1ull << lane));                   // later run starts
+        const int end = after ? __builtin_ctzll(after) - 1 : 63;                     // this lane's run end
+        const uint64_t run = (end == 63 ? ~0ull : ((1ull << (end + 1)) - 1ull)) & ~((1ull << start) - 1ull);
+        uint32_t base = 0;
+        if (lane == end && act && (keeps & run)) base = atomicAdd(&scnt[sp], (uint32_t)__popcll(keeps & run));
+        base = __shfl(base, end);
+        if (act) cand[i].w = keep ? base + (uint32_t)__popcll(keeps & run & below) : ~0u;
     }
 }
 
