@@ -794,7 +794,7 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_screen(ScanArgs a) {
 //    ceil(k/4)-th into the quarter slot of the wave's residue (the 4 waves of a wide item
 //    hold 4 distinct residues, so thr4's maximum is a valid threshold too);
 //  * a pair is collected unless lower bound > th (the inline test): (sorted pair, slot,
-//    lower bound) appended to a.cand (wave-aggregated atomic); beyond the capacity the
+//    lower bound) appended to a.cand (per-wave chunks reserved a block ahead); beyond the capacity the
 //    pair is marked overflowed;
 //  * every segment's partials are written empty.
 // Then (ivf_screen_filter / _offsets / _scatter / _recheck) each collected pair is kept
@@ -840,17 +840,42 @@ __device__ __forceinline__ float row_elem(const float (&u)[4], int e) {
     return __shfl(x, (lane_id() & ~15) + (e >> 2));
 }
 
+// Candidate slots of one wave: a.cand entries are reserved in chunks of kCandChunk (one atomic
+// on the batch's counter per chunk), the next chunk's atomic issued one block ahead of its use,
+// so no block's epilogue waits on a returning global access (vmcnt is in order: it would wait
+// for the next block's shadow prefetches too). The unused rest of a chunk is filled with
+// sentinel entries {~0, 0, 0, ~0} (never kept by the filter).
+constexpr uint32_t kCandChunk = 128;
+struct CandChunk {
+    uint32_t base = 0, left = 0;  // (wave-uniform) the current chunk's next entry and entries left
+    uint32_t next = 0;            // (wave-uniform) the first entry of the chunk reserved ahead
+    bool pending = false;
+};
+__device__ __forceinline__ void pad_cand(const ScanArgs& a, uint32_t base, uint32_t n) {
+    for (uint32_t i = (uint32_t)lane_id(); i < n; i += 64)
+        if (base + i < a.cand_cap) a.cand[base + i] = make_uint4(~0u, 0u, 0u, ~0u);
+}
+__device__ __forceinline__ void finish_cand(const ScanArgs& a, CandChunk& cc) {
+    pad_cand(a, cc.base, cc.left);
+    if (cc.pending) pad_cand(a, cc.next, kCandChunk);
+    cc.left = 0;
+    cc.pending = false;
+}
+
 // One wave: collect the candidates of segment `seg` of list it.list for the nq (<= 16 NG)
 // queries of the item starting at sorted pair it.pair_start + q0. NG = 2 (items of 17-32
 // queries): every shadow B tile the wave loads feeds two A operands (queries 0-15 and
 // 16-31: 8 MFMAs per k-step), so a list is streamed once per 32 queries, not per 16.
 // rl_lds: the wave's running lists of upper bounds (NG x 4 query rows; reset by the caller
-// per item); s_thr: the item's shared k-th (LDS); residue: the wave's quarter slot (0..3,
-// distinct per wave of an item).
+// per item); s_thr: the item's shared k-th (LDS); s_pst / s_qsc: the item's per-query pair
+// norms and int8 scales (LDS, loaded by the caller); s_mt / s_vs: the wave's LDS scratch for
+// one block's vector norms and scales; residue: the wave's quarter slot (0..3, distinct per
+// wave of an item); cc: the wave's candidate chunk.
 template <int M, int KD, int NG, bool I8, bool W2>
 __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanItem it, const int q0, const int nq,
                                                 const uint32_t seg, float4* rl_lds, uint32_t* s_thr,
-                                                const uint32_t residue) {
+                                                const float4* s_pst, const float* s_qsc, float4* s_mt, float* s_vs,
+                                                const uint32_t residue, CandChunk& cc) {
     const int lane = lane_id();
     const uint32_t dp = a.dp, ks = dp >> (I8 ? 6 : 5);  // (k-steps of 64 int8 or 32 bf16 dims)
     const uint32_t count = a.count[it.list];
@@ -876,17 +901,17 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                                                               (I8 ? 1 : 2)) +
                      (lane >> 4);
     uint32_t collected = 0;
-    // the shared thresholds (list-wide k-th, quarter slots) as last read: re-read every
-    // thr_every blocks (a stale value is larger, so only looser: still valid) so their
-    // latency is not paid by every block
-    // (kept across blocks in the one-workgroup-per-CU variant only: the two-workgroups-per-CU
-    // variant re-reads them every block, which keeps 8 registers free: 2 spills instead of 18)
+    // the shared thresholds (list-wide k-th, quarter slots) as last read, refreshed every
+    // thr_every blocks (a stale value is larger, so only looser: still valid); the 32-query
+    // variant also keeps them across blocks (its one workgroup per CU has the registers)
     float gthr[NG][4], gq4[NG][4];  // (and this wave's quarter slot)
 #pragma unroll
     for (int gg = 0; gg < NG; ++gg)
 #pragma unroll
         for (int r = 0; r < 4; ++r) gthr[gg][r] = gq4[gg][r] = __builtin_inff();
     const uint32_t thr_every = W2 ? a.thr_every : 1u;
+    // the pair whose shared thresholds this lane fetches (query lane mod 16 NG of the item)
+    const uint32_t spl = it.pair_start + q0 + min(lane & (16 * NG - 1), nq - 1);
 
     const uint4* sp = a.shadow + b0 * (uint64_t)ks * 256 + lane;
     uint4 xa[KD][4], qa[NG][KD];
@@ -899,6 +924,25 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
     }
     using AccT = std::conditional_t<I8, i32x4, f32x4>;
     for (uint32_t j = 0; j < nb; ++j) {
+        // The block's epilogue operands are issued ahead of its k-steps, so the epilogue waits
+        // on no global access: lane l's vector norms (and int8 scale), the shared thresholds
+        // of query l mod 16 NG, and the wave's next candidate chunk when the current one runs low
+        const uint64_t mslot = (b0 + j) * 64 + lane;
+        const float4 mt_l = a.meta[mslot];
+        float vs_l = 0.0f;
+        if constexpr (I8) vs_l = a.sscale[mslot];
+        const bool thr_now = j % thr_every == 0;
+        uint32_t gt_l = 0u;
+        uint4 t4_l = make_uint4(0u, 0u, 0u, 0u);
+        if (thr_now) {
+            gt_l = a.thr[spl];
+            t4_l = *(const uint4*)(a.thr4 + (size_t)spl * 4);
+        }
+        // (its reply is read at this block's epilogue: a reply held across blocks made the
+        // compiler wait for every load in flight before reading it)
+        const bool reserve = !cc.pending && cc.left < kCandChunk / 2;
+        uint32_t reply = 0;
+        if (reserve && lane == 0) reply = atomicAdd(a.ccount, kCandChunk);
         AccT acc[NG][4];
 #pragma unroll
         for (int gg = 0; gg < NG; ++gg)
@@ -930,6 +974,21 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                 for (int gg = 0; gg < NG; ++gg) qa[gg][u] = qa_row[gg][4 * ((s0 + u + KD) % ks)];
             });
         }
+        // (vector 16 vt + (lane & 15)'s norms are read from the wave's scratch below)
+        s_mt[lane] = mt_l;
+        if constexpr (I8) s_vs[lane] = vs_l;
+        if (reserve) {
+            cc.next = __builtin_amdgcn_readfirstlane(reply);
+            cc.pending = true;
+        }
+        float gthr_l = 0.0f, gq4_l = 0.0f;
+        if (thr_now) {
+            const float th4 =
+                fmaxf(fmaxf(ord_dec(t4_l.x), ord_dec(t4_l.y)), fmaxf(ord_dec(t4_l.z), ord_dec(t4_l.w)));
+            gthr_l = fminf(ord_dec(gt_l), th4);
+            gq4_l = ord_dec(residue == 0 ? t4_l.x : residue == 1 ? t4_l.y : residue == 2 ? t4_l.z : t4_l.w);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
         for (int gg = 0; gg < NG; ++gg) {
             const int g0 = 16 * gg;  // this group's first query of the item
@@ -939,15 +998,15 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
             float qsc[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const uint32_t pi = pair_of(min(g0 + 4 * (lane >> 4) + r, nq - 1));
-                pst[r] = a.pst[pi];
-                if constexpr (I8) qsc[r] = a.qscale[pi];
+                const int gc = min(g0 + 4 * (lane >> 4) + r, nq - 1);
+                pst[r] = s_pst[gc];
+                if constexpr (I8) qsc[r] = s_qsc[gc];
             }
 #pragma unroll
             for (int vt = 0; vt < 4; ++vt) {
-                const float4 mt = a.meta[(b0 + j) * 64 + 16 * vt + (lane & 15)];
+                const float4 mt = s_mt[16 * vt + (lane & 15)];
                 float vsc = 0.0f;
-                if constexpr (I8) vsc = a.sscale[(b0 + j) * 64 + 16 * vt + (lane & 15)];
+                if constexpr (I8) vsc = s_vs[16 * vt + (lane & 15)];
                 const bool valid = j * 64 + 16 * vt + (lane & 15) < nv;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -979,24 +1038,24 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
             // none of whose upper bounds is below any row's current k-th cannot change those
             // rows' first k elements (the only ones used): its sort and merge are skipped (the
             // list's elements k .. 63 may then go stale; elements 0 .. k-1 stay exact)
-            float th[4];
+            float th[4], pub_t[4], pub_q[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int g = g0 + 4 * (lane >> 4) + r;
                 const int gc = min(g, nq - 1);
-                const uint32_t spi = it.pair_start + q0 + gc;
                 float4* rlp = rl_lds + (gg * 4 + r) * 64 + lane;
                 const float4 rv = *rlp;
                 float rl[4] = {rv.x, rv.y, rv.z, rv.w};
                 float tw = row_elem(rl, k - 1), tq = row_elem(rl, kq - 1);
-                uint32_t* gt = a.thr + spi;
-                uint32_t* s4 = a.thr4 + (size_t)spi * 4;
-                if (j % thr_every == 0) {
-                    const uint4 t4 = *(const uint4*)s4;
-                    const float th4 = fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w)));
-                    gthr[gg][r] = fminf(ord_dec(*gt), th4);
-                    const uint32_t m4 = residue == 0 ? t4.x : residue == 1 ? t4.y : residue == 2 ? t4.z : t4.w;
-                    gq4[gg][r] = ord_dec(m4);
+                if (thr_now) {  // (lane gc fetched query gc's)
+                    const float gn = __shfl(gthr_l, gc), qn = __shfl(gq4_l, gc);
+                    if constexpr (W2) {
+                        gthr[gg][r] = fminf(gthr[gg][r], gn);
+                        gq4[gg][r] = fminf(gq4[gg][r], qn);
+                    } else {
+                        gthr[gg][r] = gn;
+                        gq4[gg][r] = qn;
+                    }
                 }
                 const float cur = fminf(gthr[gg][r], ord_dec(s_thr[gc]));
                 // Only upper bounds below min(tw, cur) are kept: one at or above a valid shared
@@ -1012,18 +1071,30 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                     tw = row_elem(rl, k - 1);
                     tq = row_elem(rl, kq - 1);
                 }
-                if ((lane & 15) == 0 && g < nq) {
-                    if (tw < cur) {
-                        atomicMin(&s_thr[g], ord_enc(tw));
-                        atomicMin(gt, ord_enc(tw));
-                    }
-                    if (tq < gq4[gg][r]) atomicMin(s4 + residue, ord_enc(tq));
-                }
+                // (published below by the lane of query g: no per-row addresses held)
+                pub_t[r] = tw < cur ? tw : __builtin_inff();
+                pub_q[r] = tq < gq4[gg][r] ? tq : __builtin_inff();
                 gthr[gg][r] = fminf(gthr[gg][r], tw);
                 gq4[gg][r] = fminf(gq4[gg][r], tq);
                 th[r] = g < nq ? fminf(tw, cur) : -__builtin_inff();
             }
-            // candidates: one atomic per block and group for the wave's whole batch of them
+            {  // lane 16 gg + q publishes query g0 + q's new k-th / quarter k-th (row q / 4, element q % 4)
+                const int lq = lane & 15, src = 16 * (lq >> 2), rs = lq & 3;
+                float pt = __builtin_inff(), pq = __builtin_inff();
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float t = __shfl(pub_t[r], src), q = __shfl(pub_q[r], src);
+                    if (rs == r) pt = t, pq = q;
+                }
+                if ((lane >> 4) == gg && g0 + lq < nq) {  // (then spl is this query's sorted pair)
+                    if (pt < __builtin_inff()) {
+                        atomicMin(&s_thr[g0 + lq], ord_enc(pt));
+                        atomicMin(a.thr + spl, ord_enc(pt));
+                    }
+                    if (pq < __builtin_inff()) atomicMin(a.thr4 + (size_t)spl * 4 + residue, ord_enc(pq));
+                }
+            }
+            // candidates: the wave's whole batch of them for this block and group into its chunk
             // (the ballots are recomputed for the writes rather than held: registers)
             auto lbv = [&](int vt, int r) -> float {
                 if constexpr (I8) return __int_as_float(acc[gg][vt][r]);
@@ -1038,9 +1109,28 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
 #pragma unroll
                 for (int r = 0; r < 4; ++r) tot += (uint32_t)__popcll(__ballot(is_cand(vt, r)));
             if (tot) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(a.ccount, tot);
-                base = __builtin_amdgcn_readfirstlane(base);
+                uint32_t base;
+                if (tot <= cc.left) {
+                    base = cc.base;
+                    cc.base += tot;
+                    cc.left -= tot;
+                } else if (tot > kCandChunk) {  // (a range of its own; the current chunk stays)
+                    uint32_t v = 0;
+                    if (lane == 0) v = atomicAdd(a.ccount, tot);
+                    base = __builtin_amdgcn_readfirstlane(v);
+                } else {  // the rest of the current chunk padded; the chunk reserved ahead
+                    pad_cand(a, cc.base, cc.left);
+                    uint32_t v = 0;
+                    if (cc.pending) {
+                        base = cc.next;
+                        cc.pending = false;
+                    } else {
+                        if (lane == 0) v = atomicAdd(a.ccount, kCandChunk);
+                        base = __builtin_amdgcn_readfirstlane(v);
+                    }
+                    cc.base = base + tot;
+                    cc.left = kCandChunk - tot;
+                }
                 collected += tot;
 #pragma unroll
                 for (int vt = 0; vt < 4; ++vt) {
@@ -1127,9 +1217,21 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
     __shared__ uint32_t s_thr[32];
     __shared__ uint32_t s_thr_w[4][16];
     __shared__ float4 s_rl[4][8 * 64];  // each wave's running lists (up to 2 groups x 4 query rows x 64 lanes)
+    __shared__ float4 s_pst[32], s_pst_w[4][16];  // the item's pair norms (wide: shared; narrow: per wave)
+    __shared__ float s_qsc[32], s_qsc_w[4][16];   // ... and int8 scales
+    __shared__ float4 s_mt[4][64];                // each wave's scratch: one block's vector norms
+    __shared__ float s_vs[4][64];                 // ... and int8 scales
     const uint32_t wv = wave_index();
     const int lane = lane_id();
     float4* rl = s_rl[wv];
+    CandChunk cc;
+    // (per-query pair norms of the item starting at sorted pair ps, query t)
+    auto pair_stats = [&](uint32_t ps, uint32_t t, float4* dp4, float* dsc) {
+        const uint32_t pr = a.sorted_pair[ps + t];
+        const uint32_t pi = (pr >> 16) * a.P + (pr & 0xFFFFu);
+        dp4[t] = a.pst[pi];
+        if (I8) dsc[t] = a.qscale[pi];
+    };
 
     auto drain_narrow = [&]() {
         const uint32_t n_narrow = a.counters[0];
@@ -1143,11 +1245,15 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
             it.seg = __builtin_amdgcn_readfirstlane(it.seg);
             it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
             it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
-            if (lane < (int)it.npairs) s_thr_w[wv][lane] = a.thr[it.pair_start + lane];
+            if (lane < (int)it.npairs) {
+                s_thr_w[wv][lane] = a.thr[it.pair_start + lane];
+                pair_stats(it.pair_start, lane, s_pst_w[wv], s_qsc_w[wv]);
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             const uint64_t t0 = a.stamps ? wall_clock64() : 0;
             reset_rl(rl, 4);
-            collect_segment<M, KD, 1, I8, W2>(a, it, 0, (int)it.npairs, it.seg, rl, s_thr_w[wv], it.seg & 3u);
+            collect_segment<M, KD, 1, I8, W2>(a, it, 0, (int)it.npairs, it.seg, rl, s_thr_w[wv], s_pst_w[wv],
+                                              s_qsc_w[wv], s_mt[wv], s_vs[wv], it.seg & 3u, cc);
             contribute_rl(a, it, 0, (int)it.npairs, rl);
             if (a.stamps && lane == 0)
                 put_stamp(a, ((uint64_t)idx << 16) | blockIdx.x, t0, it.npairs | (1u << 8) | (1u << 16) | ((uint64_t)it.list << 32));
@@ -1170,7 +1276,10 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
         it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
         const int nq = (int)it.npairs;
         if (threadIdx.x == 0) s_seg = 0;
-        if (threadIdx.x < (uint32_t)nq) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
+        if (threadIdx.x < (uint32_t)nq) {
+            s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
+            pair_stats(it.pair_start, threadIdx.x, s_pst, s_qsc);
+        }
         __syncthreads();
         const uint32_t seg_vectors = a.seg_blocks * 64;
         const uint32_t nseg = (a.count[it.list] + seg_vectors - 1) / seg_vectors;
@@ -1182,8 +1291,10 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
             if (lane == 0) sg = atomicAdd(&s_seg, 1u);
             sg = seg0 + __builtin_amdgcn_readfirstlane(sg);
             if (sg >= seg1) break;
-            if (W2 && nq > 16) collect_segment<M, KD, 2, I8, W2>(a, it, 0, nq, sg, rl, s_thr, wv);
-            else collect_segment<M, KD, 1, I8, W2>(a, it, 0, nq, sg, rl, s_thr, wv);
+            if (W2 && nq > 16)
+                collect_segment<M, KD, 2, I8, W2>(a, it, 0, nq, sg, rl, s_thr, s_pst, s_qsc, s_mt[wv], s_vs[wv], wv, cc);
+            else
+                collect_segment<M, KD, 1, I8, W2>(a, it, 0, nq, sg, rl, s_thr, s_pst, s_qsc, s_mt[wv], s_vs[wv], wv, cc);
             any = true;
         }
         if (any) contribute_rl(a, it, 0, nq, rl);
@@ -1192,6 +1303,7 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
             put_stamp(a, ((uint64_t)b << 16) | blockIdx.x, t_item, (uint32_t)nq | ((seg1 - seg0) << 8) | ((uint64_t)it.list << 32));
     }
     if (a.fused) drain_narrow();
+    finish_cand(a, cc);
 }
 
 // One wave per valid sorted pair: the k-th smallest of the union of its contributed upper-
@@ -1231,8 +1343,8 @@ __global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ can
     const uint64_t below = (1ull << lane) - 1ull;
     for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; i0 < n; i0 += gridDim.x * blockDim.x) {
         const uint32_t i = i0 + (uint32_t)lane;
-        const bool act = i < n;
-        const uint4 c = act ? cand[i] : make_uint4(~0u, 0u, 0u, 0u);
+        const uint4 c = i < n ? cand[i] : make_uint4(~0u, 0u, 0u, ~0u);
+        const bool act = c.x != ~0u;  // (sentinel: the padding of a collect wave's candidate chunk)
         const uint32_t sp = c.x;
         bool keep = false;
         if (act) {
