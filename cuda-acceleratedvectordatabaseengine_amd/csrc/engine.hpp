@@ -335,7 +335,7 @@ struct vdb_ivf {
     bool want_i8() const {
         if (!screen_defer) return false;
         if (screen_i8 != 2) return screen_i8 == 1;
-        return !tiered() && !i8_vetoed && last_P < 64;
+        return !tiered() && !i8_vetoed;
     }
     uint32_t screen_thr_every = 0;  // deferred collect: blocks between re-reads of the shared thresholds, 0 = automatic (option screen_thr_every)
     // Deferred re-checks (option screen_defer, default 1): the scan only collects candidates
@@ -990,15 +990,17 @@ struct vdb_ivf {
     }
 
     // The automatic shadow format's calibration (option screen_i8 = 2), at the build: one
-    // screened batch of 64 of the index's own vectors (one from each of 64 blocks spread over
-    // the lists) as queries, at the nprobe of the search that triggered the build and k = 10.
+    // screened batch of (up to) 64 of the index's own vectors (one from each of 64 blocks spread
+    // over the lists) as queries, at the nprobe of the search that triggered the build and k = 10.
     // int8 stays unless its survivors beyond k per valid (query, list) pair exceed
     // kCalibPpm of the (query, vector) pairs, or the candidates overflowed: a regime where
     // its ~5x wider bound re-checks more rows than its half-size stream saves (the two-level
     // mixture: 6.2 % and 44.4K vs 52.2K QPS; iid data: 0.3 %, 27.3K vs 25.3K).
     static constexpr uint64_t kCalibPpm = 15000;
     bool screen_calibrate() {
-        const uint32_t P = std::min<uint32_t>(nlist, last_P ? last_P : 32), k = 10, B = 64;
+        const uint32_t P = std::min<uint32_t>(nlist, last_P ? last_P : 32), k = 10;
+        // (at most one batch's queries at this nprobe: the plan kernel takes kPlanMaxPairs pairs)
+        const uint32_t B = std::min<uint32_t>(64, batch_cap(P, k));
         if (!arena_blocks || vdbk::topk_regs(k) != 1) return true;
         DevBuf<float> q, od;
         DevBuf<uint64_t> oi;

@@ -8,6 +8,7 @@
 // same results the x86 SSE path produces.
 #pragma clang fp contract(off)
 
+#include <stdexcept>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -2535,6 +2536,9 @@ void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint3
                  uint32_t* sorted_pair, uint32_t* part_base_sorted, uint32_t* part_base_qp, uint32_t* nseg_qp,
                  uint32_t* l1base_qp, uint2* l1_items, unsigned long long* stats, uint32_t* thr, uint32_t mfma_min,
                  hipStream_t s) {
+    // (the kernel sorts the batch's pairs in LDS arrays of kPlanMaxPairs: a larger batch would
+    // write past them; the engine cuts batches by batch_cap, this is the last line)
+    if ((uint64_t)B * P > (uint64_t)kPlanMaxPairs) throw std::length_error("launch_plan: batch x nprobe above kPlanMaxPairs");
     uint32_t np = 1;
     while (np < B * P) np <<= 1;
     ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, (uint32_t)wide, segs_item,

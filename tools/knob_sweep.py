@@ -108,9 +108,11 @@ def main():
                     s_ = streams[j % infl]
                     idx.search_device(q[(j % nqb) * B:].data_ptr(), B, args.nprobe, kk, od.data_ptr(), oi.data_ptr(),
                                       s_.cuda_stream)
+                t_sub = time.perf_counter()  # (host time to submit the nb calls: the GPU starves when it nears the step)
                 torch.cuda.synchronize()
                 print(json.dumps({"workload": wl, "opts": s, "inflight": infl,
-                                  "step_ms": round((time.perf_counter() - t0) / nb * 1e3, 4)}), flush=True)
+                                  "step_ms": round((time.perf_counter() - t0) / nb * 1e3, 4),
+                                  "submit_ms_per_call": round((t_sub - t0) / nb * 1e3, 4)}), flush=True)
             for n_, _ in opts:  # back to defaults
                 idx.set_option(n_, DEFAULTS[n_])
 
