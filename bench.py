@@ -21,6 +21,8 @@ checks the GPU results of that sample bit for bit.
 from __future__ import annotations
 
 import argparse
+import atexit
+import ctypes
 import importlib.util
 import json
 import os
@@ -738,17 +740,56 @@ def attach_engine_comm(vdb, idx, args, rank, world):
         os._exit(3)
 
 
+_DEDICATED_STREAMS = []
+
+
+def dedicated_streams(device, n):
+    """n streams, each on a hardware queue of its own. A plain stream takes the least-used of
+    the process's 4 queues when it is first used, so two of three batches in flight could
+    share a queue with a stream used earlier (the build's) and serialise: the 1/8 shard's step
+    at 3 in flight was 0.29 or 0.40 ms depending on which streams a run picked
+    (profiles/r05_hw_queue_probe.txt). A stream with a CU mask gets a queue of its own; the
+    mask enables every CU. (Falls back to plain streams if the call is unavailable.)"""
+    try:
+        path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+        hip = ctypes.CDLL(path)
+        ncu = torch.cuda.get_device_properties(device).multi_processor_count
+        words = (ncu + 31) // 32
+        mask = (ctypes.c_uint32 * words)(*([0xFFFFFFFF] * words))
+        out = []
+        for _ in range(n):
+            h = ctypes.c_void_p()
+            if hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), mask) != 0:
+                raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+            if not _DEDICATED_STREAMS:
+                atexit.register(_destroy_dedicated_streams)
+            _DEDICATED_STREAMS.append((hip, h))
+            out.append(torch.cuda.ExternalStream(h.value, device=device))
+        return out
+    except Exception:
+        return [torch.cuda.Stream(device) for _ in range(n)]
+
+
+def _destroy_dedicated_streams():
+    if _DEDICATED_STREAMS:
+        torch.cuda.synchronize()
+    while _DEDICATED_STREAMS:
+        hip, h = _DEDICATED_STREAMS.pop()
+        hip.hipStreamDestroy(h)
+
+
 def timed_region(vdb, idx, args, device, rank, world, queries, out_d, out_i, check=None):
     """W warm-up steps, then exactly K timed steps with `inflight` batches in flight,
     bracketed by barrier + synchronize, max over ranks; then the roofline pass: the same
     steps one at a time on one stream, so the engine's per-batch events time each scan
     launch on its own (and give the latency of a batch with nothing else in flight)."""
     B, k = args.batch, args.k
-    main_stream = torch.cuda.current_stream()
     # Batches in flight: step s runs on streams[s % inflight]; the engine gives each
     # concurrent search its own workspace slot, so one batch's small kernels and scan
-    # tail overlap the next batch's scan. Rank partials and gathers are per stream.
-    streams = [main_stream] + [torch.cuda.Stream(device) for _ in range(args.inflight - 1)]
+    # tail overlap the next batch's scan. Rank partials and gathers are per stream. Each
+    # stream has a hardware queue of its own (dedicated_streams).
+    torch.cuda.synchronize()
+    streams = dedicated_streams(device, args.inflight)
     # One packed record per rank and batch (f32 dist[B][k] | pad | u64 ids[B][k]): ONE
     # all-gather per batch over RCCL, then the on-device merge of the world records.
     rec = vdb.rank_record_bytes(B, k)

@@ -57,6 +57,7 @@ def main():
         bench.fill_rows(vdb, args, q, 0, nqb * B, 12346, st.cuda_stream)
         od = torch.empty((B, 1024), dtype=torch.float32, device=dev)
         oi = torch.empty((B, 1024), dtype=torch.int64, device=dev)
+        ded = {}
         for s in sets:
             opts = [o.split("=") for o in s.split(",") if o]
             kk, infl = 10, 1  # ("k=N", "inflight=N" in a set: the search's k, batches in flight; not engine options)
@@ -99,7 +100,9 @@ def main():
                   flush=True)
             if infl > 1:  # the step at `infl` batches in flight (round-robin streams, as bench.py)
                 idx.set_option("bounded_stats", 0)
-                streams = [st] + [torch.cuda.Stream(dev) for _ in range(infl - 1)]
+                if infl not in ded:  # (a hardware queue each, created once per depth)
+                    ded[infl] = bench.dedicated_streams(dev, infl)
+                streams = ded[infl]
                 nb = 100
                 for j in range(nb + 6):
                     if j == 6:
