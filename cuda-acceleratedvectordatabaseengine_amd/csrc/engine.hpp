@@ -538,7 +538,13 @@ struct vdb_ivf {
 
     // Order a collective on comm_stream after the work queued on s (returns comm_stream).
     void make_comm_stream() {  // with the communicator (the device must be current)
-        if (!comm_stream) HIPCHECK(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
+        // (high priority: a queue of its own, apart from the 4 the search streams share —
+        // profiles/r05_hw_queue_probe.txt — and the exchange dispatched ahead of scan work)
+        if (!comm_stream) {
+            int lo = 0, hi = 0;
+            HIPCHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIPCHECK(hipStreamCreateWithPriority(&comm_stream, hipStreamNonBlocking, hi));
+        }
     }
     hipStream_t comm_enter(SearchSlot& w, hipStream_t s) {
         if (!w.x_ready) {
