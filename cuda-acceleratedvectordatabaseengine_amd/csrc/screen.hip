@@ -1720,6 +1720,9 @@ void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, con
         ivf_screen_pairs<kIP><<<g, 256, 0, s>>>(q, BP, P, probes, cent_rm, dp, qres, pst, thr4, scnt, ovf, counters, ubcnt);
 }
 
+#ifndef VDB_COLLECT_KD
+#define VDB_COLLECT_KD 4
+#endif
 void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
     if (!grid_blocks) return;
     const bool w2 = a.wide_q > 16;
@@ -1734,6 +1737,8 @@ void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, 
         constexpr int KW = Ii ? 6 : 8;
         const uint32_t ks = a.dp / (Ii ? 64 : 32);
         if (Ww && ks % KW == 0) ivf_screen_collect<Mm, KW, Ww, Ii><<<g, 256, 0, s>>>(a);
+        else if (!Ww && VDB_COLLECT_KD != 4 && ks % VDB_COLLECT_KD == 0)  // (A/B builds of the 16-query depth)
+            ivf_screen_collect<Mm, VDB_COLLECT_KD, Ww, Ii><<<g, 256, 0, s>>>(a);
         else if (ks % 4 == 0) ivf_screen_collect<Mm, 4, Ww, Ii><<<g, 256, 0, s>>>(a);
         else if (ks % 2 == 0) ivf_screen_collect<Mm, 2, Ww, Ii><<<g, 256, 0, s>>>(a);
         else ivf_screen_collect<Mm, 1, Ww, Ii><<<g, 256, 0, s>>>(a);
