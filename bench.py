@@ -592,7 +592,8 @@ def main():
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (one-GPU rehearsal)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight (streams) in the timed region; 0 = 2 on one GPU (4: +5 %% QPS at "
-                         "twice the p99), 4 across ranks (1/8 shard: 0.27 ms per step against 0.29 at 3)")
+                         "twice the p99), 3 across ranks (with the communicator's stream, 4 active hardware "
+                         "queues: a fifth makes every queue slower, profiles/r05_sweep_slots.jsonl)")
     ap.add_argument("--latency-batches", type=int, default=1000,
                     help="batches per latency leg (p99 at the in-flight depth and one in flight; 0: p99 from the K steps)")
     ap.add_argument("--prof-steps", type=int, default=30,
@@ -666,12 +667,12 @@ def main():
         args.sharded_build |= args.cfg == "cfg4"
     if args.emulate_rank == "all" and not args.ranks_in_process:
         if args.inflight <= 0:
-            args.inflight = 4
+            args.inflight = 3
         sys.exit(run_emulated_ranks_procs(args))  # (before anything touches the GPU)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.inflight <= 0:
-        args.inflight = 4 if world > 1 else 2
+        args.inflight = 3 if world > 1 else 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()  # (does not initialise the GPU)

@@ -247,11 +247,7 @@ struct Coalescer {
 using namespace vdbe;
 
 #ifndef VDB_SLOTS
-// 4 workspace slots: 4 batches in flight run the 1/8 shard's step at 0.269-0.271 ms against
-// 0.291-0.293 ms with 3, cfg3 1.546 vs 1.571-1.600 ms (in-flight streams on queues of their
-// own; 5 slots: 0.315 ms; profiles/r05_sweep_slots.jsonl). (Round 1 measured 4 slower, with
-// batches that shared hardware queues.)
-#define VDB_SLOTS 4
+#define VDB_SLOTS 3  // 4 measured slower at the 1/8 shard: 108K QPS at 4 in flight, 90K at 3, vs 128K (3 slots, 3 in flight)
 #endif
 
 struct vdb_ivf {

@@ -34,7 +34,7 @@ SHORT="--steps 5 --warmup 1 --no-cpu --prof-steps 2 --latency-batches 0"
 # the bench lines read this call's PMC traffic, or the committed file when no traffic step ran
 TJ="$O/traffic.json"
 [[ ",$STEPS," == *",traffic"* ]] || TJ="$R/profiles/traffic.json"
-CFG4="--cfg cfg4 --emulate-shard 8 --no-cpu --inflight 4"
+CFG4="--cfg cfg4 --emulate-shard 8 --no-cpu --inflight 3"
 if has traffic; then
     run pmc_iid 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ivf_scan_|ivf_screen_collect" -d "$O/pmc_iid" -o f -f csv -- python3 bench.py $SHORT
     run pmc_mix 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ivf_scan_|ivf_screen_collect" -d "$O/pmc_mix" -o f -f csv -- python3 bench.py $SHORT --data mixture
@@ -42,7 +42,7 @@ if has traffic; then
         "$O/pmc_mix" 8 "10000000x768/4096/32/64/10/N1/mixture" | tail -3
 fi
 if has traffic8; then
-    run pmc_emu8 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ivf_scan_|ivf_screen_collect" -d "$O/pmc_emu8" -o f -f csv -- python3 bench.py $SHORT --emulate-shard 8 --inflight 4
+    run pmc_emu8 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "ivf_scan_|ivf_screen_collect" -d "$O/pmc_emu8" -o f -f csv -- python3 bench.py $SHORT --emulate-shard 8 --inflight 3
     python3 tools/pmc_traffic.py "$O/traffic.json" "$O/pmc_emu8" 8 "10000000x768/4096/32/64/10/N1/shard0of8" | tail -3
 fi
 if has traffic4; then
@@ -79,7 +79,7 @@ if has shard; then
 fi
 if has emu8; then
     # rank 0 of 8 cut from the headline index (the per-GPU work of the 8-GPU headline), 3 in flight
-    run emu8 600 python3 -u bench.py --emulate-shard 8 --inflight 4 --no-cpu --traffic-json "$TJ"
+    run emu8 600 python3 -u bench.py --emulate-shard 8 --inflight 3 --no-cpu --traffic-json "$TJ"
     grep '^{' "$O/emu8.log" > "$O/emu8.json" && cut -c 1-300 "$O/emu8.json"
 fi
 if has emu8trace; then
