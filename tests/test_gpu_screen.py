@@ -92,7 +92,7 @@ def test_screen_int8_shadow_hub_lists(metric, k):
             g.set_option("seg_vectors", seg)
             D, I, p = screen_stats(g, Q, nprobe, k, 130)
             assert_same(D, I, Dr, Ir)
-            assert p["bounded_blocks"] > 0 or (sg == 32 and k > 32), p  # (32-query items' LDS: k <= 32)
+            assert p["bounded_blocks"] > 0, p  # (the deferred collect serves every k <= 64 at both widths)
     g.set_option("screen_defer", 0)  # (the inline kernel: a bf16 shadow is built for it)
     assert_same(*search_all(g, Q, nprobe, k, 130), Dr, Ir)
     g.set_option("screen_defer", 1)
