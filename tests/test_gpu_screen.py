@@ -1,6 +1,7 @@
 """GPU parity of the screened scan (screen.hip, the default scan for L2 / IP, k <= 64):
-every (query, vector) distance is bounded on the matrix cores from a bf16 shadow of the
-lists and recomputed with the reference's sequential fp32 sum (search_list_cpu,
+every (query, vector) distance is bounded on the matrix cores from a residual shadow of the
+lists (int8 with per-vector scales or bf16, chosen by a calibration batch at the build) and
+recomputed with the reference's sequential fp32 sum (search_list_cpu,
 ivf_flat_index.cpp:347-370) only where it can reach the list's top-k. Results must stay
 bit-identical to the oracle whatever the screen prunes, so these cases stress it: hub
 lists probed by every query, both metrics, k up to the screen's 64 and just past it (the
@@ -354,3 +355,29 @@ def test_footprint_is_the_device_memory_and_one_fp32_copy():
     g.set_option("screen", 0)
     assert g.gpu_bytes_allocated() <= 1.15 * lists + (256 << 20), g.gpu_bytes_allocated()
     assert_same(*g.search(Q, nprobe=8, k=65), *o.search(Q, 8, 65))
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_automatic_shadow_at_large_nprobe(metric):
+    """The automatic shadow format (screen_i8 = 2) is calibrated by one screened batch of the
+    index's own vectors at the nprobe of the search that builds the screen. At nprobe 300 a
+    64-query batch holds 19,200 (query, probe) pairs, above the plan kernel's 8,192: the
+    calibration batch is cut like every batch (batch_cap); before that fix this search faulted
+    on the GPU. Results stay exact, the format built is reported, and 32-query items (nprobe
+    >= 64) serve k = 64."""
+    from test_gpu_parity import mirror_from_oracle
+    rng = np.random.default_rng(700 + metric)
+    dim, nlist, nprobe = 96, 300, 300
+    X = rng.standard_normal((20000, dim)).astype(np.float32)
+    Q = rng.standard_normal((70, dim)).astype(np.float32)
+    ids = np.arange(len(X), dtype=np.uint64)
+    o = oracle.OracleIndex(dim, nlist, metric)
+    o.centroids = X[:nlist] * 0.3
+    o.add(X, ids)
+    for k in (10, 64):
+        g = mirror_from_oracle(o, dim, nlist, metric)
+        g.add(X, ids)
+        D, I, p = screen_stats(g, Q, nprobe, k, 70)
+        assert_same(D, I, *o.search(Q, nprobe, k))
+        assert p["screen_shadow"] in (1, 2), p
+        assert p["bounded_blocks"] > 0, p  # (the screen served it)
