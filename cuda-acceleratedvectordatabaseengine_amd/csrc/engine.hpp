@@ -316,19 +316,14 @@ struct vdb_ivf {
     uint32_t screen_segs_auto = 4;  // segments per screened wide item (upload_directory; option segs_per_item)
     uint32_t screen_group = 0;      // queries per screened wide item at most: 16 or 32, 0 = automatic (option screen_group)
     // Shadow format of the deferred screen (option screen_i8): 1 = int8 with a per-vector scale
-    // (half the bf16 shadow's bytes, a ~4.6x wider bound); 0 (default) = bf16. Measured on the
-    // same box: the int8 collect is VALU-bound (bounds and candidate appends per pair, not
-    // bytes): cfg3 collect 2.12 vs 2.49 ms but 6.3x the re-checks (0.58 vs 0.17 ms), scan 2.72
-    // vs 2.67 ms; cfg4 shard 4.29 vs 4.09 ms; 1/8 shard 0.523 vs 0.560 ms. The inline kernel
+    // (half the bf16 shadow's bytes, a ~4.6x wider bound); 0 = bf16. The inline kernel
     // (screen_defer 0) always uses bf16.
-    // 2 (default) = automatic: int8 for lists in HBM searched with 16-query items (the build's
-    // triggering search has nprobe < 64), kept unless the calibration batch at the build vetoes
-    // it (screen_calibrate: survivors beyond k per pair above 1.5 % of the pairs, a regime
-    // where its wider bound re-checks more than its half-size stream saves); bf16 for
-    // 32-query items (VALU-bound there: cfg4 rank 0 of 8, 4.39 vs 4.10 ms per batch) and in
-    // the tier (each survivor is a row read from the home). Bench lines with the hybrid exact
-    // kernel: headline 27,321 vs 25,304 QPS, 1/8 shard at 3 in flight 173.3K vs 151.3K,
-    // mixture 44.4K vs 52.2K (calibration sends it to bf16).
+    // 2 (default) = automatic (want_i8): int8 for lists in HBM, at both item widths (16- and
+    // 32-query items), kept unless the calibration batch at the build vetoes it
+    // (screen_calibrate: survivors beyond k per pair above 1.5 % of the pairs, or an overflow:
+    // a regime where its wider bound re-checks more than its smaller stream saves); bf16 in the
+    // tier (each survivor is a row read from the home). Round 5, same box: cfg3 collect 1.40
+    // vs 2.43 ms (bf16), cfg4 shard 2.15 vs 3.38 ms; the mixture is vetoed (6.2 % excess).
     int screen_i8 = 2;
     bool i8_vetoed = false;  // (automatic: the calibration vetoed int8 for this handle)
     uint32_t last_P = 0;     // the nprobe of the search that triggers a screen build
@@ -466,7 +461,7 @@ struct vdb_ivf {
         DevBuf<float> qpad{true}, cd{true}, cdelta{true}, part_d{true}, slot_d{true}, carry_d{true}, carry2_d{true};
         DevBuf<uint64_t> part_i{true}, slot_i{true}, carry_i{true}, carry2_i{true};
         uint32_t carry_sel = 0;  // fused merge: the carry buffer the call's next batch reads (ping-pong)
-        uint32_t xfill = 0;      // (exchange_emulate_world) records placed in the other ranks' places
+        uint64_t xfill = 0;      // (exchange_emulate_world) the record size the other ranks' empty records were filled for
         const float* q = nullptr;  // the batch's zero-padded queries: qpad, or the caller's rows when dim == dp
         DevBuf<uint32_t> probes{true}, nseg_qp{true}, pbqp{true}, sorted_pair{true}, pbs{true}, counters{true},
             l1base{true}, cand{true}, thr{true};
@@ -525,9 +520,10 @@ struct vdb_ivf {
     bool comm_owned = false;
     uint32_t comm_rank = 0, comm_world = 1;
     // (option exchange_emulate_world, diagnostics) a communicator of world 1 exchanges records
-    // the size of W ranks' (the batch's record plus W - 1 earlier records of the same slot) and
+    // the size of W ranks' (the batch's record plus W - 1 empty records of the same layout) and
     // merges W records: the per-batch cost of an 8-GPU node's exchange and rank merge on one
-    // rank's timeline (one GPU cannot hold 8 ranks: RCCL refuses two ranks on one device)
+    // rank's timeline (one GPU cannot hold 8 ranks: RCCL refuses two ranks on one device); the
+    // results stay this handle's own exact answer
     uint32_t xchg_emulate = 0;
     uint32_t xchg_records() const { return comm_world > 1 ? comm_world : std::max<uint32_t>(1, xchg_emulate); }
     // Every collective of the communicator runs on this one stream, fenced by events
@@ -1041,7 +1037,7 @@ struct vdb_ivf {
         HIPCHECK(hipMemcpyAsync(hc, w.counters.p, sizeof(hc), hipMemcpyDeviceToHost, stream));
         HIPCHECK(hipStreamSynchronize(stream));
         const uint64_t surv = hc[vdbk::kCtrSurv], pairs = hc[vdbk::kCtrPairs], kvalid = (uint64_t)k * hc[vdbk::kCtrValid];
-        const bool overflow = hc[vdbk::kCtrCand] > screen_cand_cap;
+        const bool overflow = hc[vdbk::kCtrOvf] != 0;
         calib_excess_ppm = pairs ? (surv > kvalid ? surv - kvalid : 0) * 1000000ull / pairs : 0;
         return !overflow && calib_excess_ppm <= kCalibPpm;
     }
@@ -1173,7 +1169,7 @@ struct vdb_ivf {
         uint32_t hc[vdbk::kCounters];
         HIPCHECK(hipMemcpyAsync(hc, w.counters.p, sizeof(hc), hipMemcpyDeviceToHost, s));
         HIPCHECK(hipStreamSynchronize(s));
-        if (hc[vdbk::kCtrCand] > cap) {
+        if (hc[vdbk::kCtrOvf]) {  // (some candidate fell beyond the buffer; need: the slots reserved)
             need = hc[vdbk::kCtrCand];
             return nullptr;
         }
@@ -2218,7 +2214,9 @@ struct vdb_ivf {
                               w.items.p, w.items_w.p, w.counters.p, w.sorted_pair.p, w.pbs.p, w.pbqp.p, w.nseg_qp.p,
                               w.l1base.p, w.l1_items.p, st, w.thr.p, mfma_min, s);
         };
-        plan(stats.p);
+        // (the automatic shadow's calibration batch counts into scratch: profile_read reports
+        // the caller's batches only)
+        plan(calibrating ? stats_scratch.ensure(16) : stats.p);
         const bool in_ring = &w >= slots && &w < slots + kSlots;
         if (scan_window && in_ring && scan_seq >= scan_window) {  // the scan issued scan_window batches ago
             const SearchSlot& prev = slots[scan_hist[(scan_seq - scan_window) % 8]];
@@ -2229,7 +2227,7 @@ struct vdb_ivf {
         vdbk::ScanArgs sa{lists, tiered() ? cache_ids.p : arena_ids.p, d_block_off.p, d_count_local.p, w.q, w.items.p, w.items_w.p,
                                 w.counters.p, w.sorted_pair.p, w.pbs.p, w.part_d.p, w.part_i.p, d4, k,
                                 wide_stride, w.counters.p + 4, seg_blocks, segs_item, 0, w.thr.p,
-                                mfma_min, bounded_stats ? stats.p + 5 : nullptr};
+                                mfma_min, bounded_stats && !calibrating ? stats.p + 5 : nullptr};
         sa.rows_layout = rows_l ? 1u : 0u;
         // the bounded items first (the batch's most-probed lists), on the same stream
         if (mfma_min) vdbk::launch_scan_bounded(metric, (uint32_t)max_wide, sa, s);
@@ -2315,7 +2313,7 @@ struct vdb_ivf {
                         sa.floor_out = floor_host.p + floor_seq % ScreenFloor::kRing;
                         sa.floor_seq = floor_seq;
                     }
-                    sa.mstats = bounded_stats && !pass ? stats.p + 8 : nullptr;
+                    sa.mstats = bounded_stats && !pass && !calibrating ? stats.p + 8 : nullptr;
                     if (stamps_cap) {
                         sa.stamps = stamps_buf.p;
                         sa.stamps_cap = stamps_cap;
@@ -2618,11 +2616,10 @@ struct vdb_ivf {
         ensure_workspace(w, B, P, k);
         if (xworld) {
             const uint64_t rb = vdb_rank_record_bytes(B, k);
-            // (emulated exchange: W records are sent; the others hold earlier batches' records)
+            // (emulated exchange: W records are sent; the other ranks' places hold empty records)
             if (comm_world == 1 && xchg_emulate > 1 && w.xrec.cap < rb * xworld) {
                 slot_buf(w, w.xrec, rb * xworld);
                 w.xfill = 0;
-                HIPCHECK(hipMemsetAsync(w.xrec.p, 0xFF, rb * xworld, s));  // (empty entries until filled)
             }
             slot_buf(w, w.xrec, rb);
             slot_buf(w, w.xgat, rb * xworld);
@@ -2740,11 +2737,17 @@ struct vdb_ivf {
         if (comm_failed()) throw VdbError(VDB_ERR_DEVICE, comm_error_msg());
         EventSet* ev = prof && events_used ? &events[events_used - 1] : nullptr;  // (the call's last batch)
         const uint32_t nrec = xchg_records();
-        if (comm_world == 1 && nrec > 1 && w.xfill < nrec - 1) {
-            // (emulation: the slot's first W - 1 records fill the other ranks' places once)
+        if (comm_world == 1 && nrec > 1 && w.xfill != vdb_rank_record_bytes(B, k)) {
+            // (emulation: the other ranks' places hold EMPTY records of this batch's layout —
+            // (+inf or FLT_MAX, no id) entries the merge drops — so the emulated exchange moves
+            // and merges W records and the results stay this rank's exact answer;
+            // refilled whenever the record layout (B, k) changes)
             const uint64_t rb = vdb_rank_record_bytes(B, k);
-            HIPCHECK(hipMemcpyAsync(w.xrec.p + rb * (1 + w.xfill), w.xrec.p, rb, hipMemcpyDeviceToDevice, s));
-            ++w.xfill;
+            for (uint32_t r = 1; r < nrec; ++r)
+                vdbk::launch_fill_empty((uint64_t)B * k, (float*)(w.xrec.p + rb * r),
+                                        (uint64_t*)(w.xrec.p + rb * r + ((uint64_t)B * k * 4 + 7) / 8 * 8), s);
+            HIPCHECK(hipGetLastError());
+            w.xfill = rb;
         }
         const hipStream_t cs = comm_enter(w, s);
         nccl_settle(ncclAllGather(w.xrec.p, w.xgat.p, vdb_rank_record_bytes(B, k) * (comm_world == 1 ? nrec : 1), ncclUint8,

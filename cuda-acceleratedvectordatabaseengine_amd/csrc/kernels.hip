@@ -343,6 +343,9 @@ __global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict
     __shared__ uint32_t s_n;
     const uint32_t q = blockIdx.x;
     if (q >= B) return;
+    // (LDS audit: s_top_* hold 4 R x 64 entries, s_ci one chunk of <= 64 rows; the host
+    // launch checks both, this early-out is the device's last line)
+    if (P > 64u * R || ch > 64u || ch == 0u) return;
     const int lane = lane_id();
     const uint32_t w = wave_index();
     const float* ar = approx + (size_t)q * nlist;
@@ -721,6 +724,13 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     const uint32_t tid = threadIdx.x;
     const uint32_t BP = B * P;
     const uint32_t wide = wide_on;  // wide group size (0: no wide items)
+    // (LDS audit, VERDICT r5: the arrays above hold kPlanMaxPairs keys. launch_plan refuses a
+    // larger batch on the host; should one arrive anyway the kernel plans nothing — no items,
+    // no valid pairs — instead of writing past them)
+    if (NP > (uint32_t)kPlanMaxPairs || BP > NP) {
+        if (tid < (uint32_t)kCounters) counters[tid] = 0u;
+        return;
+    }
 
     if (tid == 0) {
         s_nvalid = 0;
@@ -1653,7 +1663,7 @@ __global__ __launch_bounds__(64 * W, 2 * 4 / W) void ivf_scan_wide(ScanArgs a) {
         it.seg = __builtin_amdgcn_readfirstlane(it.seg);
         it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
         it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
-        const int np = (int)it.npairs;
+        const int np = min((int)it.npairs, GW);  // (s_thr and the staged pairs hold GW queries: the plan's bound)
         const int gp = (np + 1) / 2;
         if (threadIdx.x < 2) s_seg[threadIdx.x] = 0;  // visible after the staging barrier below
         if (threadIdx.x < (uint32_t)np) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
@@ -1737,7 +1747,7 @@ __global__ __launch_bounds__(256, 2) void ivf_scan_bounded(ScanArgs a) {
         it.seg = __builtin_amdgcn_readfirstlane(it.seg);
         it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
         it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
-        const int np = (int)it.npairs;  // <= 16 (wide group 16)
+        const int np = min((int)it.npairs, 16);  // <= 16 (wide group 16; s_thr and s_cand hold 16)
         if (threadIdx.x == 0) s_seg = 0;
         if (threadIdx.x < (uint32_t)np) s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
         for (uint32_t e = threadIdx.x; e < 16 * d4; e += blockDim.x) {
@@ -2491,6 +2501,10 @@ void launch_select_rerank(int metric, int regs, const float* approx, const float
                           uint32_t nlist, uint32_t dp, const float* qpad, uint32_t B, uint32_t P, uint32_t* cand,
                           uint32_t* probes, hipStream_t s) {
     const uint32_t ch = rerank_rows(dp, regs);
+    // (the kernel's fixed LDS: s_top_* of 4 regs x 64 entries hold the partial top-P lists,
+    // s_ci one chunk of <= 64 candidate rows)
+    if (P > 64u * (uint32_t)regs || ch == 0 || ch > 64)
+        throw std::length_error("launch_select_rerank: nprobe above the top-P registers or no LDS chunk");
     const size_t lds = ((size_t)dp / 4 + (size_t)ch * (dp / 4 + 1)) * sizeof(float4);
 #define VDB_SR(R)                                                                                             \
     do {                                                                                                      \
@@ -2539,6 +2553,8 @@ void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint3
     // (the kernel sorts the batch's pairs in LDS arrays of kPlanMaxPairs: a larger batch would
     // write past them; the engine cuts batches by batch_cap, this is the last line)
     if ((uint64_t)B * P > (uint64_t)kPlanMaxPairs) throw std::length_error("launch_plan: batch x nprobe above kPlanMaxPairs");
+    // (wide items carry at most `wide` queries: the scan kernels' per-item LDS holds 16 or 32)
+    if (wide != 0 && wide != 16 && wide != 32) throw std::length_error("launch_plan: wide items of 16 or 32 queries only");
     uint32_t np = 1;
     while (np < B * P) np <<= 1;
     ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, (uint32_t)wide, segs_item,

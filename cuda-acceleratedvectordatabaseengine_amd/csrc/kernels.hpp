@@ -49,6 +49,9 @@ constexpr int kCtrValid = 8;   // valid (query, probe) pairs of the batch (sorte
 constexpr int kCtrCand = 9;    // candidates the screen collected (may exceed the buffer)
 constexpr int kCtrSurv = 10;   // survivors of the final thresholds
 constexpr int kCtrPairs = 11;  // (query, vector) pairs of the batch (saturating at 2^32 - 1)
+constexpr int kCtrOvf = 12;    // 1 when a collected candidate fell beyond the buffer (its pair marked in ovf)
+constexpr int kCtrReal = 13;   // candidates the screen collected (kCtrCand counts reserved slots: padded chunks)
+constexpr uint32_t kCandChunk = 128;  // candidate slots a collect wave reserves at once (screen.hip)
 constexpr int kCounters = 16;
 constexpr int kUbLists = 128;   // deferred screened scan: upper-bound lists kept per (query, list) pair
 

@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <stdexcept>
 #include <cfloat>
 #include <type_traits>
 
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(256) void ivf_screen_pairs(const float* __restrict_
             scnt[e] = 0u;
             ovf[e] = 0u;
             ubcnt[e] = 0u;
-            if (e == 0) counters[kCtrCand] = 0u;
+            if (e == 0) counters[kCtrCand] = counters[kCtrOvf] = counters[kCtrReal] = 0u;
         }
     for (uint32_t i = blockIdx.x * 4 + wave_index(); i < BP; i += gridDim.x * 4) {
         const float* qr = q + (size_t)(i / P) * dp;
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(256) void ivf_screen_pairs_i8(const float* __restri
         scnt[e] = 0u;
         ovf[e] = 0u;
         ubcnt[e] = 0u;
-        if (e == 0) counters[kCtrCand] = 0u;
+        if (e == 0) counters[kCtrCand] = counters[kCtrOvf] = counters[kCtrReal] = 0u;
     }
     for (uint32_t i = blockIdx.x * 4 + wave_index(); i < BP; i += gridDim.x * 4) {
         const float* qr = q + (size_t)(i / P) * dp;
@@ -845,10 +846,13 @@ __device__ __forceinline__ float row_elem(const float (&u)[4], int e) {
 // so no block's epilogue waits on a returning global access (vmcnt is in order: it would wait
 // for the next block's shadow prefetches too). The unused rest of a chunk is filled with
 // sentinel entries {~0, 0, 0, ~0} (never kept by the filter).
-constexpr uint32_t kCandChunk = 128;
+// (kCandChunk: kernels.hpp.) Reserved slots (counters[kCtrCand]) therefore exceed the candidates
+// (counters[kCtrReal], added once per wave at its end): the overflow, floor, calibration and
+// re-run decisions read kCtrOvf / kCtrReal, never the reserved count.
 struct CandChunk {
     uint32_t base = 0, left = 0;  // (wave-uniform) the current chunk's next entry and entries left
     uint32_t next = 0;            // (wave-uniform) the first entry of the chunk reserved ahead
+    uint32_t real = 0;            // (wave-uniform) candidates this wave collected
     bool pending = false;
 };
 __device__ __forceinline__ void pad_cand(const ScanArgs& a, uint32_t base, uint32_t n) {
@@ -858,7 +862,9 @@ __device__ __forceinline__ void pad_cand(const ScanArgs& a, uint32_t base, uint3
 __device__ __forceinline__ void finish_cand(const ScanArgs& a, CandChunk& cc) {
     pad_cand(a, cc.base, cc.left);
     if (cc.pending) pad_cand(a, cc.next, kCandChunk);
+    if (cc.real && lane_id() == 0) atomicAdd(a.ccount + (kCtrReal - kCtrCand), cc.real);
     cc.left = 0;
+    cc.real = 0;
     cc.pending = false;
 }
 
@@ -1132,6 +1138,7 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                     cc.left = kCandChunk - tot;
                 }
                 collected += tot;
+                cc.real += tot;
 #pragma unroll
                 for (int vt = 0; vt < 4; ++vt) {
 #pragma unroll
@@ -1145,8 +1152,10 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                             const uint32_t slot = (uint32_t)((b0 + j) * 64 + 16 * vt + (lane & 15));
                             if (idx < a.cand_cap)
                                 a.cand[idx] = make_uint4(spi, slot, __float_as_uint(lbv(vt, r)), 0u);
-                            else
+                            else {
                                 a.ovf[spi] = 1u;  // (any store of 1: idempotent)
+                                a.ccount[kCtrOvf - kCtrCand] = 1u;
+                            }
                         }
                         base += (uint32_t)__popcll(mm);
                     }
@@ -1158,6 +1167,18 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
         atomicAdd(&a.mstats[0], (unsigned long long)collected);
         atomicAdd(&a.mstats[1], (unsigned long long)nb);
     }
+}
+
+// (LDS audit) An item wider than the collect kernel's per-item LDS (s_thr, s_pst,
+// s_qsc: 32 queries for a wide item, 16 per wave for a narrow one) is never planned (the
+// plan kernel's items carry <= wide_q queries; launch_plan and launch_screen_collect check
+// the widths on the host). Should one arrive anyway, its pairs are marked overflowed, which
+// sends them to the exact recomputation over their planned segments (ivf_screen_pair_topk)
+// instead of writing past the arrays: results stay exact.
+__device__ __forceinline__ void overflow_item(const ScanArgs& a, uint32_t pair_start, uint32_t npairs, uint32_t t0,
+                                              uint32_t nt) {
+    for (uint32_t t = t0; t < npairs; t += nt) a.ovf[pair_start + t] = 1u;
+    if (t0 == 0) a.ccount[kCtrOvf - kCtrCand] = 1u;
 }
 
 __device__ __forceinline__ void reset_rl(float4* rl_lds, int rows) {
@@ -1245,6 +1266,10 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
             it.seg = __builtin_amdgcn_readfirstlane(it.seg);
             it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
             it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
+            if (it.npairs > 16u) {  // (never planned: see overflow_item)
+                overflow_item(a, it.pair_start, it.npairs, (uint32_t)lane, 64u);
+                continue;
+            }
             if (lane < (int)it.npairs) {
                 s_thr_w[wv][lane] = a.thr[it.pair_start + lane];
                 pair_stats(it.pair_start, lane, s_pst_w[wv], s_qsc_w[wv]);
@@ -1275,6 +1300,11 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
         it.pair_start = __builtin_amdgcn_readfirstlane(it.pair_start);
         it.npairs = __builtin_amdgcn_readfirstlane(it.npairs);
         const int nq = (int)it.npairs;
+        if (nq > (W2 ? 32 : 16)) {  // (never planned: see overflow_item; the barrier orders s_next)
+            overflow_item(a, it.pair_start, (uint32_t)nq, threadIdx.x, blockDim.x);
+            __syncthreads();
+            continue;
+        }
         if (threadIdx.x == 0) s_seg = 0;
         if (threadIdx.x < (uint32_t)nq) {
             s_thr[threadIdx.x] = a.thr[it.pair_start + threadIdx.x];
@@ -1409,7 +1439,7 @@ __global__ __launch_bounds__(1024) void ivf_screen_offsets(const uint32_t* __res
         // host reads the sequence before and after the counts and keeps only a match (floor.hpp))
         if (floor_out) {
             volatile uint32_t* f = (volatile uint32_t*)floor_out;
-            f[0] = counters[kCtrCand] > cap ? ~0u : total;
+            f[0] = counters[kCtrOvf] ? ~0u : total;
             f[1] = counters[kCtrPairs];
             f[3] = (uint32_t)min(0xFFFFFFFFull, (unsigned long long)k * n);
             __threadfence_system();
@@ -1621,7 +1651,7 @@ __global__ __launch_bounds__(256) void ivf_screen_pair_topk(ScanArgs a, const ui
         if (lane == 0) nseg_qp[(size_t)q * a.P + p] = 1u;
     }
     // (no pair overflowed unless the batch collected more candidates than the buffer holds)
-    const uint64_t tasks = a.counters[kCtrCand] > a.cand_cap ? (uint64_t)nvalid * smax : 0;
+    const uint64_t tasks = a.counters[kCtrOvf] ? (uint64_t)nvalid * smax : 0;
     const uint32_t segv = a.seg_blocks * 64;
     for (uint64_t t = wv; t < tasks; t += nw) {
         const uint32_t s = (uint32_t)(t % nvalid), j = (uint32_t)(t / nvalid);
@@ -1725,6 +1755,8 @@ void launch_screen_pairs(int metric, const float* q, uint32_t B, uint32_t P, con
 #endif
 void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
     if (!grid_blocks) return;
+    // (the kernel's per-item LDS holds 32 queries: wide items of 16 or 32 only)
+    if (a.wide_q != 16 && a.wide_q != 32) throw std::length_error("launch_screen_collect: items of 16 or 32 queries only");
     const bool w2 = a.wide_q > 16;
     const uint32_t g = std::min<uint32_t>(grid_blocks, w2 ? kPersistentBlocks / 2 : kPersistentBlocks);
     auto go = [&](auto m_c, auto w_c, auto i_c) {

@@ -352,8 +352,10 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * "tier_row_direct" (1, default: the screened tier reads survivors' rows with O_DIRECT),
  * "tier_row_qd" (256: survivor-row reads in flight), "tier_row_cache" (1, default: a file-home
  * screened tier fills its idle HBM cache with the largest lists, whose survivors' rows are then
- * copied from HBM instead of read from the file), "screen_i8" (0, default: the deferred
- * screen's shadow in bf16; 1: int8 with a per-vector scale, half the bytes, a wider bound), "screen_thr_every" (0 = automatic: blocks
+ * copied from HBM instead of read from the file), "screen_i8" (2, default: automatic —
+ * int8 for lists in HBM unless the build's calibration batch vetoes it (survivors beyond k above
+ * 1.5 % of the pairs, or an overflow), bf16 in the list-cache tier; 1: int8 with a per-vector
+ * scale, a quarter of the fp32 bytes, a wider bound; 0: bf16, half the fp32 bytes), "screen_thr_every" (0 = automatic: blocks
  * between the collect kernel's re-reads of the shared thresholds; 4 for 32-query items, else 1),
  * "screen_floor_ppm" (50000, default: a screened batch of at least "screen_floor_min" (4M)
  * (query, vector) pairs that overflowed its candidate buffer, or whose survivors beyond k per

@@ -61,6 +61,7 @@ def lib():
             "oracle_merge_ranks": (None, [_f32p, _u64p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _f32p, _u64p]),
             "oracle_select_nprobe": (None, [vp, _f32p, ctypes.c_uint32, _u32p]),
             "oracle_assign": (None, [vp, _f32p, ctypes.c_uint64, _u32p]),
+            "oracle_assign_mt": (None, [vp, _f32p, ctypes.c_uint64, _u32p, ctypes.c_int]),
             "oracle_get_centroids": (None, [vp, _f32p]),
             "oracle_set_centroids": (None, [vp, _f32p]),
             "oracle_list_count": (ctypes.c_uint64, [vp, ctypes.c_uint32]),
@@ -183,10 +184,15 @@ class OracleIndex:
         lib().oracle_select_nprobe(self._h, _p(q, _f32p), nprobe, _p(out, _u32p))
         return out
 
-    def assign(self, vectors: np.ndarray) -> np.ndarray:
+    def assign(self, vectors: np.ndarray, threads: int = 1) -> np.ndarray:
+        """assign_to_lists (cpp:259-295); threads != 1: rows over OpenMP threads (0: all),
+        bit-identical per row."""
         v = np.ascontiguousarray(vectors, dtype=np.float32)
         out = np.empty(v.shape[0], dtype=np.uint32)
-        lib().oracle_assign(self._h, _p(v, _f32p), v.shape[0], _p(out, _u32p))
+        if threads == 1:
+            lib().oracle_assign(self._h, _p(v, _f32p), v.shape[0], _p(out, _u32p))
+        else:
+            lib().oracle_assign_mt(self._h, _p(v, _f32p), v.shape[0], _p(out, _u32p), threads)
         return out
 
     @property

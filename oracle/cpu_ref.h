@@ -63,6 +63,8 @@ void oracle_merge_ranks(const float* dist, const uint64_t* ids, uint32_t nranks,
 void oracle_select_nprobe(oracle_ivf* h, const float* query, uint32_t nprobe, uint32_t* out);
 /* assign_to_lists (ivf_flat_index.cpp:259-295). */
 void oracle_assign(oracle_ivf* h, const float* vectors, uint64_t n, uint32_t* out);
+/* The same, rows over `threads` OpenMP threads (0: all): bit-identical per row. */
+void oracle_assign_mt(oracle_ivf* h, const float* vectors, uint64_t n, uint32_t* out, int threads);
 
 void oracle_get_centroids(oracle_ivf* h, float* out);
 void oracle_set_centroids(oracle_ivf* h, const float* centroids);

@@ -7,6 +7,11 @@
   fused persistent scan all run at their real shape. The oracle (ivf_flat_index.cpp:205-256
   restated) gets the GPU's centroids and every probed list; each search_device call is one
   reference search() call.
+  The list assignment that defines every list's contents (assign_to_lists,
+  ivf_flat_index.cpp:259-295) is pinned at this shape too: 16,384 rows of the database
+  re-generated on the device, assigned by the engine (MFMA bounds + exact re-check at D 768,
+  nlist 4096) against the oracle's argmin row by row, and the lists that hold those rows
+  compared with the oracle's membership in append order (their ids and vector bits).
 * cfg4 — 100M x 768, nlist 16384, nprobe 64 over 8 GPUs (307 GB in total, too large for
   one GPU): exact assignment of all 100M rows, the LPT plan from the final list sizes, and
   EVERY rank's shard built in turn (append of its owned lists only), its partial results
@@ -27,6 +32,37 @@ THREADS = 16  # the GPU box's CPU share
 
 def bits(a):
     return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def _window_assignment(g, o, dev, st, a, w, dim):
+    """Rows [a, a + w) of the seed-12345 database re-generated on the device: the engine's
+    assignment of them (vdb_ivf_assign_device) against the oracle's (cpp:259-295, strict '<'),
+    row by row. Returns the rows and the oracle's lists."""
+    import torch
+    with torch.cuda.stream(st):
+        rows = torch.empty((w, dim), dtype=torch.float32, device=dev)
+        vdb.gen_normal_device(rows.data_ptr(), w * dim, seed=12345, offset=a * dim, stream=st.cuda_stream)
+        out = torch.empty(w, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        g.assign_device(rows.data_ptr(), w, out.data_ptr())
+        torch.cuda.synchronize()
+        R, A = rows.cpu().numpy(), out.cpu().numpy().view(np.uint32)
+    Aref = o.assign(R, threads=THREADS)
+    bad = np.nonzero(A != Aref)[0]
+    assert bad.size == 0, f"{bad.size} of {w} rows assigned differently, first row {a + bad[0]}: gpu {A[bad[0]]} ref {Aref[bad[0]]}"
+    return R, Aref
+
+
+def _check_window_lists(g, R, Aref, a, lists):
+    """The engine's lists in append order: the ids it stores in [a, a + len(R)) are exactly the
+    window rows the oracle assigns to the list, ascending (add appends in input order,
+    cpp:148-202), with the rows' vector bits."""
+    for l in lists:
+        v, ids = g.get_list(int(l))
+        m = (ids >= a) & (ids < a + len(R))
+        want = np.nonzero(Aref == l)[0].astype(np.uint64) + np.uint64(a)
+        assert np.array_equal(ids[m], want), f"list {l}: window members differ or out of append order"
+        assert np.array_equal(bits(v[m]), bits(R[(want - np.uint64(a)).astype(np.int64)])), f"list {l}: vector bits differ"
 
 
 def _export_probed(g, o, Q, nprobe, owned=None):
@@ -80,6 +116,13 @@ def test_cfg3_10m_x_768_nlist4096_nprobe32_two_batches_in_flight():
         assert np.array_equal(bits(D[b * B:(b + 1) * B]), bits(Dr)), f"batch {b}: distance bits differ"
     # gpu_vs_cpu_test.cpp:209-219 validity rules
     assert np.all(np.isfinite(D)) and np.all(D >= 0) and np.all(I < n)
+    # the assignment at full scale (D 768, nlist 4096): 16,384 rows, two windows of the database
+    for a in (3_000_000, 9_000_000):
+        R, Aref = _window_assignment(g, o, dev, s0, a, 8192, dim)
+        lists, cnt = np.unique(Aref, return_counts=True)
+        order = np.argsort(-cnt, kind="stable")
+        # the lists holding most of the window's rows (the hub lists) and two of the fewest
+        _check_window_lists(g, R, Aref, a, list(lists[order[:3]]) + list(lists[order[-2:]]))
 
 
 CFG4 = dict(n=100_000_000, dim=768, nlist=16384, nprobe=64, k=10, world=8, chunk=10_000_000, nq=4)
@@ -125,6 +168,28 @@ def _cfg4_setup():
     return _cfg4
 
 
+@pytest.mark.timeout(900)
+def test_cfg4_assignment_nlist16384_matches_oracle():
+    """configs[3]'s list assignment, which decides every shard's contents: 4,096 rows in two
+    windows of the 100M database, the engine's bulk assignment (the pass every shard's build
+    uses) and a fresh vdb_ivf_assign_device of the same rows, both against the oracle's
+    argmin (cpp:259-295) at nlist 16384, D 768 — where near-ties are densest."""
+    import torch
+    e = _cfg4_setup()
+    dim, nlist = CFG4["dim"], CFG4["nlist"]
+    g = vdb.IVFFlatIndex(vdb.IVFFlatIndex.Config(dim, nlist, max_gpu_memory=0))
+    g.centroids = e["cent"]
+    o = oracle.OracleIndex(dim, nlist, 0)
+    o.centroids = e["cent"]
+    for a in (123_456, 77_777_216):
+        R, Aref = _window_assignment(g, o, e["dev"], e["stream"], a, 2048, dim)
+        bulk = e["asg"][a:a + 2048].cpu().numpy().view(np.uint32)
+        assert np.array_equal(bulk, Aref), f"bulk assignment differs at {np.nonzero(bulk != Aref)[0][:5] + a}"
+        e.setdefault("windows", []).append((a, R, Aref))
+    g.close()
+    torch.cuda.empty_cache()
+
+
 def _cfg4_rank(r):
     """Rank r of the LPT plan built on this GPU (plan_shard + append of its rows), its packed
     rank record for the queries against oracle_search_shard over only its probed lists."""
@@ -150,6 +215,9 @@ def _cfg4_rank(r):
         assert np.array_equal(g.list_sizes(), sizes)
         owned = e["plan"] == r
         assert np.array_equal(g.list_owners() == r, owned)
+        for a, R, Aref in e.get("windows", []):  # (this shard's lists holding rows of the windows)
+            mine = [l for l in np.unique(Aref) if owned[l]]
+            _check_window_lists(g, R, Aref, a, mine[:2])
         rec = e["records"][r * rb:]
         g.search_device(e["q"].data_ptr(), nq, nprobe, k, rec.data_ptr(), rec.data_ptr() + ids_off, s)
         torch.cuda.synchronize()

@@ -377,7 +377,17 @@ def test_automatic_shadow_at_large_nprobe(metric):
     for k in (10, 64):
         g = mirror_from_oracle(o, dim, nlist, metric)
         g.add(X, ids)
+        # (the first search builds and calibrates the screen; the statistics below are then
+        # this k's own batches: the calibration batch never counts into them)
+        assert_same(*g.search(Q[:8], nprobe=nprobe, k=k), *o.search(Q[:8], nprobe, k))
         D, I, p = screen_stats(g, Q, nprobe, k, 70)
         assert_same(D, I, *o.search(Q, nprobe, k))
         assert p["screen_shadow"] in (1, 2), p
         assert p["bounded_blocks"] > 0, p  # (the screen served it)
+    # the search that builds (and calibrates) the screen reports its own batches only: the
+    # blocks it screened equal those of the same search on the built screen
+    g = mirror_from_oracle(o, dim, nlist, metric)
+    g.add(X, ids)
+    _, _, p1 = screen_stats(g, Q, nprobe, 10, 70)
+    _, _, p2 = screen_stats(g, Q, nprobe, 10, 70)
+    assert p1["bounded_blocks"] == p2["bounded_blocks"] > 0, (p1, p2)

@@ -124,6 +124,26 @@ def test_multithreaded_search_equals_serial():
     assert np.array_equal(I1, I2) and np.array_equal(bits(D1), bits(D2))
 
 
+@pytest.mark.parametrize("metric", [0, 1])
+def test_multithreaded_assign_equals_serial(metric):
+    # the OpenMP assignment the full-scale GPU assignment tests check against: every row's
+    # argmin identical to the serial assign_to_lists (cpp:259-295) and to the numpy one,
+    # including ties (duplicated centroids go to the lowest index)
+    rng = np.random.default_rng(40 + metric)
+    X = rng.standard_normal((3000, 48)).astype(np.float32)
+    C = rng.standard_normal((100, 48)).astype(np.float32)
+    C[7] = C[3]
+    X[:50] = C[3]
+    o = oracle.OracleIndex(48, 100, metric)
+    o.centroids = C
+    a1 = o.assign(X)
+    for t in (0, 3, 8):
+        assert np.array_equal(o.assign(X, threads=t), a1)
+    assert np.array_equal(a1, npr.assign(metric, C, X))
+    if metric == 0:
+        assert np.all(a1[:50] == 3)
+
+
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_shard_decomposition(world):
     """Per-rank partials over the lists each rank owns, merged, equal the full search
