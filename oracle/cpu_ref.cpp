@@ -443,9 +443,13 @@ void oracle_assign(oracle_ivf* h, const float* v, uint64_t n, uint32_t* out) { h
 // serial one (cpp:259-295), so the result is bit-identical per row (checked on CPU against
 // oracle_assign in tests/test_oracle.py) and full-scale shapes finish in seconds.
 void oracle_assign_mt(oracle_ivf* h, const float* v, uint64_t n, uint32_t* out, int threads) {
-    const int nt = threads > 0 ? threads : omp_get_max_threads();
     const uint64_t chunk = 64;
+#ifdef _OPENMP
+    const int nt = threads > 0 ? threads : omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+#else
+    (void)threads;
+#endif
     for (uint64_t c0 = 0; c0 < n; c0 += chunk)
         h->assign(v + c0 * h->dim, std::min<uint64_t>(chunk, n - c0), out + c0);
 }
