@@ -668,6 +668,10 @@ int vdb_ivf_set_option(vdb_ivf* h, const char* name, int64_t value) {
             h->quiesce();
             h->screen_defer = value != 0;
             h->screen_update();
+        } else if (n == "screen_recheck2") {
+            h->set_device();
+            h->quiesce();
+            h->screen_recheck2 = value != 0;
         } else if (n == "screen_i8") {
             require(value >= 0 && value <= 2, "screen_i8 is 0 (bf16), 1 (int8) or 2 (automatic)");
             h->set_device();

@@ -339,6 +339,11 @@ struct vdb_ivf {
     // (re-checks as candidates appear, from a row-major fp32 copy of the lists).
     bool screen_defer = true;
     uint32_t screen_cand_cap = 4u << 20;  // collected candidates per batch (an overflowing pair is recomputed whole)
+    // Two-pass exact re-check (option screen_recheck2, default on; rows in HBM): per pair first the k
+    // survivors of smallest lower bound, then only the others whose lower bound is not above
+    // the k-th exact distance so far (screen.hip ivf_screen_recheck2); 0: every survivor of the
+    // final threshold (ivf_screen_exact_lane + ivf_screen_pair_topk). Results are identical.
+    bool screen_recheck2 = true;
     // One fp32 copy of the lists in HBM: while the screen is built, the row-major copy
     // (screen_rows, slot order: what the exact re-checks read) is the only one and the
     // interleaved arena is released (arena_dropped). Exact-path searches (k > 64, the
@@ -2293,6 +2298,7 @@ struct vdb_ivf {
             const uint32_t grid = (uint32_t)std::min<uint64_t>(want, cap);
             if (defer) {
                 const float* fetched = nullptr;
+                const bool recheck2 = screen_recheck2 && !tiered();  // (rows in HBM, by slot)
                 for (int pass = 0;; ++pass) {
                     if (pass) {  // a re-run after an overflow (tier, file home): plan and pairs reset the state
                         alloc_defer();
@@ -2325,7 +2331,10 @@ struct vdb_ivf {
                         HIPCHECK(hipEventRecord(ev->collect_end, s));
                         ev->collected = true;
                     }
-                    vdbk::launch_screen_select(sa, BP, w.scnt.p, w.soff.p, w.surv.p, w.ovf.p, s);
+                    // (the two-pass re-check, rows in HBM: the survivors' lower bounds go where the
+                    // one-pass path keeps their exact distances)
+                    vdbk::launch_screen_select(sa, BP, w.scnt.p, w.soff.p, w.surv.p, w.ovf.p, s,
+                                               recheck2 ? w.sdist.p : nullptr);
                     if (!tier_file) break;
                     uint32_t need = 0;
                     fetched = fetch_survivor_rows(w, ccap, need, s);
@@ -2343,7 +2352,8 @@ struct vdb_ivf {
                 }
                 if (tiered()) ++screen_tier_batches;
                 vdbk::launch_screen_recheck(metric, sa, BP, w.probes.p, w.nseg_qp.p, w.soff.p, w.scnt.p, w.surv.p, w.ovf.p,
-                                            fetched, w.sdist.p, ccap, (uint32_t)nseg_prefix[1], s);
+                                            fetched, w.sdist.p, ccap, (uint32_t)nseg_prefix[1], s,
+                                            recheck2 ? w.sdist.p : nullptr);
             } else {
                 vdbk::launch_scan_screen(metric, grid, sa, s);
             }

@@ -193,13 +193,15 @@ void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hip
 // survivors of it grouped per pair in surv with offsets soff[0 .. nvalid] and their count in
 // counters[kCtrSurv]), then the exact re-check of the survivors into each pair's only partial.
 void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
+// slb (optional): the survivors' lower bounds beside surv (the two-pass re-check reads them)
 void launch_screen_select(const ScanArgs& a, uint32_t BP, uint32_t* scnt, uint32_t* soff, uint2* surv,
-                          const uint32_t* ovf, hipStream_t s);
+                          const uint32_t* ovf, hipStream_t s, float* slb = nullptr);
 // surv: (slot, sorted pair) per survivor; fetched: null = rows from a.rows by slot, else the
 // survivors' rows [survivor][dp] (tier); sdist: their exact distances (max_surv entries).
 void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uint32_t* probes, uint32_t* nseg_qp,
                            const uint32_t* soff, const uint32_t* scnt, const uint2* surv, const uint32_t* ovf,
-                           const float* fetched, float* sdist, uint32_t max_surv, uint32_t smax, hipStream_t s);
+                           const float* fetched, float* sdist, uint32_t max_surv, uint32_t smax, hipStream_t s,
+                           const float* slb = nullptr);  // slb: the two-pass re-check (rows in HBM)
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                        const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,

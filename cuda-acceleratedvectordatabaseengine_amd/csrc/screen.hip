@@ -1451,11 +1451,14 @@ __global__ __launch_bounds__(1024) void ivf_screen_offsets(const uint32_t* __res
 __global__ __launch_bounds__(256) void ivf_screen_scatter(const uint4* __restrict__ cand,
                                                           const uint32_t* __restrict__ counters, uint32_t cap,
                                                           const uint32_t* __restrict__ soff,
-                                                          uint2* __restrict__ surv) {
+                                                          uint2* __restrict__ surv, float* __restrict__ slb) {
     const uint32_t n = min(counters[kCtrCand], cap);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint4 c = cand[i];
-        if (c.w != ~0u) surv[soff[c.x] + c.w] = make_uint2(c.y, c.x);  // (slot, sorted pair)
+        if (c.w != ~0u) {
+            surv[soff[c.x] + c.w] = make_uint2(c.y, c.x);  // (slot, sorted pair)
+            if (slb) slb[soff[c.x] + c.w] = __uint_as_float(c.z);  // (its lower bound: the two-pass re-check)
+        }
     }
 }
 
@@ -1689,6 +1692,180 @@ __global__ __launch_bounds__(256) void ivf_screen_pair_topk(ScanArgs a, const ui
     if (a.mstats && lane == 0 && rechecked) atomicAdd(&a.mstats[2], rechecked);
 }
 
+// The reference's sequential sum of one row-major row against the query row, kLaneRowPipe
+// float4 of both in flight per lane (ivf_screen_exact_lane's loop).
+template <int M>
+__device__ __forceinline__ float lane_row_dist(const float4* __restrict__ xr, const float4* __restrict__ qr,
+                                               uint32_t d4) {
+    float4 xb[kLaneRowPipe], qb[kLaneRowPipe];
+#pragma unroll
+    for (int p = 0; p < kLaneRowPipe; ++p) {
+        xb[p] = xr[p];
+        qb[p] = qr[p];
+    }
+    float acc = 0.0f;
+    for (uint32_t t0 = 0; t0 < d4; t0 += kLaneRowPipe) {
+        const bool more = t0 + kLaneRowPipe < d4;  // (wave-uniform)
+#pragma unroll
+        for (int p = 0; p < kLaneRowPipe; ++p) {
+            acc = acc4<M>(acc, qb[p], xb[p]);
+            if (more) {
+                xb[p] = xr[t0 + kLaneRowPipe + p];
+                qb[p] = qr[t0 + kLaneRowPipe + p];
+            }
+        }
+    }
+    return dist_finish<M>(acc);
+}
+
+// TWO-PASS exact re-check (default for rows in HBM; option screen_recheck2), in place of
+// ivf_screen_exact_lane + ivf_screen_pair_topk. One wave per valid sorted (query, list) pair
+// with n survivors of its final upper-bound threshold T (ivf_screen_filter):
+//  * n <= k: all of them, one round (one lane per survivor: the reference's sequential sum);
+//  * else pass A: the k survivors with the smallest lower bounds (key (lb, index), a wave
+//    top-k), one round; their k-th exact distance kd is a valid threshold (k vectors of the
+//    list are at or below it) and, on iid 768-D data, far below T (the k-th smallest UPPER
+//    bound: about one bound width, delta, above the k-th distance, so T admits a window of 2
+//    delta above it and kd one of delta);
+//  * pass B: every other survivor whose lower bound is not above the current kd (NaN bounds
+//    always), compacted 64 at a time through the wave's LDS ring; kd tightens with every
+//    round and each entry is tested again when its round starts.
+// A skipped survivor has lb > kd, i.e. an exact distance strictly above k distances of its
+// list: it cannot be in the list's multiset top-k (the exact scan's pruning rule), so the
+// pair's exact top-k — written as its only partial, as ivf_screen_pair_topk does — is the
+// same. Re-checks at the headline: ~37 per pair instead of ~110 (a CPU model of the int8
+// bound; the bench reports the measured count). Overflowed pairs: ivf_screen_pair_topk's
+// recomputation over their planned segments, unchanged.
+constexpr uint32_t kR2Ring = 128;
+template <int M>
+__global__ __launch_bounds__(256) void ivf_screen_recheck2(ScanArgs a, const uint32_t* __restrict__ probes,
+                                                           uint32_t* __restrict__ nseg_qp,
+                                                           const uint32_t* __restrict__ soff,
+                                                           const uint32_t* __restrict__ scnt,
+                                                           const uint2* __restrict__ surv,
+                                                           const float* __restrict__ slb,
+                                                           const uint32_t* __restrict__ ovf, uint32_t smax) {
+    __shared__ uint32_t s_ring[4][kR2Ring];
+    const int lane = lane_id();
+    const uint32_t wl = wave_index();
+    uint32_t* ring = s_ring[wl];
+    const uint32_t nvalid = a.counters[kCtrValid];
+    const int k = (int)a.k;
+    const uint32_t d4 = a.d4;
+    const float4* rows = (const float4*)a.rows;
+    const uint32_t wv = blockIdx.x * 4 + wl, nw = gridDim.x * 4;
+    unsigned long long rechecked = 0;
+    for (uint32_t s = wv; s < nvalid; s += nw) {
+        if (ovf[s]) continue;
+        const uint32_t pr = a.sorted_pair[s];
+        const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
+        const uint32_t n = scnt[s], o = soff[s];
+        const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
+        WaveTopK<1> tk;
+        tk.init();
+        float kd = __builtin_inff();
+        uint64_t ki = kNoId;
+        // one round: survivor o + idx per active lane (inactive lanes read the first active
+        // lane's row: no extra traffic, every load unconditional)
+        auto round = [&](bool act, uint32_t idx) {
+            const uint64_t m = __ballot(act);
+            if (!m) return;
+            const int first = __ffsll((long long)m) - 1;
+            const uint32_t ie = act ? idx : (uint32_t)__builtin_amdgcn_readlane((int)idx, first);
+            const uint64_t slot = surv[o + ie].x;
+            const float dist = lane_row_dist<M>(rows + slot * d4, qr, d4);
+            const uint64_t id = a.ids[slot];
+            offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
+            rechecked += (unsigned long long)__popcll(m);
+        };
+        if (n <= (uint32_t)k) {
+            round((uint32_t)lane < n, (uint32_t)lane);
+        } else {
+            // pass A: the k smallest keys (lb, index); NaN bounds first
+            WaveTopK<1> sel;
+            sel.init();
+            float sk = __builtin_inff();
+            uint64_t si = kNoId;
+            for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+                const uint32_t i = i0 + (uint32_t)lane;
+                const bool act = i < n;
+                const float lb = act ? slb[o + i] : __builtin_inff();
+                const float lk = lb == lb ? lb : -__builtin_inff();
+                offer_lanes<1>(sel, act && key_less(lk, i, sk, si), lk, (uint64_t)i, k, sk, si);
+            }
+            round(lane < k, (uint32_t)sel.id[0]);
+            // pass B: the others not above the current k-th exact distance
+            uint32_t head = 0, tail = 0;  // (wave-uniform ring cursors)
+            auto drain = [&](uint32_t cnt) {
+                const bool in = (uint32_t)lane < cnt;
+                const uint32_t idx = ring[(head + (in ? (uint32_t)lane : 0u)) & (kR2Ring - 1)];
+                head += cnt;
+                const float lb = slb[o + idx];
+                round(in && !(lb > kd), idx);
+            };
+            for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+                const uint32_t i = i0 + (uint32_t)lane;
+                const bool act = i < n;
+                const float lb = act ? slb[o + i] : __builtin_inff();
+                const float lk = lb == lb ? lb : -__builtin_inff();
+                const bool in_a = !key_less(sk, si, lk, (uint64_t)i);  // (lk, i) <= the k-th key of pass A
+                const bool want = act && !in_a && !(lb > kd);
+                const uint64_t m = __ballot(want);
+                if (want)
+                    ring[(tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))) &
+                         (kR2Ring - 1)] = i;
+                tail += (uint32_t)__popcll(m);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                if (tail - head >= 64) drain(64u);
+            }
+            if (tail != head) drain(tail - head);
+        }
+        // the pair's exact top-k is its only partial: the merge reads the first of its segments
+        const uint32_t part = a.part_base_sorted[s];
+        if (lane < k) {
+            a.part_d[(size_t)part * k + lane] = tk.d[0];
+            a.part_i[(size_t)part * k + lane] = tk.id[0];
+        }
+        if (lane == 0) nseg_qp[(size_t)q * a.P + p] = 1u;
+    }
+    // overflowed pairs: as ivf_screen_pair_topk (its planned segments recomputed)
+    const uint64_t tasks = a.counters[kCtrOvf] ? (uint64_t)nvalid * smax : 0;
+    const uint32_t segv = a.seg_blocks * 64;
+    for (uint64_t t = wv; t < tasks; t += nw) {
+        const uint32_t s = (uint32_t)(t % nvalid), j = (uint32_t)(t / nvalid);
+        if (!ovf[s]) continue;
+        const uint32_t pr = a.sorted_pair[s];
+        const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
+        if (j >= nseg_qp[(size_t)q * a.P + p]) continue;
+        const uint32_t list = probes[(size_t)q * a.P + p];
+        const uint32_t n = min(a.count[list], (j + 1) * segv);
+        const uint64_t lbase = a.block_off[list] * 64;
+        const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
+        WaveTopK<1> tk;
+        tk.init();
+        float kd = __builtin_inff();
+        uint64_t ki = kNoId;
+        for (uint32_t i0 = j * segv; i0 < n; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool act = i < n;
+            float dist = __builtin_inff();
+            uint64_t id = kNoId;
+            if (act) {
+                dist = exact_dist<M, true>(rows, lbase + i, d4, qr);
+                id = a.ids[lbase + i];
+            }
+            offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
+        }
+        rechecked += n > j * segv ? n - j * segv : 0;
+        const uint32_t part = a.part_base_sorted[s] + j;
+        if (lane < k) {
+            a.part_d[(size_t)part * k + lane] = tk.d[0];
+            a.part_i[(size_t)part * k + lane] = tk.id[0];
+        }
+    }
+    if (a.mstats && lane == 0 && rechecked) atomicAdd(&a.mstats[2], rechecked);
+}
+
 // Screened tier: survivor rows whose list is in the HBM cache ({row index, cache slot}: one wave
 // each) copied from the cache's block layout into the batch's row-major rows [n][dp].
 __global__ __launch_bounds__(256) void ivf_gather_cache_rows(const float4* __restrict__ cache, uint32_t d4,
@@ -1788,20 +1965,27 @@ void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, 
 }
 
 void launch_screen_select(const ScanArgs& a, uint32_t BP, uint32_t* scnt, uint32_t* soff, uint2* surv,
-                          const uint32_t* ovf, hipStream_t s) {
+                          const uint32_t* ovf, hipStream_t s, float* slb) {
     if (!BP) return;
     uint32_t* ctr = const_cast<uint32_t*>(a.counters);
     ivf_screen_tfinal<<<std::max<uint32_t>(1, std::min<uint32_t>(2048, (BP + 3) / 4)), 256, 0, s>>>(a);
     const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(1024, (a.cand_cap + 255) / 256));
     ivf_screen_filter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, a.thr, a.thr4, ovf, scnt);
     ivf_screen_offsets<<<1, 1024, 0, s>>>(scnt, ctr, soff, a.floor_out, a.floor_seq, a.cand_cap, a.k);
-    ivf_screen_scatter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, soff, surv);
+    ivf_screen_scatter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, soff, surv, slb);
 }
 
 void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uint32_t* probes, uint32_t* nseg_qp,
                            const uint32_t* soff, const uint32_t* scnt, const uint2* surv, const uint32_t* ovf,
-                           const float* fetched, float* sdist, uint32_t max_surv, uint32_t smax, hipStream_t s) {
+                           const float* fetched, float* sdist, uint32_t max_surv, uint32_t smax, hipStream_t s,
+                           const float* slb) {
     if (!BP) return;
+    if (slb && !fetched && a.rows) {  // the two-pass re-check (rows in HBM)
+        const uint32_t gp = std::max<uint32_t>(512, std::min<uint32_t>(2048, (BP + 3) / 4));
+        if (metric == kL2) ivf_screen_recheck2<kL2><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, slb, ovf, smax);
+        else ivf_screen_recheck2<kIP><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, slb, ovf, smax);
+        return;
+    }
     static const bool raised = [] {
         for (const void* fn : {(const void*)ivf_screen_exact<kL2, 0>, (const void*)ivf_screen_exact<kIP, 0>,
                                (const void*)ivf_screen_exact<kL2, 1>, (const void*)ivf_screen_exact<kIP, 1>,

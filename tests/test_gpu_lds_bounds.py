@@ -54,9 +54,8 @@ def test_select_rerank_at_nprobe_cap(metric):
     # lists re-ranked in LDS chunks of 64 rows at dim 64
     g, o, Q = _index(21 + metric, 30000, 64, 1100, metric)
     Q = Q[:40]
-    for nprobe in (1023, 1024):
+    for nprobe in (1023, 1024):  # (1024: the engine's nprobe cap; above it the call is refused)
         assert_same(*g.search(Q, nprobe=nprobe, k=10), *o.search(Q, nprobe, 10))
-    assert_same(*g.search(Q, nprobe=1100, k=10), *o.search(Q, 1100, 10))  # (clamped to nlist)
 
 
 @pytest.mark.parametrize("metric", [0, 1])

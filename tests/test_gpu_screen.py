@@ -125,6 +125,37 @@ def test_screen_int8_odd_dims_and_extremes(dim):
             assert_same(*g.search(Q, nprobe=3, k=k), *o.search(Q, 3, k))
 
 
+@pytest.mark.parametrize("i8", [1, 0], ids=["int8", "bf16"])
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("k", [1, 10, 17, 64])
+def test_two_pass_recheck(metric, k, i8):
+    """The two-pass exact re-check (ivf_screen_recheck2, default for rows in HBM): per pair
+    first the k survivors of smallest lower bound, then only the others whose lower bound is
+    not above the k-th exact distance so far. Hub lists probed by every query at 16- and
+    32-query items and two segment sizes: results identical to the oracle and to the one-pass
+    re-check (screen_recheck2 0), with fewer rows re-checked."""
+    X, ids, lists, C, Q = hub_data(64, seed=200 + k)
+    g, o = lists_pair(X, ids, lists, C, metric)
+    g.set_option("screen_i8", i8)
+    g.set_option("screen_floor_ppm", 0)
+    nprobe = 3 if metric == 0 else 6
+    Dr, Ir = o.search(Q, nprobe, k)
+    for sg in (16, 32):
+        g.set_option("screen_group", sg)
+        for seg in (0, 64):
+            g.set_option("seg_vectors", seg)
+            got = {}
+            for r2 in (1, 0):
+                g.set_option("screen_recheck2", r2)
+                D, I, p = screen_stats(g, Q, nprobe, k, 130)
+                assert_same(D, I, Dr, Ir)
+                got[r2] = p["exact_reranks"]
+            assert got[1] <= got[0], got
+            if k <= 17:
+                assert got[1] < got[0], got
+    g.set_option("screen_recheck2", 1)
+
+
 @pytest.mark.parametrize("metric", [0, 1])
 def test_screen_deferred_overflow_recomputes_the_pair(metric):
     """A candidate buffer far too small for the batch: every pair whose candidates do not fit

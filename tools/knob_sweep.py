@@ -27,7 +27,7 @@ import bench  # noqa: E402
 DEFAULTS = {"seg_vectors": 0, "segs_per_item": 0, "wide_stride": 1, "fused_scan": 1, "narrow_blocks": 64,
             "wide_group": 16, "fused_merge": 1, "scan_window": 0, "screen": 1, "bounded_stats": 0, "screen_group": 0,
             "screen_defer": 1, "screen_cand_cap": 4 << 20, "screen_floor_ppm": 50000, "screen_thr_every": 0, "screen_i8": 2,
-            "collect_stamps": 0, "scan_blocks": 0}
+            "collect_stamps": 0, "scan_blocks": 0, "screen_recheck2": 1}
 
 
 def main():
