@@ -178,6 +178,7 @@ bool scan_bounded_fits(uint32_t d4, uint32_t k);
 void launch_scan_bounded(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s);
 // ---- screened scan (screen.hip): L2 / IP, k <= 64, lists in HBM ----
 bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq, bool deferred);
+size_t screen_exact_lds(uint32_t d4);  // dynamic LDS of the LDS-staged exact re-check (screen_post.hip)
 void launch_gather_cache_rows(const float4* cache, uint32_t d4, const ulonglong2* src, uint32_t n, float* rows,
                               hipStream_t s);
 size_t screen_shadow_u4(uint64_t blocks, uint32_t d4, bool i8 = false);  // shadow size (uint4) incl. the prefetch slack

@@ -1336,561 +1336,11 @@ __global__ __launch_bounds__(256, W2 ? 1 : 2) void ivf_screen_collect(ScanArgs a
     finish_cand(a, cc);
 }
 
-// One wave per valid sorted pair: the k-th smallest of the union of its contributed upper-
-// bound lists (k vectors of the list have exact distances at or below it) lowers a.thr.
-__global__ __launch_bounds__(256) void ivf_screen_tfinal(ScanArgs a) {
-    const int lane = lane_id();
-    const uint32_t nvalid = a.counters[kCtrValid];
-    const int k = (int)a.k;
-    for (uint32_t s = blockIdx.x * 4 + wave_index(); s < nvalid; s += gridDim.x * 4) {
-        const uint32_t nl = min(a.ubcnt[s], (uint32_t)kUbLists);
-        const uint32_t n = nl * (uint32_t)k;
-        const float* src = a.ublist + (size_t)s * kUbLists * k;
-        float best = __builtin_inff();  // the 64 smallest so far, ascending over lanes
-        uint64_t bid = kNoId;
-        for (uint32_t e0 = 0; e0 < n; e0 += 64) {
-            float d = e0 + lane < n ? src[e0 + lane] : __builtin_inff();
-            uint64_t id = kNoId;
-            bitonic_sort64(d, id);
-            bitonic_merge64(best, bid, d, id);
-        }
-        const float kth = rd_lane(best, k - 1);
-        if (lane == 0 && kth < ord_dec(a.thr[s])) a.thr[s] = ord_enc(kth);
-    }
-}
-
-// Per collected pair: keep it if its lower bound is not above its pair's final threshold;
-// its rank among its pair's survivors into .w (~0: dropped). The collect kernel appends a
-// ballot's candidates in lane order, so consecutive entries come in runs of one pair (up to
-// 16): each wave takes 64 consecutive entries and does one atomic per run (segmented by equal
-// pairs across its lanes) instead of one per survivor on the pair's counter.
-__global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ cand, const uint32_t* __restrict__ counters,
-                                                         uint32_t cap, const uint32_t* __restrict__ thr,
-                                                         const uint32_t* __restrict__ thr4,
-                                                         const uint32_t* __restrict__ ovf, uint32_t* __restrict__ scnt) {
-    const uint32_t n = min(counters[kCtrCand], cap);
-    const int lane = lane_id();
-    const uint64_t below = (1ull << lane) - 1ull;
-    for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; i0 < n; i0 += gridDim.x * blockDim.x) {
-        const uint32_t i = i0 + (uint32_t)lane;
-        const uint4 c = i < n ? cand[i] : make_uint4(~0u, 0u, 0u, ~0u);
-        const bool act = c.x != ~0u;  // (sentinel: the padding of a collect wave's candidate chunk)
-        const uint32_t sp = c.x;
-        bool keep = false;
-        if (act) {
-            const uint4 t4 = *(const uint4*)(thr4 + (size_t)sp * 4);
-            const float T = fminf(ord_dec(thr[sp]),
-                                  fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w))));
-            keep = !ovf[sp] && !(__uint_as_float(c.z) > T);
-        }
-        // runs of equal pairs: a run starts where the previous lane's pair differs
-        const uint32_t prev = __shfl_up(sp, 1);
-        const uint64_t heads = __ballot(lane == 0 || prev != sp);
-        const uint64_t keeps = __ballot(keep);
-        const int start = 63 - __builtin_clzll(heads & (below | (1ull << lane)));  // this lane's run start
-        const uint64_t after = heads & ~(below | (1ull << lane));                   // later run starts
-        const int end = after ? __builtin_ctzll(after) - 1 : 63;                     // this lane's run end
-        const uint64_t run = (end == 63 ? ~0ull : ((1ull << (end + 1)) - 1ull)) & ~((1ull << start) - 1ull);
-        uint32_t base = 0;
-        if (lane == end && act && (keeps & run)) base = atomicAdd(&scnt[sp], (uint32_t)__popcll(keeps & run));
-        base = __shfl(base, end);
-        if (act) cand[i].w = keep ? base + (uint32_t)__popcll(keeps & run & below) : ~0u;
-    }
-}
-
-// Exclusive scan of the survivor counts of the batch's valid sorted pairs (one workgroup):
-// soff[0 .. nvalid], the total into counters[kCtrSurv].
-__global__ __launch_bounds__(1024) void ivf_screen_offsets(const uint32_t* __restrict__ scnt,
-                                                           uint32_t* __restrict__ counters,
-                                                           uint32_t* __restrict__ soff, uint4* __restrict__ floor_out,
-                                                           uint32_t floor_seq, uint32_t cap, uint32_t k) {
-    __shared__ uint32_t wsum[16];
-    const uint32_t n = counters[kCtrValid];
-    const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
-    const uint32_t c0 = min(n, threadIdx.x * per), c1 = min(n, c0 + per);
-    uint32_t s = 0;
-    for (uint32_t i = c0; i < c1; ++i) s += scnt[i];
-    // inclusive scan of s over the workgroup
-    uint32_t x = s;
-    const int lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[threadIdx.x >> 6] = x;
-    __syncthreads();
-    uint32_t wbase = 0, total = 0;
-    for (uint32_t w = 0; w < (blockDim.x >> 6); ++w) {
-        if (w < (threadIdx.x >> 6)) wbase += wsum[w];
-        total += wsum[w];
-    }
-    uint32_t o = wbase + x - s;
-    for (uint32_t i = c0; i < c1; ++i) {
-        soff[i] = o;
-        o += scnt[i];
-    }
-    if (threadIdx.x == 0) {
-        soff[n] = total;
-        counters[kCtrSurv] = total;
-        // (the run-time floor's report into its ring entry of page-locked host memory:
-        // {survivors or ~0 after an overflow, (query, vector) pairs, sequence, k x valid pairs}.
-        // The counts first, then a system-scope release fence, then the sequence number: the
-        // host reads the sequence before and after the counts and keeps only a match (floor.hpp))
-        if (floor_out) {
-            volatile uint32_t* f = (volatile uint32_t*)floor_out;
-            f[0] = counters[kCtrOvf] ? ~0u : total;
-            f[1] = counters[kCtrPairs];
-            f[3] = (uint32_t)min(0xFFFFFFFFull, (unsigned long long)k * n);
-            __threadfence_system();
-            f[2] = floor_seq;
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void ivf_screen_scatter(const uint4* __restrict__ cand,
-                                                          const uint32_t* __restrict__ counters, uint32_t cap,
-                                                          const uint32_t* __restrict__ soff,
-                                                          uint2* __restrict__ surv, float* __restrict__ slb) {
-    const uint32_t n = min(counters[kCtrCand], cap);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint4 c = cand[i];
-        if (c.w != ~0u) {
-            surv[soff[c.x] + c.w] = make_uint2(c.y, c.x);  // (slot, sorted pair)
-            if (slb) slb[soff[c.x] + c.w] = __uint_as_float(c.z);  // (its lower bound: the two-pass re-check)
-        }
-    }
-}
-
-// The exact sequential distance of `slot` for query row qr: from the interleaved arena
-// ([block][d4][64 lanes] float4; device or page-locked host memory) or a row-major row.
-template <int M, bool ROWS>
-__device__ __forceinline__ float exact_dist(const float4* __restrict__ src, uint64_t row_or_slot, uint32_t d4,
-                                            const float4* __restrict__ qr) {
-    constexpr int kP = 8;
-    const float4* base;
-    size_t stride;
-    if (ROWS) {
-        base = src + row_or_slot * d4;
-        stride = 1;
-    } else {
-        base = src + (row_or_slot >> 6) * (uint64_t)d4 * 64 + (row_or_slot & 63);
-        stride = 64;
-    }
-    float acc = 0.0f;
-    float4 xb[kP], qb[kP];
-#pragma unroll
-    for (int i = 0; i < kP; ++i) {
-        xb[i] = i < (int)d4 ? base[(size_t)i * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
-        qb[i] = i < (int)d4 ? qr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    for (uint32_t t0 = 0; t0 < d4; t0 += kP) {
-#pragma unroll
-        for (int i = 0; i < kP; ++i) {
-            if (t0 + i < d4) acc = acc4<M>(acc, qb[i], xb[i]);
-            const uint32_t tn = t0 + kP + i;
-            if (tn < d4) {
-                xb[i] = base[(size_t)tn * stride];
-                qb[i] = qr[tn];
-            }
-        }
-    }
-    return dist_finish<M>(acc);
-}
-
-// Exact distances of the survivors (one 64-thread workgroup per kExactRows of them, in
-// their per-pair order): the rows are loaded into LDS together, kExactRows x 1 KiB
-// contiguous wave-loads per 256 dims, all in flight at once, from the row-major fp32 copy
-// of the lists (SRC 0, slot-indexed), from rows fetched from the tier's file home (SRC 1,
-// [survivor][dp]), or from the interleaved arena in page-locked host memory (SRC 2, the
-// tier's host home, read over PCIe);
-// then one lane per row runs the reference's sequential sum over its LDS row (row stride
-// d4 + 1 float4: the lanes' rows fall on distinct banks) against its pair's query.
-#ifndef VDB_EXACT_LANE
-#define VDB_EXACT_LANE 1
-#endif
-constexpr bool kExactLane = VDB_EXACT_LANE != 0;  // (A/B builds: 0 = the LDS-staged kernel for HBM rows too)
-constexpr uint32_t kExactLaneMin = 16384;
-constexpr int kExactRows = 16;
-constexpr int kExactChunks = 3;  // 64-float4 chunks of a row loaded per pass (768 dims)
-__host__ __device__ constexpr size_t exact_lds(uint32_t d4) { return ((size_t)kExactRows * (d4 + 1) + 64) * 16; }
-
-template <int M, int SRC>
-__global__ __launch_bounds__(64) void ivf_screen_exact(ScanArgs a, const uint2* __restrict__ surv,
-                                                       const float* __restrict__ fetched,
-                                                       float* __restrict__ sdist) {
-    extern __shared__ __attribute__((aligned(16))) float4 rlds[];
-    const int lane = lane_id();
-    const uint32_t total = a.counters[kCtrSurv];
-    if (SRC != 2 && kExactLane && total >= kExactLaneMin) return;  // (ivf_screen_exact_lane's)
-    const uint32_t d4 = a.d4, rs = d4 + 1;
-    const float4* src = SRC == 1 ? (const float4*)fetched : SRC == 0 ? (const float4*)a.rows : a.arena;
-    for (uint32_t base = blockIdx.x * kExactRows; base < total; base += gridDim.x * kExactRows) {
-        const uint32_t ng = min((uint32_t)kExactRows, total - base);
-        const uint2 my = lane < (int)ng ? surv[base + lane] : make_uint2(0u, 0u);
-        // every load unconditional (clamped to valid rows and dims) so that all of them are in
-        // flight together; writes of clamped elements go to the LDS dump row kExactRows
-        for (uint32_t c0 = 0; c0 < d4; c0 += 64 * kExactChunks) {
-            float4 v[kExactRows][kExactChunks];
-#pragma unroll
-            for (int r = 0; r < kExactRows; ++r) {
-                const uint32_t rr = min((uint32_t)r, ng - 1);
-                const uint64_t row = SRC == 1 ? (uint64_t)(base + rr) : (uint64_t)__builtin_amdgcn_readlane(my.x, (int)rr);
-#pragma unroll
-                for (int c = 0; c < kExactChunks; ++c) {
-                    const uint32_t t = min(c0 + 64 * c + lane, d4 - 1);
-                    v[r][c] = SRC == 2 ? src[((row >> 6) * d4 + t) * 64 + (row & 63)] : src[row * d4 + t];
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < kExactRows; ++r)
-#pragma unroll
-                for (int c = 0; c < kExactChunks; ++c) {
-                    const uint32_t t = c0 + 64 * c + lane;
-                    rlds[(r < (int)ng && t < d4) ? r * rs + t : kExactRows * rs + lane] = v[r][c];
-                }
-        }
-        __syncthreads();
-        if (lane < (int)ng) {
-            const uint32_t q = a.sorted_pair[my.y] >> 16;
-            const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
-            const float4* xr = rlds + (size_t)lane * rs;
-            float acc = 0.0f;
-#pragma unroll 8
-            for (uint32_t t = 0; t < d4; ++t) acc = acc4<M>(acc, qr[t], xr[t]);
-            sdist[base + lane] = dist_finish<M>(acc);
-        }
-        __syncthreads();  // (the next rows overwrite the LDS)
-    }
-}
-
-// The same exact distances for rows in HBM (SRC 0: the row-major copy by slot; SRC 1: the
-// tier's fetched rows [survivor][dp]) when a batch has many survivors (at least
-// kExactLaneMin: the LDS-staged kernel, one round trip per 16 rows, is faster for a few
-// thousand), 64 survivors per wave, one lane each (the reference's
-// sequential sum needs one lane per (query, row) pair): every lane streams its own row and
-// its query (a few distinct queries per wave: the survivors are grouped per pair, so those
-// loads are mostly one address) kLaneRowPipe float4 ahead of its sum, without LDS. All 64
-// lanes sum (the LDS-staged kernel above keeps 48 idle and holds 50 KB of LDS per 16 rows).
-constexpr int kLaneRowPipe = 16;                  // (d4 is a multiple of 16 for the screen)
-template <int M, int SRC>
-__global__ __launch_bounds__(256) void ivf_screen_exact_lane(ScanArgs a, const uint2* __restrict__ surv,
-                                                             const float* __restrict__ fetched,
-                                                             float* __restrict__ sdist) {
-    const int lane = lane_id();
-    const uint32_t total = a.counters[kCtrSurv];
-    if (total < kExactLaneMin) return;  // (ivf_screen_exact's)
-    const uint32_t d4 = a.d4;
-    const float4* src = SRC == 1 ? (const float4*)fetched : (const float4*)a.rows;
-    for (uint32_t i0 = (blockIdx.x * 4 + wave_index()) * 64; i0 < total; i0 += gridDim.x * 256) {
-        const uint32_t i = min(i0 + (uint32_t)lane, total - 1);
-        const uint2 my = surv[i];
-        const float4* xr = src + (SRC == 1 ? (uint64_t)i : (uint64_t)my.x) * d4;
-        const float4* qr = (const float4*)(a.qpad + (size_t)(a.sorted_pair[my.y] >> 16) * a.dp);
-        float4 xb[kLaneRowPipe], qb[kLaneRowPipe];
-#pragma unroll
-        for (int p = 0; p < kLaneRowPipe; ++p) {
-            xb[p] = xr[p];
-            qb[p] = qr[p];
-        }
-        float acc = 0.0f;
-        for (uint32_t t0 = 0; t0 < d4; t0 += kLaneRowPipe) {
-            const bool more = t0 + kLaneRowPipe < d4;  // (wave-uniform)
-#pragma unroll
-            for (int p = 0; p < kLaneRowPipe; ++p) {
-                acc = acc4<M>(acc, qb[p], xb[p]);
-                if (more) {
-                    xb[p] = xr[t0 + kLaneRowPipe + p];
-                    qb[p] = qr[t0 + kLaneRowPipe + p];
-                }
-            }
-        }
-        if (i0 + (uint32_t)lane < total) sdist[i0 + lane] = dist_finish<M>(acc);
-    }
-}
-
-// One wave per valid sorted (query, list) pair: the exact top-k of its survivors' distances,
-// written as the pair's only partial. A pair that overflowed the candidate buffer keeps its
-// planned segments instead: one wave per (pair, segment) recomputes the segment lane =
-// vector from the row-major copy and writes the segment's partial (neighbouring waves take
-// the same segment of one list for neighbouring queries: its rows are shared in L2), so a
-// batch in the cancellation regime costs a parallel dense pass, not one wave per pair.
-template <int M>
-__global__ __launch_bounds__(256) void ivf_screen_pair_topk(ScanArgs a, const uint32_t* __restrict__ probes,
-                                                            uint32_t* __restrict__ nseg_qp,
-                                                            const uint32_t* __restrict__ soff,
-                                                            const uint32_t* __restrict__ scnt,
-                                                            const uint2* __restrict__ surv,
-                                                            const float* __restrict__ sdist,
-                                                            const uint32_t* __restrict__ ovf, uint32_t smax) {
-    const int lane = lane_id();
-    const uint32_t nvalid = a.counters[kCtrValid];
-    const int k = (int)a.k;
-    const uint32_t wv = blockIdx.x * 4 + wave_index(), nw = gridDim.x * 4;
-    unsigned long long rechecked = 0;
-    for (uint32_t s = wv; s < nvalid; s += nw) {
-        if (ovf[s]) continue;
-        const uint32_t pr = a.sorted_pair[s];
-        const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
-        WaveTopK<1> tk;
-        tk.init();
-        float kd = __builtin_inff();
-        uint64_t ki = kNoId;
-        const uint32_t n = scnt[s], o = soff[s];
-        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            const bool act = i < n;
-            const float dist = act ? sdist[o + i] : __builtin_inff();
-            const uint64_t id = act ? a.ids[surv[o + i].x] : kNoId;
-            offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
-        }
-        rechecked += n;
-        // the pair's exact top-k is its only partial: the merge reads the first of its segments
-        const uint32_t part = a.part_base_sorted[s];
-        if (lane < k) {
-            a.part_d[(size_t)part * k + lane] = tk.d[0];
-            a.part_i[(size_t)part * k + lane] = tk.id[0];
-        }
-        if (lane == 0) nseg_qp[(size_t)q * a.P + p] = 1u;
-    }
-    // (no pair overflowed unless the batch collected more candidates than the buffer holds)
-    const uint64_t tasks = a.counters[kCtrOvf] ? (uint64_t)nvalid * smax : 0;
-    const uint32_t segv = a.seg_blocks * 64;
-    for (uint64_t t = wv; t < tasks; t += nw) {
-        const uint32_t s = (uint32_t)(t % nvalid), j = (uint32_t)(t / nvalid);
-        if (!ovf[s]) continue;
-        const uint32_t pr = a.sorted_pair[s];
-        const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
-        if (j >= nseg_qp[(size_t)q * a.P + p]) continue;  // (the planned segments: untouched above)
-        const uint32_t list = probes[(size_t)q * a.P + p];
-        const uint32_t n = min(a.count[list], (j + 1) * segv);
-        const uint64_t lbase = a.block_off[list] * 64;
-        const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
-        WaveTopK<1> tk;
-        tk.init();
-        float kd = __builtin_inff();
-        uint64_t ki = kNoId;
-        for (uint32_t i0 = j * segv; i0 < n; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            const bool act = i < n;
-            float dist = __builtin_inff();
-            uint64_t id = kNoId;
-            if (act) {  // (the row-major copy, or the tier's host arena; a file home never overflows)
-                dist = a.rows ? exact_dist<M, true>((const float4*)a.rows, lbase + i, a.d4, qr)
-                              : exact_dist<M, false>(a.arena, lbase + i, a.d4, qr);
-                id = a.ids[lbase + i];
-            }
-            offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
-        }
-        rechecked += n > j * segv ? n - j * segv : 0;
-        const uint32_t part = a.part_base_sorted[s] + j;
-        if (lane < k) {
-            a.part_d[(size_t)part * k + lane] = tk.d[0];
-            a.part_i[(size_t)part * k + lane] = tk.id[0];
-        }
-    }
-    if (a.mstats && lane == 0 && rechecked) atomicAdd(&a.mstats[2], rechecked);
-}
-
-// The reference's sequential sum of one row-major row against the query row, kLaneRowPipe
-// float4 of both in flight per lane (ivf_screen_exact_lane's loop).
-template <int M>
-__device__ __forceinline__ float lane_row_dist(const float4* __restrict__ xr, const float4* __restrict__ qr,
-                                               uint32_t d4) {
-    float4 xb[kLaneRowPipe], qb[kLaneRowPipe];
-#pragma unroll
-    for (int p = 0; p < kLaneRowPipe; ++p) {
-        xb[p] = xr[p];
-        qb[p] = qr[p];
-    }
-    float acc = 0.0f;
-    for (uint32_t t0 = 0; t0 < d4; t0 += kLaneRowPipe) {
-        const bool more = t0 + kLaneRowPipe < d4;  // (wave-uniform)
-#pragma unroll
-        for (int p = 0; p < kLaneRowPipe; ++p) {
-            acc = acc4<M>(acc, qb[p], xb[p]);
-            if (more) {
-                xb[p] = xr[t0 + kLaneRowPipe + p];
-                qb[p] = qr[t0 + kLaneRowPipe + p];
-            }
-        }
-    }
-    return dist_finish<M>(acc);
-}
-
-// TWO-PASS exact re-check (default for rows in HBM; option screen_recheck2), in place of
-// ivf_screen_exact_lane + ivf_screen_pair_topk. One wave per valid sorted (query, list) pair
-// with n survivors of its final upper-bound threshold T (ivf_screen_filter):
-//  * n <= k: all of them, one round (one lane per survivor: the reference's sequential sum);
-//  * else pass A: the k survivors with the smallest lower bounds (key (lb, index), a wave
-//    top-k), one round; their k-th exact distance kd is a valid threshold (k vectors of the
-//    list are at or below it) and, on iid 768-D data, far below T (the k-th smallest UPPER
-//    bound: about one bound width, delta, above the k-th distance, so T admits a window of 2
-//    delta above it and kd one of delta);
-//  * pass B: every other survivor whose lower bound is not above the current kd (NaN bounds
-//    always), compacted 64 at a time through the wave's LDS ring; kd tightens with every
-//    round and each entry is tested again when its round starts.
-// A skipped survivor has lb > kd, i.e. an exact distance strictly above k distances of its
-// list: it cannot be in the list's multiset top-k (the exact scan's pruning rule), so the
-// pair's exact top-k — written as its only partial, as ivf_screen_pair_topk does — is the
-// same. Re-checks at the headline: ~37 per pair instead of ~110 (a CPU model of the int8
-// bound; the bench reports the measured count). Overflowed pairs: ivf_screen_pair_topk's
-// recomputation over their planned segments, unchanged.
-constexpr uint32_t kR2Ring = 128;
-template <int M>
-__global__ __launch_bounds__(256) void ivf_screen_recheck2(ScanArgs a, const uint32_t* __restrict__ probes,
-                                                           uint32_t* __restrict__ nseg_qp,
-                                                           const uint32_t* __restrict__ soff,
-                                                           const uint32_t* __restrict__ scnt,
-                                                           const uint2* __restrict__ surv,
-                                                           const float* __restrict__ slb,
-                                                           const uint32_t* __restrict__ ovf, uint32_t smax) {
-    __shared__ uint32_t s_ring[4][kR2Ring];
-    const int lane = lane_id();
-    const uint32_t wl = wave_index();
-    uint32_t* ring = s_ring[wl];
-    const uint32_t nvalid = a.counters[kCtrValid];
-    const int k = (int)a.k;
-    const uint32_t d4 = a.d4;
-    const float4* rows = (const float4*)a.rows;
-    const uint32_t wv = blockIdx.x * 4 + wl, nw = gridDim.x * 4;
-    unsigned long long rechecked = 0;
-    for (uint32_t s = wv; s < nvalid; s += nw) {
-        if (ovf[s]) continue;
-        const uint32_t pr = a.sorted_pair[s];
-        const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
-        const uint32_t n = scnt[s], o = soff[s];
-        const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
-        WaveTopK<1> tk;
-        tk.init();
-        float kd = __builtin_inff();
-        uint64_t ki = kNoId;
-        // one round: survivor o + idx per active lane (inactive lanes read the first active
-        // lane's row: no extra traffic, every load unconditional)
-        auto round = [&](bool act, uint32_t idx) {
-            const uint64_t m = __ballot(act);
-            if (!m) return;
-            const int first = __ffsll((long long)m) - 1;
-            const uint32_t ie = act ? idx : (uint32_t)__builtin_amdgcn_readlane((int)idx, first);
-            const uint64_t slot = surv[o + ie].x;
-            const float dist = lane_row_dist<M>(rows + slot * d4, qr, d4);
-            const uint64_t id = a.ids[slot];
-            offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
-            rechecked += (unsigned long long)__popcll(m);
-        };
-        if (n <= (uint32_t)k) {
-            round((uint32_t)lane < n, (uint32_t)lane);
-        } else {
-            // pass A: the k smallest keys (lb, index); NaN bounds first
-            WaveTopK<1> sel;
-            sel.init();
-            float sk = __builtin_inff();
-            uint64_t si = kNoId;
-            for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-                const uint32_t i = i0 + (uint32_t)lane;
-                const bool act = i < n;
-                const float lb = act ? slb[o + i] : __builtin_inff();
-                const float lk = lb == lb ? lb : -__builtin_inff();
-                offer_lanes<1>(sel, act && key_less(lk, i, sk, si), lk, (uint64_t)i, k, sk, si);
-            }
-            round(lane < k, (uint32_t)sel.id[0]);
-            // pass B: the others not above the current k-th exact distance
-            uint32_t head = 0, tail = 0;  // (wave-uniform ring cursors)
-            auto drain = [&](uint32_t cnt) {
-                const bool in = (uint32_t)lane < cnt;
-                const uint32_t idx = ring[(head + (in ? (uint32_t)lane : 0u)) & (kR2Ring - 1)];
-                head += cnt;
-                const float lb = slb[o + idx];
-                round(in && !(lb > kd), idx);
-            };
-            for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-                const uint32_t i = i0 + (uint32_t)lane;
-                const bool act = i < n;
-                const float lb = act ? slb[o + i] : __builtin_inff();
-                const float lk = lb == lb ? lb : -__builtin_inff();
-                const bool in_a = !key_less(sk, si, lk, (uint64_t)i);  // (lk, i) <= the k-th key of pass A
-                const bool want = act && !in_a && !(lb > kd);
-                const uint64_t m = __ballot(want);
-                if (want)
-                    ring[(tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))) &
-                         (kR2Ring - 1)] = i;
-                tail += (uint32_t)__popcll(m);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                if (tail - head >= 64) drain(64u);
-            }
-            if (tail != head) drain(tail - head);
-        }
-        // the pair's exact top-k is its only partial: the merge reads the first of its segments
-        const uint32_t part = a.part_base_sorted[s];
-        if (lane < k) {
-            a.part_d[(size_t)part * k + lane] = tk.d[0];
-            a.part_i[(size_t)part * k + lane] = tk.id[0];
-        }
-        if (lane == 0) nseg_qp[(size_t)q * a.P + p] = 1u;
-    }
-    // overflowed pairs: as ivf_screen_pair_topk (its planned segments recomputed)
-    const uint64_t tasks = a.counters[kCtrOvf] ? (uint64_t)nvalid * smax : 0;
-    const uint32_t segv = a.seg_blocks * 64;
-    for (uint64_t t = wv; t < tasks; t += nw) {
-        const uint32_t s = (uint32_t)(t % nvalid), j = (uint32_t)(t / nvalid);
-        if (!ovf[s]) continue;
-        const uint32_t pr = a.sorted_pair[s];
-        const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
-        if (j >= nseg_qp[(size_t)q * a.P + p]) continue;
-        const uint32_t list = probes[(size_t)q * a.P + p];
-        const uint32_t n = min(a.count[list], (j + 1) * segv);
-        const uint64_t lbase = a.block_off[list] * 64;
-        const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
-        WaveTopK<1> tk;
-        tk.init();
-        float kd = __builtin_inff();
-        uint64_t ki = kNoId;
-        for (uint32_t i0 = j * segv; i0 < n; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            const bool act = i < n;
-            float dist = __builtin_inff();
-            uint64_t id = kNoId;
-            if (act) {
-                dist = exact_dist<M, true>(rows, lbase + i, d4, qr);
-                id = a.ids[lbase + i];
-            }
-            offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
-        }
-        rechecked += n > j * segv ? n - j * segv : 0;
-        const uint32_t part = a.part_base_sorted[s] + j;
-        if (lane < k) {
-            a.part_d[(size_t)part * k + lane] = tk.d[0];
-            a.part_i[(size_t)part * k + lane] = tk.id[0];
-        }
-    }
-    if (a.mstats && lane == 0 && rechecked) atomicAdd(&a.mstats[2], rechecked);
-}
-
-// Screened tier: survivor rows whose list is in the HBM cache ({row index, cache slot}: one wave
-// each) copied from the cache's block layout into the batch's row-major rows [n][dp].
-__global__ __launch_bounds__(256) void ivf_gather_cache_rows(const float4* __restrict__ cache, uint32_t d4,
-                                                             const ulonglong2* __restrict__ src, uint32_t n,
-                                                             float4* __restrict__ rows) {
-    const int lane = lane_id();
-    for (uint32_t i = blockIdx.x * 4 + wave_index(); i < n; i += gridDim.x * 4) {
-        const ulonglong2 e = src[i];
-        const uint64_t blk = e.y >> 6, vl = e.y & 63;
-        for (uint32_t t = lane; t < d4; t += 64) rows[e.x * d4 + t] = cache[(blk * d4 + t) * 64 + vl];
-    }
-}
-
-void launch_gather_cache_rows(const float4* cache, uint32_t d4, const ulonglong2* src, uint32_t n, float* rows,
-                              hipStream_t s) {
-    if (!n) return;
-    const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(4096, (n + 3) / 4));
-    ivf_gather_cache_rows<<<g, 256, 0, s>>>(cache, d4, src, n, (float4*)rows);
-}
-
 bool scan_screen_fits(uint32_t k, uint32_t dp, uint32_t wq, bool deferred) {
     // (the deferred collect kernel's LDS is static and independent of k and the item width:
     // only the exact re-check's row staging counts; the inline kernel stages the item's
     // queries and its waves' top-k lists)
-    return k >= 1 && k <= 64 && dp % 64 == 0 && (wq == 16 || wq == 32) && exact_lds(dp / 4) <= kLdsBytes / 2 &&
+    return k >= 1 && k <= 64 && dp % 64 == 0 && (wq == 16 || wq == 32) && screen_exact_lds(dp / 4) <= kLdsBytes / 2 &&
            (deferred || screen_item_lds(k, wq) + 4 * screen_wave_lds(k) + 256 <= kLdsBytes / 2);
 }
 
@@ -1962,64 +1412,6 @@ void launch_screen_collect(int metric, uint32_t grid_blocks, const ScanArgs& a, 
     };
     if (metric == kL2) go_i(std::integral_constant<int, kL2>{});
     else go_i(std::integral_constant<int, kIP>{});
-}
-
-void launch_screen_select(const ScanArgs& a, uint32_t BP, uint32_t* scnt, uint32_t* soff, uint2* surv,
-                          const uint32_t* ovf, hipStream_t s, float* slb) {
-    if (!BP) return;
-    uint32_t* ctr = const_cast<uint32_t*>(a.counters);
-    ivf_screen_tfinal<<<std::max<uint32_t>(1, std::min<uint32_t>(2048, (BP + 3) / 4)), 256, 0, s>>>(a);
-    const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(1024, (a.cand_cap + 255) / 256));
-    ivf_screen_filter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, a.thr, a.thr4, ovf, scnt);
-    ivf_screen_offsets<<<1, 1024, 0, s>>>(scnt, ctr, soff, a.floor_out, a.floor_seq, a.cand_cap, a.k);
-    ivf_screen_scatter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, soff, surv, slb);
-}
-
-void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uint32_t* probes, uint32_t* nseg_qp,
-                           const uint32_t* soff, const uint32_t* scnt, const uint2* surv, const uint32_t* ovf,
-                           const float* fetched, float* sdist, uint32_t max_surv, uint32_t smax, hipStream_t s,
-                           const float* slb) {
-    if (!BP) return;
-    if (slb && !fetched && a.rows) {  // the two-pass re-check (rows in HBM)
-        const uint32_t gp = std::max<uint32_t>(512, std::min<uint32_t>(2048, (BP + 3) / 4));
-        if (metric == kL2) ivf_screen_recheck2<kL2><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, slb, ovf, smax);
-        else ivf_screen_recheck2<kIP><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, slb, ovf, smax);
-        return;
-    }
-    static const bool raised = [] {
-        for (const void* fn : {(const void*)ivf_screen_exact<kL2, 0>, (const void*)ivf_screen_exact<kIP, 0>,
-                               (const void*)ivf_screen_exact<kL2, 1>, (const void*)ivf_screen_exact<kIP, 1>,
-                               (const void*)ivf_screen_exact<kL2, 2>, (const void*)ivf_screen_exact<kIP, 2>})
-            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kLdsBytes / 2));
-        (void)hipGetLastError();
-        return true;
-    }();
-    (void)raised;
-    // (a grid-stride loop: 2048 workgroups of one wave cover 32K survivors per pass; a grid
-    // sized to the buffer's capacity launched 16384, nearly all of which found nothing to do)
-    const uint32_t ge = std::max<uint32_t>(1, std::min<uint32_t>(2048, (max_surv + kExactRows - 1) / kExactRows));
-    const size_t lds = exact_lds(a.d4);
-    // (a wave per pair, and at least 2048 waves for the (pair, segment) tasks of overflowed pairs)
-    const uint32_t gp = std::max<uint32_t>(512, std::min<uint32_t>(2048, (BP + 3) / 4));
-    const int src = fetched ? 1 : (a.rows ? 0 : 2);
-    // (rows in HBM: 64 survivors per wave, 4 waves per workgroup; the host arena over PCIe:
-    // 16 rows per workgroup)
-    const uint32_t gl = std::max<uint32_t>(1, std::min<uint32_t>(2048, (max_surv + 255) / 256));
-    auto exact = [&](auto m_c) {
-        constexpr int Mm = decltype(m_c)::value;
-        // (both kernels for rows in HBM: each serves the batch whose survivor count is its
-        // regime and returns at once otherwise; the count is known only on the device)
-        if (src == 0 && kExactLane && max_surv >= kExactLaneMin)
-            ivf_screen_exact_lane<Mm, 0><<<gl, 256, 0, s>>>(a, surv, fetched, sdist);
-        else if (src == 1 && kExactLane && max_surv >= kExactLaneMin)
-            ivf_screen_exact_lane<Mm, 1><<<gl, 256, 0, s>>>(a, surv, fetched, sdist);
-        if (src == 0) ivf_screen_exact<Mm, 0><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
-        else if (src == 1) ivf_screen_exact<Mm, 1><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
-        else ivf_screen_exact<Mm, 2><<<ge, 64, lds, s>>>(a, surv, fetched, sdist);
-        ivf_screen_pair_topk<Mm><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, sdist, ovf, smax);
-    };
-    if (metric == kL2) exact(std::integral_constant<int, kL2>{});
-    else exact(std::integral_constant<int, kIP>{});
 }
 
 void launch_scan_screen(int metric, uint32_t grid_blocks, const ScanArgs& a, hipStream_t s) {
