@@ -443,6 +443,9 @@ def tier_leg(vdb, idx, args, device, queries):
                       "survivor_rows_from_hbm_cache_per_batch": round(
                           (s1.get("screen_rows_cached", 0) - s0.get("screen_rows_cached", 0)) / batches, 1),
                       "survivor_row_bytes_per_batch": int((s1["screen_row_bytes"] - s0["screen_row_bytes"]) / batches),
+                      # file bytes read per byte of the survivor rows read (O_DIRECT granule supersets)
+                      "read_amplification": round((s1["file_bytes_read"] - s0["file_bytes_read"]) /
+                                                  max(s1["screen_row_bytes"] - s0["screen_row_bytes"], 1), 3),
                       "screen_batches": s1["screen_batches"] - s0["screen_batches"],
                       "screen_reruns": s1["screen_reruns"] - s0["screen_reruns"],
                       "first_call_s_incl_shadow_build": round(t_first, 1),
@@ -465,7 +468,13 @@ def tier_leg(vdb, idx, args, device, queries):
                              "survivor_rows_from_hbm_cache_per_batch": round(
                                  (v1.get("screen_rows_cached", 0) - v0.get("screen_rows_cached", 0)) / batches, 1),
                              "survivor_rows_read_per_batch": round((v1["screen_rows_fetched"] - v0["screen_rows_fetched"]) / batches, 1),
+                             "read_amplification": round((v1["file_bytes_read"] - v0["file_bytes_read"]) /
+                                                         max(v1["screen_row_bytes"] - v0["screen_row_bytes"], 1), 3),
                              "file_read_gbps": round((v1["file_bytes_read"] - v0["file_bytes_read"]) / ev / 1e9, 2)})
+            defaults = {"screen_recheck2": 1, "tier_row_direct": 1, "tier_row_cache": 1, "tier_row_qd": 256}
+            for nm, v in opts:  # (back to the defaults for what follows)
+                if nm in defaults:
+                    h.set_option(nm, defaults[nm])
         if args.tier_adapt > 0 and s1["screen_resident"]:
             # the row cache refilled by the survivor rows that other queries (the queries'
             # generator, another seed: tier_adapt of them, served in calls) needed per list

@@ -25,6 +25,7 @@
 #include <memory>
 #include <thread>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -32,6 +33,7 @@
 #include <random>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -437,6 +439,10 @@ struct vdb_ivf {
     // then pad + interleave kernels into the cache's block layout.
     int home_fd = -1;
     int home_fd_direct = -1;         // O_DIRECT descriptor of the same file (or -1: buffered)
+    // O_DIRECT granule the file system accepts for offsets and sizes, probed at open: 512 on
+    // most (a 3,072-B survivor row then reads 3,072 or 3,584 B), else 4096 (4 KiB-aligned
+    // supersets, 1.5-2 pages per row)
+    uint32_t dio_align = 4096;
     std::vector<uint64_t> file_off;  // per list: file offset of its ids (vectors follow)
     struct Stage {                   // one page-locked staging buffer of the read ring
         DevBuf<char> buf;
@@ -485,6 +491,9 @@ struct vdb_ivf {
         DevBuf<uint2> surv{true};
         DevBuf<float> ublist{true}, sdist{true};
         DevBuf<float> srows{true};
+        DevBuf<float> slb{true};         // screened tier, two-pass: the survivors' lower bounds
+        DevBuf<uint8_t> smark{true};     // ... their pass marks (1 A, 2 B)
+        DevBuf<uint32_t> rowmap{true};   // ... survivor -> compact fetched row
         DevBuf<uint8_t> xrec{true}, xgat{true};  // multi-GPU: this rank's packed partials, the gathered records
         DevBuf<float> gq{true};            // group member: the call's queries on this device
         DevBuf<uint32_t> greq{true};       // group member: the call's request starts on this device
@@ -506,6 +515,7 @@ struct vdb_ivf {
                                qres.device_bytes(), pst.device_bytes(), qscale.device_bytes(), thr4.device_bytes(), scand.device_bytes(),
                                scnt.device_bytes(), soff.device_bytes(), ovf.device_bytes(), ubcnt.device_bytes(),
                                surv.device_bytes(), ublist.device_bytes(), sdist.device_bytes(), srows.device_bytes(),
+                               slb.device_bytes(), smark.device_bytes(), rowmap.device_bytes(),
                                xrec.device_bytes(), xgat.device_bytes(), gq.device_bytes(), greq.device_bytes()})
                 b += x;
             return b;
@@ -1245,7 +1255,8 @@ struct vdb_ivf {
                     if (direct) {
                         const uint32_t b = free_slots.back();
                         free_slots.pop_back();
-                        const uint64_t a0 = off & ~4095ull, a1 = (off + row_bytes + 4095) & ~4095ull;
+                        const uint64_t g = dio_align;  // (the file system's O_DIRECT granule)
+                        const uint64_t a0 = off / g * g, a1 = (off + row_bytes + g - 1) / g * g;
                         delta[b] = off - a0;
                         slot_of[b] = si;
                         ur->read(home_fd_direct, bounce + (size_t)b * span, (uint32_t)(a1 - a0), a0,
@@ -1303,6 +1314,161 @@ struct vdb_ivf {
         }
         HIPCHECK(hipStreamSynchronize(s));  // (the staging and the cache's contents are reused later)
         return rows;
+    }
+
+    // Tier, file home, TWO-PASS re-check (option screen_recheck2): read the rows of the batch's
+    // survivors marked `phase` (1: pass A, each pair's k smallest lower bounds; 2: pass B, the
+    // others not above pass A's k-th exact distance; launch_tier_recheck) into the slot's
+    // compact device rows, after those of the earlier phase; a row needed again (the same
+    // vector surviving for another query, or in both phases) is read once. Rows of lists in the
+    // HBM cache are copied from there. The survivor -> row map is uploaded. Phase 1 returns
+    // false (need: the reserved candidate slots) when the candidate buffer overflowed: the
+    // caller re-runs the batch with a larger one.
+    std::vector<uint8_t> fetch_mark;
+    std::vector<uint32_t> fetch_rowmap;
+    std::unordered_map<uint64_t, uint32_t> fetch_slot_row;
+    uint32_t fetch_n = 0, fetch_rows_n = 0;
+    bool fetch_rows_phase(SearchSlot& w, int phase, uint32_t& need, hipStream_t s) {
+        if (phase == 1) {
+            uint32_t hc[vdbk::kCounters];
+            HIPCHECK(hipMemcpyAsync(hc, w.counters.p, sizeof(hc), hipMemcpyDeviceToHost, s));
+            HIPCHECK(hipStreamSynchronize(s));
+            if (hc[vdbk::kCtrOvf]) {
+                need = hc[vdbk::kCtrCand];
+                return false;
+            }
+            fetch_n = hc[vdbk::kCtrSurv];
+            fetch_surv.resize(fetch_n);
+            if (fetch_n) HIPCHECK(hipMemcpyAsync(fetch_surv.data(), w.surv.p, (size_t)fetch_n * 8, hipMemcpyDeviceToHost, s));
+            fetch_rows_n = 0;
+            fetch_slot_row.clear();
+            fetch_rowmap.assign(fetch_n, 0u);
+        }
+        const uint32_t n = fetch_n;
+        fetch_mark.resize(n);
+        if (n) HIPCHECK(hipMemcpyAsync(fetch_mark.data(), w.smark.p, n, hipMemcpyDeviceToHost, s));
+        HIPCHECK(hipStreamSynchronize(s));
+        if (surv_hist.size() != nlist) surv_hist.assign(nlist, 0);
+        // this phase's survivors: a slot read before maps to its row; new slots get rows j0 ..
+        const uint32_t j0 = fetch_rows_n;
+        std::vector<uint32_t> todo;  // (a survivor per new slot)
+        for (uint32_t i = 0; i < n; ++i) {
+            if (fetch_mark[i] != (uint8_t)phase) continue;
+            const uint64_t slot = fetch_surv[i].x;
+            ++surv_hist[sblist_host[slot >> 6]];
+            auto it = fetch_slot_row.find(slot);
+            if (it != fetch_slot_row.end()) {
+                fetch_rowmap[i] = it->second;
+                continue;
+            }
+            const uint32_t j = fetch_rows_n++;
+            fetch_slot_row.emplace(slot, j);
+            fetch_rowmap[i] = j;
+            todo.push_back(i);
+        }
+        const uint32_t nn = fetch_rows_n - j0;
+        fetch_stage.host = true;
+        float* st = fetch_stage.ensure((size_t)std::max<uint32_t>(nn, 1) * dim);
+        if (row_uring && row_uring->capacity() < tier_row_qd) row_uring.reset();
+        if (!row_uring) row_uring.reset(new UringReader(tier_row_qd));
+        UringReader* const ur = row_uring.get();
+        const uint64_t row_bytes = (uint64_t)dim * 4;
+        const bool direct = tier_row_direct && home_fd_direct >= 0;
+        const uint32_t kQD = std::min(tier_row_qd, row_uring->capacity());
+        const uint64_t span = ((row_bytes + 4095) / 4096 + 1) * 4096;
+        char* bounce = nullptr;
+        if (direct) {
+            fetch_bounce.host = true;
+            bounce = fetch_bounce.ensure(kQD * span + 4096);
+            bounce = (char*)(((uintptr_t)bounce + 4095) & ~(uintptr_t)4095);
+        }
+        // cached lists' rows from HBM; the rest read in file order
+        cache_src_host.clear();
+        std::vector<uint32_t> order;  // (positions in todo)
+        order.reserve(todo.size());
+        for (uint32_t t = 0; t < (uint32_t)todo.size(); ++t) {
+            const uint64_t slot = fetch_surv[todo[t]].x;
+            const uint32_t l = sblist_host[slot >> 6];
+            if (tier_row_cache && !cache_off.empty() && cache_off[l] != kAbsent)
+                cache_src_host.push_back({(unsigned long long)(j0 + t),
+                                          (unsigned long long)(cache_off[l] * 64 + (slot - sblock_off[l] * 64))});
+            else
+                order.push_back(t);
+        }
+        std::sort(order.begin(), order.end(),
+                  [&](uint32_t x, uint32_t y) { return fetch_surv[todo[x]].x < fetch_surv[todo[y]].x; });
+        std::vector<uint32_t> slot_of(kQD), free_slots(kQD);
+        for (uint32_t b = 0; b < kQD; ++b) free_slots[b] = kQD - 1 - b;
+        std::vector<uint64_t> delta(kQD);
+        uint64_t bytes_read = 0;
+        const uint32_t nf = (uint32_t)order.size();
+        uint32_t next = 0, done = 0;
+        try {
+            while (done < nf) {
+                while (next < nf && next - done < kQD) {
+                    const uint32_t t = order[next];
+                    const uint64_t slot = fetch_surv[todo[t]].x;
+                    const uint32_t l = sblist_host[slot >> 6];
+                    const uint64_t off = file_off[l] + count[l] * 8 + (slot - sblock_off[l] * 64) * row_bytes;
+                    if (direct) {
+                        const uint32_t b = free_slots.back();
+                        free_slots.pop_back();
+                        const uint64_t g = dio_align;
+                        const uint64_t a0 = off / g * g, a1 = (off + row_bytes + g - 1) / g * g;
+                        delta[b] = off - a0;
+                        slot_of[b] = t;
+                        ur->read(home_fd_direct, bounce + (size_t)b * span, (uint32_t)(a1 - a0), a0, ((uint64_t)b << 32) | t);
+                        bytes_read += a1 - a0;
+                    } else {
+                        ur->read(home_fd, st + (size_t)t * dim, (uint32_t)row_bytes, off, t);
+                        bytes_read += row_bytes;
+                    }
+                    ++next;
+                }
+                for (const UringReader::Done& d : ur->wait(1)) {
+                    const uint32_t b = (uint32_t)(d.tag >> 32), t = (uint32_t)d.tag;
+                    const int64_t want = direct ? (int64_t)(delta[b] + row_bytes) : (int64_t)row_bytes;
+                    require(d.result >= want,
+                            "short read of a survivor row from the list file" +
+                                (d.result < 0 ? std::string(": ") + std::strerror((int)-d.result) : ""),
+                            VDB_ERR_STATE);
+                    if (direct) {
+                        std::memcpy(st + (size_t)t * dim, bounce + (size_t)b * span + delta[b], row_bytes);
+                        free_slots.push_back(b);
+                    }
+                    ++done;
+                }
+            }
+        } catch (...) {
+            ur->drain();
+            throw;
+        }
+        screen_rows_fetched += nf;
+        screen_row_bytes += (uint64_t)nf * row_bytes;
+        screen_rows_cached += cache_src_host.size();
+        file_bytes_read += bytes_read;
+        float* rows = slot_buf(w, w.srows, (size_t)std::max<uint32_t>(n, 1) * dp);
+        if (nn) {
+            if (dim == dp) {
+                HIPCHECK(hipMemcpyAsync(rows + (size_t)j0 * dp, st, (size_t)nn * row_bytes, hipMemcpyHostToDevice, s));
+            } else {
+                HIPCHECK(hipMemcpyAsync(fetch_dev.ensure((size_t)std::max<uint32_t>(n, 1) * dim), st, (size_t)nn * row_bytes,
+                                        hipMemcpyHostToDevice, s));
+                vdbk::launch_pad_rows(fetch_dev.p, nn, dim, dp, rows + (size_t)j0 * dp, s);
+                HIPCHECK(hipGetLastError());
+            }
+        }
+        if (!cache_src_host.empty()) {  // (overwrites those rows' unused staging content)
+            if (tier_call_used) HIPCHECK(hipEventSynchronize(tier_call_ev));
+            const uint32_t nc = (uint32_t)cache_src_host.size();
+            HIPCHECK(hipMemcpyAsync(cache_src.ensure(nc), cache_src_host.data(), (size_t)nc * sizeof(ulonglong2),
+                                    hipMemcpyHostToDevice, s));
+            vdbk::launch_gather_cache_rows(cache.p, d4, cache_src.p, nc, rows, s);
+            HIPCHECK(hipGetLastError());
+        }
+        if (n) HIPCHECK(hipMemcpyAsync(w.rowmap.p, fetch_rowmap.data(), (size_t)n * 4, hipMemcpyHostToDevice, s));
+        HIPCHECK(hipStreamSynchronize(s));  // (the staging, the map and the cache's contents are reused later)
+        return true;
     }
 
     // Rebuild the arena so list l holds `keep[l]` of its current blocks at new
@@ -1674,6 +1840,14 @@ struct vdb_ivf {
         home_fd = fd;
         // lists are read with O_DIRECT where the file system allows it (no page-cache copy)
         home_fd_direct = ::open(path, O_RDONLY | O_CLOEXEC | O_DIRECT);
+        dio_align = 4096;
+        if (home_fd_direct >= 0) {  // (a 512-B read at a 512-B offset: accepted or EINVAL)
+            void* pb = nullptr;
+            if (posix_memalign(&pb, 4096, 4096) == 0) {
+                if (::pread(home_fd_direct, pb, 512, 512) == 512) dio_align = 512;
+                std::free(pb);
+            }
+        }
         char magic[8];
         uint32_t hdr[6] = {0, 0, 0, 0, 0, 0};
         pread_all(magic, 8, 0);
@@ -2256,6 +2430,11 @@ struct vdb_ivf {
                 slot_buf(w, w.sdist, ccap);
                 slot_buf(w, w.ubcnt, BP);
                 slot_buf(w, w.ublist, (size_t)BP * vdbk::kUbLists * k);
+                if (tier_file && screen_recheck2) {
+                    slot_buf(w, w.slb, ccap);
+                    slot_buf(w, w.smark, ccap);
+                    slot_buf(w, w.rowmap, ccap);
+                }
             };
             auto pairs = [&]() {
                 vdbk::launch_screen_pairs(metric, w.q, B, P, w.probes.p, cent_rm.p, dp,
@@ -2299,6 +2478,7 @@ struct vdb_ivf {
             if (defer) {
                 const float* fetched = nullptr;
                 const bool recheck2 = screen_recheck2 && !tiered();  // (rows in HBM, by slot)
+                const bool tier2 = screen_recheck2 && tier_file;       // (rows from the file, two read phases)
                 for (int pass = 0;; ++pass) {
                     if (pass) {  // a re-run after an overflow (tier, file home): plan and pairs reset the state
                         alloc_defer();
@@ -2334,11 +2514,20 @@ struct vdb_ivf {
                     // (the two-pass re-check, rows in HBM: the survivors' lower bounds go where the
                     // one-pass path keeps their exact distances)
                     vdbk::launch_screen_select(sa, BP, w.scnt.p, w.soff.p, w.surv.p, w.ovf.p, s,
-                                               recheck2 ? w.sdist.p : nullptr);
+                                               recheck2 ? w.sdist.p : tier2 ? w.slb.p : nullptr);
                     if (!tier_file) break;
                     uint32_t need = 0;
-                    fetched = fetch_survivor_rows(w, ccap, need, s);
-                    if (fetched) break;
+                    if (tier2) {  // (pass A marked, its rows read; pass B after the loop)
+                        vdbk::launch_tier_recheck(0, metric, sa, BP, w.nseg_qp.p, w.soff.p, w.scnt.p, w.surv.p, w.slb.p,
+                                                  w.smark.p, nullptr, nullptr, nullptr, s);
+                        if (fetch_rows_phase(w, 1, need, s)) {
+                            fetched = w.srows.p;
+                            break;
+                        }
+                    } else {
+                        fetched = fetch_survivor_rows(w, ccap, need, s);
+                        if (fetched) break;
+                    }
                     const uint64_t grow = std::max<uint64_t>((uint64_t)need + need / 2, (uint64_t)ccap + 1024);
                     if (grow > std::max<uint64_t>(tier_cand_max, screen_cand_cap)) {
                         // (a regime where the bound is wider than the distance spread: the
@@ -2351,9 +2540,19 @@ struct vdb_ivf {
                     ++screen_reruns;
                 }
                 if (tiered()) ++screen_tier_batches;
-                vdbk::launch_screen_recheck(metric, sa, BP, w.probes.p, w.nseg_qp.p, w.soff.p, w.scnt.p, w.surv.p, w.ovf.p,
-                                            fetched, w.sdist.p, ccap, (uint32_t)nseg_prefix[1], s,
-                                            recheck2 ? w.sdist.p : nullptr);
+                if (tier2) {  // pass A's exact distances and pass B's marks; its rows; the pairs' top-k
+                    vdbk::launch_tier_recheck(1, metric, sa, BP, w.nseg_qp.p, w.soff.p, w.scnt.p, w.surv.p, w.slb.p,
+                                              w.smark.p, w.rowmap.p, w.srows.p, w.sdist.p, s);
+                    uint32_t need = 0;
+                    (void)fetch_rows_phase(w, 2, need, s);
+                    vdbk::launch_tier_recheck(2, metric, sa, BP, w.nseg_qp.p, w.soff.p, w.scnt.p, w.surv.p, w.slb.p,
+                                              w.smark.p, w.rowmap.p, w.srows.p, w.sdist.p, s);
+                    HIPCHECK(hipGetLastError());
+                } else {
+                    vdbk::launch_screen_recheck(metric, sa, BP, w.probes.p, w.nseg_qp.p, w.soff.p, w.scnt.p, w.surv.p,
+                                                w.ovf.p, fetched, w.sdist.p, ccap, (uint32_t)nseg_prefix[1], s,
+                                                recheck2 ? w.sdist.p : nullptr);
+                }
             } else {
                 vdbk::launch_scan_screen(metric, grid, sa, s);
             }

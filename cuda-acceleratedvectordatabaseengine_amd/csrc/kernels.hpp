@@ -203,6 +203,13 @@ void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uin
                            const uint32_t* soff, const uint32_t* scnt, const uint2* surv, const uint32_t* ovf,
                            const float* fetched, float* sdist, uint32_t max_surv, uint32_t smax, hipStream_t s,
                            const float* slb = nullptr);  // slb: the two-pass re-check (rows in HBM)
+// The screened tier's two-pass re-check from the index file (screen_post.hip): phase 0 marks
+// each pair's pass-A survivors (mark 1), phase 1 computes their exact distances from the compact
+// fetched rows (rowmap: survivor -> row) and marks pass B (mark 2), phase 2 computes pass B and
+// writes each pair's exact top-k as its only partial.
+void launch_tier_recheck(int phase, int metric, const ScanArgs& a, uint32_t BP, uint32_t* nseg_qp, const uint32_t* soff,
+                         const uint32_t* scnt, const uint2* surv, const float* slb, uint8_t* mark, const uint32_t* rowmap,
+                         const float* fetched, float* sdist, hipStream_t s);
 void launch_slot_merge(int regs, const uint32_t* probes, const uint32_t* count_global,
                        const uint32_t* nseg_qp, const uint32_t* part_base_qp, const uint32_t* l1base_qp,
                        const float* part_d, const uint64_t* part_i, const float* l1_d, const uint64_t* l1_i,

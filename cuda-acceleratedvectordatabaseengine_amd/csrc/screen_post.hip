@@ -626,4 +626,163 @@ void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uin
     else exact(std::integral_constant<int, kIP>{});
 }
 
+// ============================================================================
+// The screened tier's two-pass re-check (file home): the survivors' rows are read from the
+// index file by the host, so the two passes of ivf_screen_recheck2 become two read phases —
+// only the rows each pass needs are read. Rows arrive compact ([j][dp], j =
+// rowmap[survivor]); mark[survivor]: 1 pass A, 2 pass B, 0 not needed.
+//  1. ivf_tier_pass_a: per pair its k survivors of smallest lower bound (all of them when
+//     n <= k) marked 1;
+//  2. (host: read the marked rows) ivf_tier_pass_b: their exact distances into sdist, the
+//     pair's k-th of them kd, and every other survivor whose lower bound is not above kd
+//     (NaN always) marked 2 — strictly worse ones cannot be in the list's top-k;
+//  3. (host: read those rows) ivf_tier_finish: their exact distances, then the pair's exact
+//     top-k over both marks, written as its only partial.
+// ============================================================================
+__device__ __forceinline__ void select_k_smallest_lb(const float* __restrict__ lbp, uint32_t n, int k, float& sk,
+                                                     uint64_t& si) {
+    WaveTopK<1> sel;
+    sel.init();
+    sk = __builtin_inff();
+    si = kNoId;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + (uint32_t)lane_id();
+        const bool act = i < n;
+        const float lb = act ? lbp[i] : __builtin_inff();
+        const float lk = lb == lb ? lb : -__builtin_inff();
+        offer_lanes<1>(sel, act && key_less(lk, i, sk, si), lk, (uint64_t)i, k, sk, si);
+    }
+}
+
+__global__ __launch_bounds__(256) void ivf_tier_pass_a(ScanArgs a, const uint32_t* __restrict__ soff,
+                                                       const uint32_t* __restrict__ scnt, const float* __restrict__ slb,
+                                                       uint8_t* __restrict__ mark) {
+    const int lane = lane_id();
+    const uint32_t nvalid = a.counters[kCtrValid];
+    const int k = (int)a.k;
+    for (uint32_t s = blockIdx.x * 4 + wave_index(); s < nvalid; s += gridDim.x * 4) {
+        const uint32_t n = scnt[s], o = soff[s];
+        if (n <= (uint32_t)k) {
+            if ((uint32_t)lane < n) mark[o + lane] = 1;
+            continue;
+        }
+        float sk;
+        uint64_t si;
+        select_k_smallest_lb(slb + o, n, k, sk, si);
+        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+            const uint32_t i = i0 + (uint32_t)lane;
+            if (i >= n) continue;
+            const float lb = slb[o + i];
+            const float lk = lb == lb ? lb : -__builtin_inff();
+            mark[o + i] = key_less(sk, si, lk, (uint64_t)i) ? 0 : 1;  // (lk, i) <= the k-th key: pass A
+        }
+    }
+}
+
+// exact distances of the pair's survivors marked `want`, from the compact fetched rows
+template <int M>
+__device__ __forceinline__ void tier_exact_marked(const ScanArgs& a, uint32_t o, uint32_t n, uint8_t want,
+                                                  const uint8_t* __restrict__ mark, const uint32_t* __restrict__ rowmap,
+                                                  const float4* __restrict__ rows, const float4* __restrict__ qr,
+                                                  float* __restrict__ sdist) {
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + (uint32_t)lane_id();
+        const bool act = i < n && mark[o + i] == want;
+        const uint64_t m = __ballot(act);
+        if (!m) continue;
+        const int first = __ffsll((long long)m) - 1;
+        const uint32_t ie = act ? i : (uint32_t)__builtin_amdgcn_readlane((int)i, first);
+        const float dist = lane_row_dist<M>(rows + (uint64_t)rowmap[o + ie] * a.d4, qr, a.d4);
+        if (act) sdist[o + i] = dist;
+    }
+}
+
+template <int M>
+__global__ __launch_bounds__(256) void ivf_tier_pass_b(ScanArgs a, const uint32_t* __restrict__ soff,
+                                                       const uint32_t* __restrict__ scnt, const uint2* __restrict__ surv,
+                                                       const float* __restrict__ slb, uint8_t* __restrict__ mark,
+                                                       const uint32_t* __restrict__ rowmap, const float* __restrict__ fetched,
+                                                       float* __restrict__ sdist) {
+    const int lane = lane_id();
+    const uint32_t nvalid = a.counters[kCtrValid];
+    const int k = (int)a.k;
+    for (uint32_t s = blockIdx.x * 4 + wave_index(); s < nvalid; s += gridDim.x * 4) {
+        const uint32_t n = scnt[s], o = soff[s];
+        const float4* qr = (const float4*)(a.qpad + (size_t)(a.sorted_pair[s] >> 16) * a.dp);
+        tier_exact_marked<M>(a, o, n, 1, mark, rowmap, (const float4*)fetched, qr, sdist);
+        if (n <= (uint32_t)k) continue;  // (every survivor was in pass A)
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        WaveTopK<1> tk;
+        tk.init();
+        float kd = __builtin_inff();
+        uint64_t ki = kNoId;
+        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+            const uint32_t i = i0 + (uint32_t)lane;
+            const bool act = i < n && mark[o + i] == 1;
+            const float d = act ? sdist[o + i] : __builtin_inff();
+            const uint64_t id = act ? a.ids[surv[o + i].x] : kNoId;
+            offer_lanes<1>(tk, act && key_less(d, id, kd, ki), d, id, k, kd, ki);
+        }
+        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+            const uint32_t i = i0 + (uint32_t)lane;
+            if (i < n && mark[o + i] == 0 && !(slb[o + i] > kd)) mark[o + i] = 2;
+        }
+    }
+}
+
+template <int M>
+__global__ __launch_bounds__(256) void ivf_tier_finish(ScanArgs a, uint32_t* __restrict__ nseg_qp,
+                                                       const uint32_t* __restrict__ soff, const uint32_t* __restrict__ scnt,
+                                                       const uint2* __restrict__ surv, const uint8_t* __restrict__ mark,
+                                                       const uint32_t* __restrict__ rowmap, const float* __restrict__ fetched,
+                                                       float* __restrict__ sdist) {
+    const int lane = lane_id();
+    const uint32_t nvalid = a.counters[kCtrValid];
+    const int k = (int)a.k;
+    unsigned long long rechecked = 0;
+    for (uint32_t s = blockIdx.x * 4 + wave_index(); s < nvalid; s += gridDim.x * 4) {
+        const uint32_t pr = a.sorted_pair[s];
+        const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
+        const uint32_t n = scnt[s], o = soff[s];
+        const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
+        if (n > (uint32_t)k) tier_exact_marked<M>(a, o, n, 2, mark, rowmap, (const float4*)fetched, qr, sdist);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        WaveTopK<1> tk;
+        tk.init();
+        float kd = __builtin_inff();
+        uint64_t ki = kNoId;
+        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+            const uint32_t i = i0 + (uint32_t)lane;
+            const bool act = i < n && mark[o + i] != 0;
+            const float d = act ? sdist[o + i] : __builtin_inff();
+            const uint64_t id = act ? a.ids[surv[o + i].x] : kNoId;
+            offer_lanes<1>(tk, act && key_less(d, id, kd, ki), d, id, k, kd, ki);
+            rechecked += (unsigned long long)__popcll(__ballot(act));
+        }
+        const uint32_t part = a.part_base_sorted[s];
+        if (lane < k) {
+            a.part_d[(size_t)part * k + lane] = tk.d[0];
+            a.part_i[(size_t)part * k + lane] = tk.id[0];
+        }
+        if (lane == 0) nseg_qp[(size_t)q * a.P + p] = 1u;
+    }
+    if (a.mstats && lane == 0 && rechecked) atomicAdd(&a.mstats[2], rechecked);
+}
+
+void launch_tier_recheck(int phase, int metric, const ScanArgs& a, uint32_t BP, uint32_t* nseg_qp, const uint32_t* soff,
+                         const uint32_t* scnt, const uint2* surv, const float* slb, uint8_t* mark, const uint32_t* rowmap,
+                         const float* fetched, float* sdist, hipStream_t s) {
+    if (!BP) return;
+    const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(2048, (BP + 3) / 4));
+    if (phase == 0) {
+        ivf_tier_pass_a<<<g, 256, 0, s>>>(a, soff, scnt, slb, mark);
+    } else if (phase == 1) {
+        if (metric == kL2) ivf_tier_pass_b<kL2><<<g, 256, 0, s>>>(a, soff, scnt, surv, slb, mark, rowmap, fetched, sdist);
+        else ivf_tier_pass_b<kIP><<<g, 256, 0, s>>>(a, soff, scnt, surv, slb, mark, rowmap, fetched, sdist);
+    } else {
+        if (metric == kL2) ivf_tier_finish<kL2><<<g, 256, 0, s>>>(a, nseg_qp, soff, scnt, surv, mark, rowmap, fetched, sdist);
+        else ivf_tier_finish<kIP><<<g, 256, 0, s>>>(a, nseg_qp, soff, scnt, surv, mark, rowmap, fetched, sdist);
+    }
+}
+
 }  // namespace vdbk

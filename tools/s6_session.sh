@@ -1,0 +1,77 @@
+#!/bin/bash
+# Round-6 GPU sessions (run via gpurun from the repo root), one parametrised recipe:
+#   bash tools/s6_session.sh <tag> <step,step,...>
+#   prof8     rocprofv3 kernel trace of the 1/8-shard rehearsal (headline index, rank 0 of 8), one in flight
+#   prof3     the same for the headline, one and two in flight
+#   tier      configs[4] shape: cfg4 rank 0 of 5 as a shard file through the screened tier at
+#             TIER_GIB (default 11.5 = 0.2 of the lists), two-pass vs one-pass re-check, refill
+#   probe     the disk's random-read ceiling (tools/rand_read_probe.cpp)
+#   ranks3    every rank of the 8-GPU headline, a process each, emulated 8-record exchange
+#   ranks4    the same for configs[3]
+#   tests     pytest -m gpu (PYTEST_K: -k filter)
+#   bench     the default bench line
+set -o pipefail
+TAG=$1; STEPS=$2
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$R" || exit 1
+export TMPDIR=/tmp
+has() { [[ ",$STEPS," == *",$1,"* ]]; }
+run() {  # run <name> <seconds> <cmd...>: stop at the first failure
+    local name=$1 secs=$2
+    shift 2
+    echo "[$(date +%T)] $name: $*"
+    timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1
+    local rc=$?
+    echo "[$(date +%T)] $name rc=$rc"
+    if [ $rc -ne 0 ]; then tail -30 "$O/$name.log"; exit $rc; fi
+}
+if has tests; then
+    run pytest 1100 python -u -m pytest tests -m gpu -x -v --durations=25 --timeout 600 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
+    tail -3 "$O/pytest.log"
+fi
+if has prof8; then
+    run prof8 400 rocprofv3 --kernel-trace --stats -d "$O/prof8" -o k -f csv -- python3 bench.py --emulate-shard 8 --inflight 1 --steps 30 --warmup 3 --no-cpu --latency-batches 0 --prof-steps 5
+    find "$O/prof8" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_emu8.csv" \;
+    cut -d, -f1-4 "$O/kernel_stats_emu8.csv" | cut -c1-150 | head -24
+fi
+if has prof3; then
+    for inf in 1 2; do
+        run prof3_$inf 400 rocprofv3 --kernel-trace --stats -d "$O/prof3_$inf" -o k -f csv -- python3 bench.py --inflight $inf --steps 30 --warmup 3 --no-cpu --latency-batches 0 --prof-steps 5
+        find "$O/prof3_$inf" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_inflight$inf.csv" \;
+        cut -d, -f1-4 "$O/kernel_stats_inflight$inf.csv" | cut -c1-150 | head -16
+    done
+fi
+if has probe; then
+    g++ -O2 -std=c++17 -o /tmp/rand_read_probe tools/rand_read_probe.cpp || exit 1
+    run probe 300 /tmp/rand_read_probe /tmp 24 256 5
+    cat "$O/probe.log"
+fi
+if has tier; then
+    c=${TIER_GIB:-11.5}
+    run tier 1150 python3 -u bench.py --cfg cfg4 --emulate-shard 5 --steps 20 --warmup 2 --no-cpu --latency-batches 0 --prof-steps 3 \
+        --tier-cache-gib $c --tier-call 512 --tier-calls 4 --tier-variant screen_recheck2=0 --tier-adapt 4096
+    grep '^{' "$O/tier.log" > "$O/tier.json"
+    python3 -c "
+import json; d=json.load(open('$O/tier.json')); t=d['tier']
+print('cache', t['cache_gib'], t['cache_fraction_of_lists'], 'QPS', t['value'], 'rows read', t['survivor_rows_per_batch'], 'cached', t['survivor_rows_from_hbm_cache_per_batch'], 'amp', t.get('read_amplification'), 'gbps', t['file_read_gbps'], 'parity', t['parity_with_resident_index'])
+for v in t.get('variants', []): print('   ', v)
+print('resident', d['value'], d['ms_per_step'])"
+fi
+if has ranks3; then
+    run ranks3 900 python -u bench.py --cfg cfg3 --emulate-rank all --emulate-shard 8 --inflight 3 --no-cpu
+    grep '^{' "$O/ranks3.log" > "$O/ranks3.json"
+    cut -c 1-600 "$O/ranks3.json"
+fi
+if has ranks4; then
+    run ranks4 1100 python -u bench.py --cfg cfg4 --emulate-rank all --emulate-shard 8 --inflight 3 --no-cpu
+    grep '^{' "$O/ranks4.log" > "$O/ranks4.json"
+    cut -c 1-600 "$O/ranks4.json"
+fi
+if has bench; then
+    run bench 600 python -u bench.py ${BENCH_ARGS}
+    grep '^{' "$O/bench.log" > "$O/bench.json"
+    cut -c 1-400 "$O/bench.json"
+fi
+echo "session $TAG done"
