@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <stdexcept>
+#include <type_traits>
 
 #include "kernels.hpp"
 #include "scan_common.hpp"
@@ -19,6 +20,9 @@ namespace vdbk {
 
 // One wave per valid sorted pair: the k-th smallest of the union of its contributed upper-
 // bound lists (k vectors of the list have exact distances at or below it) lowers a.thr.
+// (Latency-bound: the contributions are read four 64-element chunks at a time, all loads in
+// flight together, and only values below the running k-th are inserted — a wave top-k keyed
+// (value, element) — instead of sorting and merging every chunk.)
 __global__ __launch_bounds__(256) void ivf_screen_tfinal(ScanArgs a) {
     const int lane = lane_id();
     const uint32_t nvalid = a.counters[kCtrValid];
@@ -27,16 +31,24 @@ __global__ __launch_bounds__(256) void ivf_screen_tfinal(ScanArgs a) {
         const uint32_t nl = min(a.ubcnt[s], (uint32_t)kUbLists);
         const uint32_t n = nl * (uint32_t)k;
         const float* src = a.ublist + (size_t)s * kUbLists * k;
-        float best = __builtin_inff();  // the 64 smallest so far, ascending over lanes
-        uint64_t bid = kNoId;
-        for (uint32_t e0 = 0; e0 < n; e0 += 64) {
-            float d = e0 + lane < n ? src[e0 + lane] : __builtin_inff();
-            uint64_t id = kNoId;
-            bitonic_sort64(d, id);
-            bitonic_merge64(best, bid, d, id);
+        WaveTopK<1> tk;
+        tk.init();
+        float kd = __builtin_inff();
+        uint64_t ki = kNoId;
+        for (uint32_t e0 = 0; e0 < n; e0 += 4 * 64) {
+            float d[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t e = e0 + 64 * u + (uint32_t)lane;
+                d[u] = e < n ? src[e] : __builtin_inff();
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t e = e0 + 64 * u + (uint32_t)lane;
+                offer_lanes<1>(tk, e < n && key_less(d[u], e, kd, ki), d[u], (uint64_t)e, k, kd, ki);
+            }
         }
-        const float kth = rd_lane(best, k - 1);
-        if (lane == 0 && kth < ord_dec(a.thr[s])) a.thr[s] = ord_enc(kth);
+        if (lane == 0 && kd < ord_dec(a.thr[s])) a.thr[s] = ord_enc(kd);
     }
 }
 
@@ -44,7 +56,10 @@ __global__ __launch_bounds__(256) void ivf_screen_tfinal(ScanArgs a) {
 // its rank among its pair's survivors into .w (~0: dropped). The collect kernel appends a
 // ballot's candidates in lane order, so consecutive entries come in runs of one pair (up to
 // 16): each wave takes 64 consecutive entries and does one atomic per run (segmented by equal
-// pairs across its lanes) instead of one per survivor on the pair's counter.
+// pairs across its lanes) instead of one per survivor on the pair's counter. (Latency-bound:
+// each wave takes kFilterU 64-entry chunks a grid pass apart at once, every load of one kind
+// in flight together: the entries, then their thresholds, then the run atomics.)
+constexpr int kFilterU = 4;
 __global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ cand, const uint32_t* __restrict__ counters,
                                                          uint32_t cap, const uint32_t* __restrict__ thr,
                                                          const uint32_t* __restrict__ thr4,
@@ -52,30 +67,52 @@ __global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ can
     const uint32_t n = min(counters[kCtrCand], cap);
     const int lane = lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
-    for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; i0 < n; i0 += gridDim.x * blockDim.x) {
-        const uint32_t i = i0 + (uint32_t)lane;
-        const uint4 c = i < n ? cand[i] : make_uint4(~0u, 0u, 0u, ~0u);
-        const bool act = c.x != ~0u;  // (sentinel: the padding of a collect wave's candidate chunk)
-        const uint32_t sp = c.x;
-        bool keep = false;
-        if (act) {
-            const uint4 t4 = *(const uint4*)(thr4 + (size_t)sp * 4);
-            const float T = fminf(ord_dec(thr[sp]),
-                                  fmaxf(fmaxf(ord_dec(t4.x), ord_dec(t4.y)), fmaxf(ord_dec(t4.z), ord_dec(t4.w))));
-            keep = !ovf[sp] && !(__uint_as_float(c.z) > T);
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; i0 < n; i0 += kFilterU * stride) {
+        uint4 c[kFilterU];
+#pragma unroll
+        for (int u = 0; u < kFilterU; ++u) {
+            const uint32_t i = i0 + u * stride + (uint32_t)lane;
+            c[u] = i < n ? cand[i] : make_uint4(~0u, 0u, 0u, ~0u);
         }
-        // runs of equal pairs: a run starts where the previous lane's pair differs
-        const uint32_t prev = __shfl_up(sp, 1);
-        const uint64_t heads = __ballot(lane == 0 || prev != sp);
-        const uint64_t keeps = __ballot(keep);
-        const int start = 63 - __builtin_clzll(heads & (below | (1ull << lane)));  // this lane's run start
-        const uint64_t after = heads & ~(below | (1ull << lane));                   // later run starts
-        const int end = after ? __builtin_ctzll(after) - 1 : 63;                     // this lane's run end
-        const uint64_t run = (end == 63 ? ~0ull : ((1ull << (end + 1)) - 1ull)) & ~((1ull << start) - 1ull);
-        uint32_t base = 0;
-        if (lane == end && act && (keeps & run)) base = atomicAdd(&scnt[sp], (uint32_t)__popcll(keeps & run));
-        base = __shfl(base, end);
-        if (act) cand[i].w = keep ? base + (uint32_t)__popcll(keeps & run & below) : ~0u;
+        uint4 t4[kFilterU];
+        uint32_t tg[kFilterU], ov[kFilterU];
+#pragma unroll
+        for (int u = 0; u < kFilterU; ++u) {
+            const bool act = c[u].x != ~0u;  // (sentinel: the padding of a collect wave's candidate chunk)
+            const uint32_t sp = act ? c[u].x : 0u;
+            t4[u] = act ? *(const uint4*)(thr4 + (size_t)sp * 4) : make_uint4(0u, 0u, 0u, 0u);
+            tg[u] = act ? thr[sp] : 0u;
+            ov[u] = act ? ovf[sp] : 1u;
+        }
+        uint32_t base[kFilterU];
+        bool keep[kFilterU];
+        uint64_t runm[kFilterU], keeps[kFilterU];
+        int endl[kFilterU];
+#pragma unroll
+        for (int u = 0; u < kFilterU; ++u) {
+            const bool act = c[u].x != ~0u;
+            const uint32_t sp = c[u].x;
+            const float T = fminf(ord_dec(tg[u]), fmaxf(fmaxf(ord_dec(t4[u].x), ord_dec(t4[u].y)),
+                                                         fmaxf(ord_dec(t4[u].z), ord_dec(t4[u].w))));
+            keep[u] = act && !ov[u] && !(__uint_as_float(c[u].z) > T);
+            // runs of equal pairs: a run starts where the previous lane's pair differs
+            const uint32_t prev = __shfl_up(sp, 1);
+            const uint64_t heads = __ballot(lane == 0 || prev != sp);
+            keeps[u] = __ballot(keep[u]);
+            const int start = 63 - __builtin_clzll(heads & (below | (1ull << lane)));  // this lane's run start
+            const uint64_t after = heads & ~(below | (1ull << lane));                   // later run starts
+            endl[u] = after ? __builtin_ctzll(after) - 1 : 63;                           // this lane's run end
+            runm[u] = (endl[u] == 63 ? ~0ull : ((1ull << (endl[u] + 1)) - 1ull)) & ~((1ull << start) - 1ull);
+            base[u] = 0;
+            if (lane == endl[u] && act && (keeps[u] & runm[u])) base[u] = atomicAdd(&scnt[sp], (uint32_t)__popcll(keeps[u] & runm[u]));
+        }
+#pragma unroll
+        for (int u = 0; u < kFilterU; ++u) {
+            const uint32_t bs = __shfl(base[u], endl[u]);
+            const uint32_t i = i0 + u * stride + (uint32_t)lane;
+            if (c[u].x != ~0u && i < n) cand[i].w = keep[u] ? bs + (uint32_t)__popcll(keeps[u] & runm[u] & below) : ~0u;
+        }
     }
 }
 
@@ -418,8 +455,29 @@ __device__ __forceinline__ float lane_row_dist(const float4* __restrict__ xr, co
 // same. Re-checks at the headline: ~37 per pair instead of ~110 (a CPU model of the int8
 // bound; the bench reports the measured count). Overflowed pairs: ivf_screen_pair_topk's
 // recomputation over their planned segments, unchanged.
+// The same sum with the query row read from LDS (one pair per wave: every lane has the same
+// query) and KP float4 of the lane's row in flight: twice the loads in flight per lane of
+// lane_row_dist for the same registers, so a round of re-checks costs half the round trips.
+template <int M, int KP>
+__device__ __forceinline__ float lane_row_dist_lq(const float4* __restrict__ xr, const float4* ql, uint32_t d4) {
+    float4 xb[KP];
+#pragma unroll
+    for (int p = 0; p < KP; ++p) xb[p] = xr[p];
+    float acc = 0.0f;
+    for (uint32_t t0 = 0; t0 < d4; t0 += KP) {
+        const bool more = t0 + KP < d4;  // (wave-uniform)
+#pragma unroll
+        for (int p = 0; p < KP; ++p) {
+            acc = acc4<M>(acc, ql[t0 + p], xb[p]);
+            if (more) xb[p] = xr[t0 + KP + p];
+        }
+    }
+    return dist_finish<M>(acc);
+}
+
 constexpr uint32_t kR2Ring = 128;
-template <int M>
+constexpr uint32_t kR2MaxD4 = 512;  // (query rows staged in LDS up to 2048 dims: 32 KB; wider: from global memory)
+template <int M, int KP>
 __global__ __launch_bounds__(256) void ivf_screen_recheck2(ScanArgs a, const uint32_t* __restrict__ probes,
                                                            uint32_t* __restrict__ nseg_qp,
                                                            const uint32_t* __restrict__ soff,
@@ -428,9 +486,11 @@ __global__ __launch_bounds__(256) void ivf_screen_recheck2(ScanArgs a, const uin
                                                            const float* __restrict__ slb,
                                                            const uint32_t* __restrict__ ovf, uint32_t smax) {
     __shared__ uint32_t s_ring[4][kR2Ring];
+    extern __shared__ __attribute__((aligned(16))) float4 s_qrow[];  // (KP > 0: per wave its pair's query row)
     const int lane = lane_id();
     const uint32_t wl = wave_index();
     uint32_t* ring = s_ring[wl];
+    float4* ql = s_qrow + (size_t)wl * a.d4;
     const uint32_t nvalid = a.counters[kCtrValid];
     const int k = (int)a.k;
     const uint32_t d4 = a.d4;
@@ -443,31 +503,32 @@ __global__ __launch_bounds__(256) void ivf_screen_recheck2(ScanArgs a, const uin
         const uint32_t q = pr >> 16, p = pr & 0xFFFFu;
         const uint32_t n = scnt[s], o = soff[s];
         const float4* qr = (const float4*)(a.qpad + (size_t)q * a.dp);
+        if constexpr (KP > 0) {  // (the previous pair's reads of the row are done: in order within the wave)
+            for (uint32_t t = (uint32_t)lane; t < d4; t += 64) ql[t] = qr[t];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         WaveTopK<1> tk;
         tk.init();
         float kd = __builtin_inff();
         uint64_t ki = kNoId;
-        // one round: survivor o + idx per active lane (inactive lanes read the first active
-        // lane's row: no extra traffic, every load unconditional)
-        auto round = [&](bool act, uint32_t idx) {
-            const uint64_t m = __ballot(act);
-            if (!m) return;
-            const int first = __ffsll((long long)m) - 1;
-            const uint32_t ie = act ? idx : (uint32_t)__builtin_amdgcn_readlane((int)idx, first);
-            const uint64_t slot = surv[o + ie].x;
-            const float dist = lane_row_dist<M>(rows + slot * d4, qr, d4);
-            const uint64_t id = a.ids[slot];
-            offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
-            rechecked += (unsigned long long)__popcll(m);
-        };
+        // Every round of re-checks goes through the wave's LDS ring and ONE call site (the
+        // row-stream registers are allocated once): pass A's entries (all n when n <= k) are
+        // queued first; then the scan of the others (pass B) queues those not above the
+        // current k-th, and a round runs whenever 64 are queued or the scan is done. Each
+        // entry is tested again against the k-th when its round starts (pass A's: kd is +inf).
+        uint32_t head = 0, tail = 0;  // (wave-uniform ring cursors)
+        float sk = __builtin_inff();
+        uint64_t si = kNoId;
+        uint32_t scan = n;  // (pass B's next survivor; n: no pass B)
         if (n <= (uint32_t)k) {
-            round((uint32_t)lane < n, (uint32_t)lane);
+            if ((uint32_t)lane < n) ring[lane] = (uint32_t)lane;
+            tail = n;
         } else {
             // pass A: the k smallest keys (lb, index); NaN bounds first
             WaveTopK<1> sel;
             sel.init();
-            float sk = __builtin_inff();
-            uint64_t si = kNoId;
             for (uint32_t i0 = 0; i0 < n; i0 += 64) {
                 const uint32_t i = i0 + (uint32_t)lane;
                 const bool act = i < n;
@@ -475,18 +536,14 @@ __global__ __launch_bounds__(256) void ivf_screen_recheck2(ScanArgs a, const uin
                 const float lk = lb == lb ? lb : -__builtin_inff();
                 offer_lanes<1>(sel, act && key_less(lk, i, sk, si), lk, (uint64_t)i, k, sk, si);
             }
-            round(lane < k, (uint32_t)sel.id[0]);
-            // pass B: the others not above the current k-th exact distance
-            uint32_t head = 0, tail = 0;  // (wave-uniform ring cursors)
-            auto drain = [&](uint32_t cnt) {
-                const bool in = (uint32_t)lane < cnt;
-                const uint32_t idx = ring[(head + (in ? (uint32_t)lane : 0u)) & (kR2Ring - 1)];
-                head += cnt;
-                const float lb = slb[o + idx];
-                round(in && !(lb > kd), idx);
-            };
-            for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-                const uint32_t i = i0 + (uint32_t)lane;
+            if (lane < k) ring[lane] = (uint32_t)sel.id[0];
+            tail = (uint32_t)k;
+            scan = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (;;) {
+            if (scan < n && tail - head < 64 && head != 0) {  // (pass B scans after pass A's round)
+                const uint32_t i = scan + (uint32_t)lane;
                 const bool act = i < n;
                 const float lb = act ? slb[o + i] : __builtin_inff();
                 const float lk = lb == lb ? lb : -__builtin_inff();
@@ -497,10 +554,29 @@ __global__ __launch_bounds__(256) void ivf_screen_recheck2(ScanArgs a, const uin
                     ring[(tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))) &
                          (kR2Ring - 1)] = i;
                 tail += (uint32_t)__popcll(m);
+                scan += 64;
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                if (tail - head >= 64) drain(64u);
+                continue;
             }
-            if (tail != head) drain(tail - head);
+            if (tail == head) break;
+            // one round: up to 64 queued survivors, one lane each (inactive lanes read the first
+            // active lane's row: no extra traffic, every load unconditional)
+            const uint32_t cnt = min(64u, tail - head);
+            const bool in = (uint32_t)lane < cnt;
+            const uint32_t idx = ring[(head + (in ? (uint32_t)lane : 0u)) & (kR2Ring - 1)];
+            head += cnt;
+            const bool act = in && !(slb[o + idx] > kd);
+            const uint64_t m = __ballot(act);
+            if (!m) continue;
+            const int first = __ffsll((long long)m) - 1;
+            const uint32_t ie = act ? idx : (uint32_t)__builtin_amdgcn_readlane((int)idx, first);
+            const uint64_t slot = surv[o + ie].x;
+            float dist;
+            if constexpr (KP > 0) dist = lane_row_dist_lq<M, KP>(rows + slot * d4, ql, d4);
+            else dist = lane_row_dist<M>(rows + slot * d4, qr, d4);
+            const uint64_t id = a.ids[slot];
+            offer_lanes<1>(tk, act && key_less(dist, id, kd, ki), dist, id, k, kd, ki);
+            rechecked += (unsigned long long)__popcll(m);
         }
         // the pair's exact top-k is its only partial: the merge reads the first of its segments
         const uint32_t part = a.part_base_sorted[s];
@@ -586,8 +662,20 @@ void launch_screen_recheck(int metric, const ScanArgs& a, uint32_t BP, const uin
     if (!BP) return;
     if (slb && !fetched && a.rows) {  // the two-pass re-check (rows in HBM)
         const uint32_t gp = std::max<uint32_t>(512, std::min<uint32_t>(2048, (BP + 3) / 4));
-        if (metric == kL2) ivf_screen_recheck2<kL2><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, slb, ovf, smax);
-        else ivf_screen_recheck2<kIP><<<gp, 256, 0, s>>>(a, probes, nseg_qp, soff, scnt, surv, slb, ovf, smax);
+        // (the pair's query row in LDS, 16 float4 of each lane's row in flight: 220 VGPRs, two
+        // waves per SIMD; 32 in flight spilled)
+        const int kp = a.d4 <= kR2MaxD4 ? 16 : 0;
+        const size_t lds = kp ? (size_t)4 * a.d4 * sizeof(float4) : 0;
+        auto go = [&](auto m_c, auto kp_c) {
+            constexpr int Mm = decltype(m_c)::value, KPc = decltype(kp_c)::value;
+            ivf_screen_recheck2<Mm, KPc><<<gp, 256, lds, s>>>(a, probes, nseg_qp, soff, scnt, surv, slb, ovf, smax);
+        };
+        auto go_m = [&](auto m_c) {
+            if (kp == 16) go(m_c, std::integral_constant<int, 16>{});
+            else go(m_c, std::integral_constant<int, 0>{});
+        };
+        if (metric == kL2) go_m(std::integral_constant<int, kL2>{});
+        else go_m(std::integral_constant<int, kIP>{});
         return;
     }
     static const bool raised = [] {

@@ -69,6 +69,13 @@ if has ranks4; then
     grep '^{' "$O/ranks4.log" > "$O/ranks4.json"
     cut -c 1-600 "$O/ranks4.json"
 fi
+if has sweep; then
+    # one build, several option sets: tools/knob_sweep.py $SWEEP_WL $SWEEP_SETS
+    for wl in ${SWEEP_WL:-s8 cfg3}; do
+        run sweep_$wl 900 python -u tools/knob_sweep.py $wl $SWEEP_SETS
+        grep '^{' "$O/sweep_$wl.log" | cut -c1-330
+    done
+fi
 if has bench; then
     run bench 600 python -u bench.py ${BENCH_ARGS}
     grep '^{' "$O/bench.log" > "$O/bench.json"
