@@ -681,7 +681,10 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.inflight <= 0:
-        args.inflight = 3 if world > 1 else 2
+        # (3 batches in flight, one per workspace slot: round 6's two-pass re-check made the
+        # third batch pay at one GPU too — cfg3 1.448 vs 1.513 ms per step at 2, same box,
+        # profiles/r06_sweep_recheck2.jsonl; a batch's latency is then ~3 steps, p99 reported)
+        args.inflight = 3
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()  # (does not initialise the GPU)

@@ -844,8 +844,10 @@ __device__ __forceinline__ float row_elem(const float (&u)[4], int e) {
 // Candidate slots of one wave: a.cand entries are reserved in chunks of kCandChunk (one atomic
 // on the batch's counter per chunk), the next chunk's atomic issued one block ahead of its use,
 // so no block's epilogue waits on a returning global access (vmcnt is in order: it would wait
-// for the next block's shadow prefetches too). The unused rest of a chunk is filled with
-// sentinel entries {~0, 0, 0, ~0} (never kept by the filter).
+// for the next block's shadow prefetches too). A block's candidates fill the current chunk to
+// its end and continue in the next (round 6: round 5 padded the rest of a chunk whenever a
+// block's candidates did not fit, up to half the entries the filter then read); the wave's
+// unused rest at its end is filled with sentinel entries {~0, 0, 0, ~0} (never kept).
 // (kCandChunk: kernels.hpp.) Reserved slots (counters[kCtrCand]) therefore exceed the candidates
 // (counters[kCtrReal], added once per wave at its end): the overflow, floor, calibration and
 // re-run decisions read kCtrOvf / kCtrReal, never the reserved count.
@@ -1115,30 +1117,37 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
 #pragma unroll
                 for (int r = 0; r < 4; ++r) tot += (uint32_t)__popcll(__ballot(is_cand(vt, r)));
             if (tot) {
-                uint32_t base;
+                // the block's candidates take ranks 0 .. tot-1: the first n0 go to [b0, b0 + n0),
+                // the rest to [b1, ..): the current chunk is filled to its end and the next one
+                // continues it, so no entry is left unused except at a wave's very end
+                uint32_t b0, n0, b1 = 0;
                 if (tot <= cc.left) {
-                    base = cc.base;
+                    b0 = cc.base;
+                    n0 = tot;
                     cc.base += tot;
                     cc.left -= tot;
                 } else if (tot > kCandChunk) {  // (a range of its own; the current chunk stays)
                     uint32_t v = 0;
                     if (lane == 0) v = atomicAdd(a.ccount, tot);
-                    base = __builtin_amdgcn_readfirstlane(v);
-                } else {  // the rest of the current chunk padded; the chunk reserved ahead
-                    pad_cand(a, cc.base, cc.left);
+                    b0 = __builtin_amdgcn_readfirstlane(v);
+                    n0 = tot;
+                } else {  // the current chunk's rest, then the chunk reserved ahead
+                    b0 = cc.base;
+                    n0 = cc.left;
                     uint32_t v = 0;
                     if (cc.pending) {
-                        base = cc.next;
+                        b1 = cc.next;
                         cc.pending = false;
                     } else {
                         if (lane == 0) v = atomicAdd(a.ccount, kCandChunk);
-                        base = __builtin_amdgcn_readfirstlane(v);
+                        b1 = __builtin_amdgcn_readfirstlane(v);
                     }
-                    cc.base = base + tot;
-                    cc.left = kCandChunk - tot;
+                    cc.base = b1 + (tot - n0);
+                    cc.left = kCandChunk - (tot - n0);
                 }
                 collected += tot;
                 cc.real += tot;
+                uint32_t rank = 0;
 #pragma unroll
                 for (int vt = 0; vt < 4; ++vt) {
 #pragma unroll
@@ -1146,8 +1155,9 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                         const bool c = is_cand(vt, r);
                         const uint64_t mm = __ballot(c);
                         if (c) {
-                            const uint32_t idx = base + __builtin_amdgcn_mbcnt_hi(
-                                                            (uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+                            const uint32_t rk = rank + __builtin_amdgcn_mbcnt_hi(
+                                                           (uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+                            const uint32_t idx = rk < n0 ? b0 + rk : b1 + (rk - n0);
                             const uint32_t spi = it.pair_start + q0 + g0 + 4 * (lane >> 4) + r;
                             const uint32_t slot = (uint32_t)((b0 + j) * 64 + 16 * vt + (lane & 15));
                             if (idx < a.cand_cap)
@@ -1157,7 +1167,7 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                                 a.ccount[kCtrOvf - kCtrCand] = 1u;
                             }
                         }
-                        base += (uint32_t)__popcll(mm);
+                        rank += (uint32_t)__popcll(mm);
                     }
                 }
             }

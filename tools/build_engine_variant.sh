@@ -12,7 +12,7 @@ mkdir -p "$O"
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wall -I$R/include"
 /opt/rocm/bin/hipcc $F "$@" -DVDB_BUILD_ID='"variant"' -c "$P/csrc/engine.cpp" -o "$O/engine.o"
 /opt/rocm/bin/hipcc $F "$@" -c "$P/csrc/group.cpp" -o "$O/group.o"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libvdb_ivf.so" "$P/build/kernels.o" "$P/build/screen.o" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libvdb_ivf.so" "$P/build/kernels.o" "$P/build/screen.o" "$P/build/screen_post.o" \
     "$O/engine.o" "$O/group.o" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f "$O/engine.o" "$O/group.o"
 echo "$O/libvdb_ivf.so"

@@ -36,6 +36,11 @@ if has prof8; then
     find "$O/prof8" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_emu8.csv" \;
     cut -d, -f1-4 "$O/kernel_stats_emu8.csv" | cut -c1-150 | head -24
 fi
+if has trace8; then
+    # the 1/8 shard at 3 in flight under a kernel trace: the timed region's timeline (tools/timeline.py)
+    run trace8 400 rocprofv3 --kernel-trace -d "$O/trace8" -o k -f csv -- python3 bench.py --emulate-shard 8 --inflight 3 --steps 100 --warmup 5 --no-cpu --latency-batches 0 --prof-steps 2
+    python3 tools/timeline.py "$(find "$O/trace8" -name '*kernel_trace.csv' | head -1)" 100 > "$O/timeline8.json" && cut -c1-1500 "$O/timeline8.json"
+fi
 if has prof3; then
     for inf in 1 2; do
         run prof3_$inf 400 rocprofv3 --kernel-trace --stats -d "$O/prof3_$inf" -o k -f csv -- python3 bench.py --inflight $inf --steps 30 --warmup 3 --no-cpu --latency-batches 0 --prof-steps 5
