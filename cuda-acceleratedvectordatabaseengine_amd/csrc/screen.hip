@@ -1117,33 +1117,33 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
 #pragma unroll
                 for (int r = 0; r < 4; ++r) tot += (uint32_t)__popcll(__ballot(is_cand(vt, r)));
             if (tot) {
-                // the block's candidates take ranks 0 .. tot-1: the first n0 go to [b0, b0 + n0),
-                // the rest to [b1, ..): the current chunk is filled to its end and the next one
+                // the block's candidates take ranks 0 .. tot-1: the first cn0 go to [cb0, cb0 + cn0),
+                // the rest to [cb1, ..): the current chunk is filled to its end and the next one
                 // continues it, so no entry is left unused except at a wave's very end
-                uint32_t b0, n0, b1 = 0;
+                uint32_t cb0, cn0, cb1 = 0;  // (cb0: not the segment's first block b0)
                 if (tot <= cc.left) {
-                    b0 = cc.base;
-                    n0 = tot;
+                    cb0 = cc.base;
+                    cn0 = tot;
                     cc.base += tot;
                     cc.left -= tot;
                 } else if (tot > kCandChunk) {  // (a range of its own; the current chunk stays)
                     uint32_t v = 0;
                     if (lane == 0) v = atomicAdd(a.ccount, tot);
-                    b0 = __builtin_amdgcn_readfirstlane(v);
-                    n0 = tot;
+                    cb0 = __builtin_amdgcn_readfirstlane(v);
+                    cn0 = tot;
                 } else {  // the current chunk's rest, then the chunk reserved ahead
-                    b0 = cc.base;
-                    n0 = cc.left;
+                    cb0 = cc.base;
+                    cn0 = cc.left;
                     uint32_t v = 0;
                     if (cc.pending) {
-                        b1 = cc.next;
+                        cb1 = cc.next;
                         cc.pending = false;
                     } else {
                         if (lane == 0) v = atomicAdd(a.ccount, kCandChunk);
-                        b1 = __builtin_amdgcn_readfirstlane(v);
+                        cb1 = __builtin_amdgcn_readfirstlane(v);
                     }
-                    cc.base = b1 + (tot - n0);
-                    cc.left = kCandChunk - (tot - n0);
+                    cc.base = cb1 + (tot - cn0);
+                    cc.left = kCandChunk - (tot - cn0);
                 }
                 collected += tot;
                 cc.real += tot;
@@ -1157,7 +1157,7 @@ __device__ __forceinline__ void collect_segment(const ScanArgs& a, const ScanIte
                         if (c) {
                             const uint32_t rk = rank + __builtin_amdgcn_mbcnt_hi(
                                                            (uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
-                            const uint32_t idx = rk < n0 ? b0 + rk : b1 + (rk - n0);
+                            const uint32_t idx = rk < cn0 ? cb0 + rk : cb1 + (rk - cn0);
                             const uint32_t spi = it.pair_start + q0 + g0 + 4 * (lane >> 4) + r;
                             const uint32_t slot = (uint32_t)((b0 + j) * 64 + 16 * vt + (lane & 15));
                             if (idx < a.cand_cap)
