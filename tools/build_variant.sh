@@ -11,7 +11,7 @@ O=$R/_variants/$N
 mkdir -p "$O"
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wall -I$R/include"
 /opt/rocm/bin/hipcc $F "$@" -c "${SRC:-$P/csrc/kernels.hip}" -I"$P/csrc" -o "$O/kernels.o"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libvdb_ivf.so" "$O/kernels.o" "$P/build/engine.o" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libvdb_ivf.so" "$O/kernels.o" "$P/build/screen.o" "$P/build/screen_post.o" "$P/build/engine.o" \
     "$P/build/group.o" -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -f "$O/kernels.o"
 echo "$O/libvdb_ivf.so"

@@ -1,6 +1,12 @@
 #!/bin/bash
-# Round-6 GPU sessions (run via gpurun from the repo root), one parametrised recipe:
-#   bash tools/s6_session.sh <tag> <step,step,...>
+# GPU sessions (run via gpurun from the repo root), one parametrised recipe for every
+# measurement of round 6 (profiles/INDEX.md names the tag and steps behind each record):
+#   bash tools/session.sh <tag> <step,step,...>
+#   smoke     __graft_entry__.smoke()
+#   multi     the two-rank rehearsal of the N-rank path on one GPU (bench.py --gpus 2)
+#   grpc      the gRPC front end under load (tools/grpc_load.py)
+#   sweep     tools/knob_sweep.py $SWEEP_WL (default "s8 cfg3") over $SWEEP_SETS (engine option sets)
+#   trace8    the 1/8 shard at 3 in flight under a kernel trace, its timeline (tools/timeline.py)
 #   prof8     rocprofv3 kernel trace of the 1/8-shard rehearsal (headline index, rank 0 of 8), one in flight
 #   prof3     the same for the headline, one and two in flight
 #   tier      configs[4] shape: cfg4 rank 0 of 5 as a shard file through the screened tier at
@@ -30,6 +36,20 @@ run() {  # run <name> <seconds> <cmd...>: stop at the first failure
 if has tests; then
     run pytest 1100 python -u -m pytest tests -m gpu -x -v --durations=25 --timeout 600 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
     tail -3 "$O/pytest.log"
+fi
+if has smoke; then
+    run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+    tail -2 "$O/smoke.log"
+fi
+if has multi; then
+    run multi 600 python -u bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu --prof-steps 4
+    grep '^{' "$O/multi.log" > "$O/multi.json"
+    cut -c 1-400 "$O/multi.json"
+fi
+if has grpc; then
+    run grpc 600 python -u tools/grpc_load.py
+    grep '^{' "$O/grpc.log" > "$O/grpc.json"
+    cat "$O/grpc.json"
 fi
 if has prof8; then
     run prof8 400 rocprofv3 --kernel-trace --stats -d "$O/prof8" -o k -f csv -- python3 bench.py --emulate-shard 8 --inflight 1 --steps 30 --warmup 3 --no-cpu --latency-batches 0 --prof-steps 5
