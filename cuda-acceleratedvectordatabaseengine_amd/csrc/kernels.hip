@@ -719,7 +719,6 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     __shared__ uint32_t base_w[kPlanMaxPairs];
     __shared__ uint32_t sh[33];
     __shared__ uint32_t sh_multi[(VDB_SEED_LEVELS + 2) * 17];
-    __shared__ uint32_t s_nvalid;
     __shared__ unsigned long long s_pairs;
     const uint32_t tid = threadIdx.x;
     const uint32_t BP = B * P;
@@ -733,28 +732,46 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
     }
 
     if (tid == 0) {
-        s_nvalid = 0;
         s_pairs = 0;
     }
     for (uint32_t i = tid; i < BP; i += blockDim.x) thr[i] = kThrInf;  // the scan's shared thresholds
-    for (uint32_t i = tid; i < NP; i += blockDim.x) {
-        uint32_t key = kInvalidKey;
+    // The valid pairs' keys (probed lists this shard stores) compacted to keys[0, nvalid), then
+    // only those sorted: a 1/8 shard's batch has ~1/8 of its pairs valid, so its sort is 8x
+    // shorter (round 6; at one GPU nothing changes). Each thread keys up to kPlanMaxPairs / 1024
+    // pairs i = tid + 1024 j, counted, scanned, written.
+    constexpr int kPer = kPlanMaxPairs / 1024;
+    uint32_t kv[kPer];
+    uint32_t nmine = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const uint32_t i = tid + 1024u * (uint32_t)j;
+        kv[j] = kInvalidKey;
         if (i < BP) {
             const uint32_t l = probes[i];
             const uint32_t ns = nseg_local[l];
             nseg_qp[i] = ns;
-            if (ns) key = (l << 13) | i;
+            if (ns) {
+                kv[j] = (l << 13) | i;
+                ++nmine;
+            }
         }
-        keys[i] = key;
     }
+    uint32_t nvalid;
+    uint32_t wpos = plan_excl_scan(nmine, sh, nvalid);
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+        if (kv[j] != kInvalidKey) keys[wpos++] = kv[j];
+    uint32_t NS = 1;  // (the sort's size: a power of two >= nvalid)
+    while (NS < nvalid) NS <<= 1;
+    for (uint32_t i = nvalid + tid; i < NS; i += blockDim.x) keys[i] = kInvalidKey;
     __syncthreads();
 
     // Bitonic sort in LDS, one compare-exchange per thread and step: pair p is (i, i + j)
     // with i = 2j (p / j) + p % j. A wave's 64 pairs then lie inside one 128-key block for
     // every j <= 64, so those steps need no workgroup barrier (a wave's LDS operations
     // complete in order); only the steps with j >= 128 (and the step before one) do.
-    const uint32_t npairs = NP >> 1;
-    for (uint32_t kk = 2; kk <= NP; kk <<= 1) {
+    const uint32_t npairs = NS >> 1;
+    for (uint32_t kk = 2; kk <= NS; kk <<= 1) {
         for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
             for (uint32_t p = tid; p < npairs; p += blockDim.x) {
                 const uint32_t i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), x = i + j;
@@ -775,10 +792,6 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
         }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < NP; i += blockDim.x)
-        if (keys[i] != kInvalidKey && (i + 1 == NP || keys[i + 1] == kInvalidKey)) s_nvalid = i + 1;
-    __syncthreads();
-    const uint32_t nvalid = s_nvalid;
 
     // Each thread owns a contiguous chunk of sorted positions.
     const uint32_t per = (nvalid + blockDim.x - 1) / blockDim.x;
