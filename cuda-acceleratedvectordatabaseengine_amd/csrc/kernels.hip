@@ -713,10 +713,15 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
                                                         uint2* __restrict__ l1_items,
                                                         unsigned long long* __restrict__ stats,
                                                         uint32_t* __restrict__ thr) {
-    __shared__ uint32_t keys[kPlanMaxPairs];
-    __shared__ uint32_t starts[kPlanMaxPairs + 1];
-    __shared__ uint32_t base_n[kPlanMaxPairs];
-    __shared__ uint32_t base_w[kPlanMaxPairs];
+    // keys, starts, base_n, base_w: dynamic LDS sized by the batch (NP = B x P rounded up to a
+    // power of two; 4 NP + 1 words, at most kPlanMaxPairs), not by kPlanMaxPairs: the 128 KB
+    // static arrays of round 5 fit no CU that held a collect workgroup, so with batches in flight
+    // a batch's plan waited for a CU to drain (round 6; the headline batch takes 32 KB)
+    extern __shared__ uint32_t plan_lds[];
+    uint32_t* const keys = plan_lds;
+    uint32_t* const starts = keys + NP;
+    uint32_t* const base_n = starts + NP + 1;
+    uint32_t* const base_w = base_n + NP;
     __shared__ uint32_t sh[33];
     __shared__ uint32_t sh_multi[(VDB_SEED_LEVELS + 2) * 17];
     __shared__ unsigned long long s_pairs;
@@ -2503,11 +2508,17 @@ void launch_coarse_mfma(int metric, const float* cent_rm, uint32_t nlist, uint32
 // chunk's candidate ids (plus slack).
 static constexpr size_t rerank_static_lds(int regs) { return (size_t)4 * regs * 64 * 8 + 512; }
 
+// (LDS budget of one re-rank workgroup: 64 KB, so it runs beside collect workgroups of the
+// batches in flight. Round 5 took the whole CU (51 candidate rows per chunk at 768 dims), and
+// with batches in flight its workgroups waited for CUs to drain: 96 us against 31 us alone
+// under a kernel trace. 19 rows per chunk at 768 dims.)
+constexpr size_t kRerankLds = 64 * 1024;
 uint32_t rerank_rows(uint32_t dp, int regs) {
     const size_t fixed = (size_t)dp * 4 + rerank_static_lds(regs);
     const size_t row = ((size_t)dp + 4) * 4;
+    const size_t budget = std::max(kRerankLds, fixed + 4 * row);  // (wide rows: at least 4 per chunk)
     if (fixed + row > kLdsBytes) return 0;
-    return (uint32_t)std::min<size_t>(64, (kLdsBytes - fixed) / row);
+    return (uint32_t)std::min<size_t>(64, (std::min(budget, kLdsBytes) - fixed) / row);
 }
 
 void launch_select_rerank(int metric, int regs, const float* approx, const float* delta, const float* cent_rm,
@@ -2570,7 +2581,15 @@ void launch_plan(const uint32_t* probes, const uint32_t* nseg_local, const uint3
     if (wide != 0 && wide != 16 && wide != 32) throw std::length_error("launch_plan: wide items of 16 or 32 queries only");
     uint32_t np = 1;
     while (np < B * P) np <<= 1;
-    ivf_plan_probes<<<1, 1024, 0, s>>>(probes, nseg_local, count_local, B, P, np, group, (uint32_t)wide, segs_item,
+    static const bool raised = [] {  // (up to 4 x kPlanMaxPairs + 1 words of dynamic LDS)
+        (void)hipFuncSetAttribute((const void*)ivf_plan_probes, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)((4 * (size_t)kPlanMaxPairs + 1) * 4));
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)raised;
+    const size_t lds = (4 * (size_t)np + 1) * 4;
+    ivf_plan_probes<<<1, 1024, lds, s>>>(probes, nseg_local, count_local, B, P, np, group, (uint32_t)wide, segs_item,
                                        wide == 16 ? mfma_min : 0u, items,
                                        items_w, counters, sorted_pair, part_base_sorted, part_base_qp, nseg_qp,
                                        l1base_qp, l1_items, stats, thr);

@@ -89,6 +89,13 @@ if has ranks3; then
     grep '^{' "$O/ranks3.log" > "$O/ranks3.json"
     cut -c 1-600 "$O/ranks3.json"
 fi
+if has ranks3q; then
+    # the same with 4 workspace slots (a _variants/slots4 build), 4 batches in flight and 8 hardware
+    # queues per process (4 in-flight streams + the communicator's each on a queue of their own)
+    run ranks3q 900 env VDB_IVF_LIB=$R/_variants/slots4/libvdb_ivf.so GPU_MAX_HW_QUEUES=8 python -u bench.py --cfg cfg3 --emulate-rank all --emulate-shard 8 --inflight 4 --no-cpu
+    grep '^{' "$O/ranks3q.log" > "$O/ranks3q.json"
+    cut -c 1-600 "$O/ranks3q.json"
+fi
 if has ranks4; then
     run ranks4 1100 python -u bench.py --cfg cfg4 --emulate-rank all --emulate-shard 8 --inflight 3 --no-cpu
     grep '^{' "$O/ranks4.log" > "$O/ranks4.json"
