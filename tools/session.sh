@@ -108,6 +108,13 @@ if has sweep; then
         grep '^{' "$O/sweep_$wl.log" | cut -c1-330
     done
 fi
+if has sweepq; then
+    # the sweep on the 4-slot build (_variants/slots4) with 8 hardware queues per process
+    for wl in ${SWEEP_WL:-s8 cfg3}; do
+        run sweepq_$wl 900 env VDB_IVF_LIB=$R/_variants/slots4/libvdb_ivf.so GPU_MAX_HW_QUEUES=8 python -u tools/knob_sweep.py $wl $SWEEP_SETS
+        grep '^{' "$O/sweepq_$wl.log" | cut -c1-330
+    done
+fi
 if has bench; then
     run bench 600 python -u bench.py ${BENCH_ARGS}
     grep '^{' "$O/bench.log" > "$O/bench.json"
