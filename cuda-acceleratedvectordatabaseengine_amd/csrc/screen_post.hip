@@ -25,7 +25,6 @@ namespace vdbk {
 // (value, element) — instead of sorting and merging every chunk.)
 __global__ __launch_bounds__(256) void ivf_screen_tfinal(ScanArgs a) {
     const int lane = lane_id();
-    if (blockIdx.x == 0 && threadIdx.x == 0) const_cast<uint32_t*>(a.counters)[14] = 0u;  // (kCtrFilterDone: the next kernel's)
     const uint32_t nvalid = a.counters[kCtrValid];
     const int k = (int)a.k;
     for (uint32_t s = blockIdx.x * 4 + wave_index(); s < nvalid; s += gridDim.x * 4) {
@@ -61,16 +60,10 @@ __global__ __launch_bounds__(256) void ivf_screen_tfinal(ScanArgs a) {
 // each wave takes kFilterU 64-entry chunks a grid pass apart at once, every load of one kind
 // in flight together: the entries, then their thresholds, then the run atomics.)
 constexpr int kFilterU = 4;
-__device__ void screen_offsets(const uint32_t* scnt, uint32_t* __restrict__ counters, uint32_t* __restrict__ soff,
-                               uint4* __restrict__ floor_out, uint32_t floor_seq, uint32_t k, uint32_t* wsum);
-constexpr int kCtrFilterDone = 14;  // (counters: the filter's finished workgroups; reset by ivf_screen_tfinal)
-__global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ cand, uint32_t* __restrict__ counters,
+__global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ cand, const uint32_t* __restrict__ counters,
                                                          uint32_t cap, const uint32_t* __restrict__ thr,
                                                          const uint32_t* __restrict__ thr4,
-                                                         const uint32_t* __restrict__ ovf, uint32_t* __restrict__ scnt,
-                                                         uint32_t* __restrict__ soff, uint4* __restrict__ floor_out,
-                                                         uint32_t floor_seq, uint32_t k) {
-    __shared__ uint32_t s_last, wsum[4];
+                                                         const uint32_t* __restrict__ ovf, uint32_t* __restrict__ scnt) {
     const uint32_t n = min(counters[kCtrCand], cap);
     const int lane = lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
@@ -121,30 +114,20 @@ __global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ can
             if (c[u].x != ~0u && i < n) cand[i].w = keep[u] ? bs + (uint32_t)__popcll(keeps[u] & runm[u] & below) : ~0u;
         }
     }
-    // the last workgroup to finish computes the survivors' offsets (every count is final)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        s_last = atomicAdd(counters + kCtrFilterDone, 1u) == gridDim.x - 1 ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    screen_offsets(scnt, counters, soff, floor_out, floor_seq, k, wsum);
 }
 
 // Exclusive scan of the survivor counts of the batch's valid sorted pairs (one workgroup):
-// soff[0 .. nvalid], the total into counters[kCtrSurv]. Run by the filter's last workgroup
-// (round 6: one launch fewer per batch; the counts are read with device-scope atomic loads
-// after the other workgroups' release).
-__device__ void screen_offsets(const uint32_t* scnt, uint32_t* __restrict__ counters, uint32_t* __restrict__ soff,
-                               uint4* __restrict__ floor_out, uint32_t floor_seq, uint32_t k, uint32_t* wsum) {
+// soff[0 .. nvalid], the total into counters[kCtrSurv].
+__global__ __launch_bounds__(1024) void ivf_screen_offsets(const uint32_t* __restrict__ scnt,
+                                                           uint32_t* __restrict__ counters,
+                                                           uint32_t* __restrict__ soff, uint4* __restrict__ floor_out,
+                                                           uint32_t floor_seq, uint32_t cap, uint32_t k) {
+    __shared__ uint32_t wsum[16];
     const uint32_t n = counters[kCtrValid];
     const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
     const uint32_t c0 = min(n, threadIdx.x * per), c1 = min(n, c0 + per);
-    auto cnt = [&](uint32_t i) { return __hip_atomic_load(scnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     uint32_t s = 0;
-    for (uint32_t i = c0; i < c1; ++i) s += cnt(i);
+    for (uint32_t i = c0; i < c1; ++i) s += scnt[i];
     // inclusive scan of s over the workgroup
     uint32_t x = s;
     const int lane = lane_id();
@@ -163,7 +146,7 @@ __device__ void screen_offsets(const uint32_t* scnt, uint32_t* __restrict__ coun
     uint32_t o = wbase + x - s;
     for (uint32_t i = c0; i < c1; ++i) {
         soff[i] = o;
-        o += cnt(i);
+        o += scnt[i];
     }
     if (threadIdx.x == 0) {
         soff[n] = total;
@@ -667,8 +650,8 @@ void launch_screen_select(const ScanArgs& a, uint32_t BP, uint32_t* scnt, uint32
     uint32_t* ctr = const_cast<uint32_t*>(a.counters);
     ivf_screen_tfinal<<<std::max<uint32_t>(1, std::min<uint32_t>(2048, (BP + 3) / 4)), 256, 0, s>>>(a);
     const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(1024, (a.cand_cap + 255) / 256));
-    ivf_screen_filter<<<g, 256, 0, s>>>(a.cand, ctr, a.cand_cap, a.thr, a.thr4, ovf, scnt, soff, a.floor_out,
-                                        a.floor_seq, a.k);
+    ivf_screen_filter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, a.thr, a.thr4, ovf, scnt);
+    ivf_screen_offsets<<<1, 1024, 0, s>>>(scnt, ctr, soff, a.floor_out, a.floor_seq, a.cand_cap, a.k);
     ivf_screen_scatter<<<g, 256, 0, s>>>(a.cand, a.counters, a.cand_cap, soff, surv, slb);
 }
 
