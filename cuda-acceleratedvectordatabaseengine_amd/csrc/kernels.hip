@@ -133,6 +133,7 @@ template <int M, int G>
 __global__ __launch_bounds__(256) void ivf_coarse_mfma(const float* __restrict__ cent_rm, uint32_t nlist,
                                                        uint32_t dp, const float* __restrict__ qpad, uint32_t B,
                                                        float* __restrict__ approx, float* __restrict__ delta) {
+    chain_prio();
     const int lane = lane_id();
     const uint32_t ct = blockIdx.x * 4 + wave_index();  // centroid tile
     const uint32_t qt = blockIdx.y;                      // query tile
@@ -336,6 +337,7 @@ __global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict
                                                          uint32_t dp, const float* __restrict__ qpad, uint32_t B,
                                                          uint32_t P, uint32_t ch, uint32_t* __restrict__ cand,
                                                          uint32_t* __restrict__ probes) {
+    chain_prio();
     extern __shared__ __attribute__((aligned(16))) float4 smem[];
     __shared__ float s_top_d[4 * R * 64];
     __shared__ uint32_t s_top_i[4 * R * 64];
@@ -713,6 +715,7 @@ __global__ __launch_bounds__(1024) void ivf_plan_probes(const uint32_t* __restri
                                                         uint2* __restrict__ l1_items,
                                                         unsigned long long* __restrict__ stats,
                                                         uint32_t* __restrict__ thr) {
+    chain_prio();
     // keys, starts, base_n, base_w: dynamic LDS sized by the batch (NP = B x P rounded up to a
     // power of two; 4 NP + 1 words, at most kPlanMaxPairs), not by kPlanMaxPairs: the 128 KB
     // static arrays of round 5 fit no CU that held a collect workgroup, so with batches in flight
@@ -2168,6 +2171,7 @@ __global__ __launch_bounds__(1024) void ivf_merge_fused(const uint32_t* __restri
                                                      uint64_t* __restrict__ slot_i, float* __restrict__ carry_nd,
                                                      uint64_t* __restrict__ carry_ni, float* __restrict__ out_d,
                                                      uint64_t* __restrict__ out_i) {
+    chain_prio();
     const uint32_t q = blockIdx.x;
     const uint32_t wv = wave_index();
     const int lane = lane_id();

@@ -46,6 +46,17 @@ __device__ __forceinline__ uint32_t wave_index() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
+// Issue priority of the per-batch chain's short kernels (coarse step, re-rank, plan, the
+// screen's selection, re-check and merge) over the collect kernel's waves sharing their SIMDs
+// (s_setprio; 0: the hardware default for every wave). Timing experiment (a separate build,
+// tools/build_chain_prio_variant.sh), never changes results.
+#ifndef VDB_CHAIN_PRIO
+#define VDB_CHAIN_PRIO 0
+#endif
+__device__ __forceinline__ void chain_prio() {
+    if constexpr (VDB_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(VDB_CHAIN_PRIO);
+}
+
 // Order-preserving float <-> uint encoding of the shared k-th thresholds (atomicMin).
 __device__ __forceinline__ uint32_t ord_enc(float f) {
     const uint32_t b = __float_as_uint(f);

@@ -24,6 +24,7 @@ namespace vdbk {
 // flight together, and only values below the running k-th are inserted — a wave top-k keyed
 // (value, element) — instead of sorting and merging every chunk.)
 __global__ __launch_bounds__(256) void ivf_screen_tfinal(ScanArgs a) {
+    chain_prio();
     const int lane = lane_id();
     const uint32_t nvalid = a.counters[kCtrValid];
     const int k = (int)a.k;
@@ -64,6 +65,7 @@ __global__ __launch_bounds__(256) void ivf_screen_filter(uint4* __restrict__ can
                                                          uint32_t cap, const uint32_t* __restrict__ thr,
                                                          const uint32_t* __restrict__ thr4,
                                                          const uint32_t* __restrict__ ovf, uint32_t* __restrict__ scnt) {
+    chain_prio();
     const uint32_t n = min(counters[kCtrCand], cap);
     const int lane = lane_id();
     const uint64_t below = (1ull << lane) - 1ull;
@@ -122,6 +124,7 @@ __global__ __launch_bounds__(1024) void ivf_screen_offsets(const uint32_t* __res
                                                            uint32_t* __restrict__ counters,
                                                            uint32_t* __restrict__ soff, uint4* __restrict__ floor_out,
                                                            uint32_t floor_seq, uint32_t cap, uint32_t k) {
+    chain_prio();
     __shared__ uint32_t wsum[16];
     const uint32_t n = counters[kCtrValid];
     const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
@@ -170,6 +173,7 @@ __global__ __launch_bounds__(256) void ivf_screen_scatter(const uint4* __restric
                                                           const uint32_t* __restrict__ counters, uint32_t cap,
                                                           const uint32_t* __restrict__ soff,
                                                           uint2* __restrict__ surv, float* __restrict__ slb) {
+    chain_prio();
     const uint32_t n = min(counters[kCtrCand], cap);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint4 c = cand[i];
@@ -485,6 +489,7 @@ __global__ __launch_bounds__(256) void ivf_screen_recheck2(ScanArgs a, const uin
                                                            const uint2* __restrict__ surv,
                                                            const float* __restrict__ slb,
                                                            const uint32_t* __restrict__ ovf, uint32_t smax) {
+    chain_prio();
     __shared__ uint32_t s_ring[4][kR2Ring];
     extern __shared__ __attribute__((aligned(16))) float4 s_qrow[];  // (KP > 0: per wave its pair's query row)
     const int lane = lane_id();

@@ -115,6 +115,18 @@ if has sweepq; then
         grep '^{' "$O/sweepq_$wl.log" | cut -c1-330
     done
 fi
+if has sweepv; then
+    # the sweep on an A/B library: _variants/$VARIANT (tools/build_*variant.sh)
+    for wl in ${SWEEP_WL:-s8 cfg3}; do
+        run sweepv_$wl 900 env VDB_IVF_LIB=$R/_variants/$VARIANT/libvdb_ivf.so python -u tools/knob_sweep.py $wl $SWEEP_SETS
+        grep '^{' "$O/sweepv_$wl.log" | cut -c1-330
+    done
+fi
+if has ranks3v; then
+    run ranks3v 900 env VDB_IVF_LIB=$R/_variants/$VARIANT/libvdb_ivf.so python -u bench.py --cfg cfg3 --emulate-rank all --emulate-shard 8 --inflight 3 --no-cpu
+    grep '^{' "$O/ranks3v.log" > "$O/ranks3v.json"
+    cut -c 1-600 "$O/ranks3v.json"
+fi
 if has bench; then
     run bench 600 python -u bench.py ${BENCH_ARGS}
     grep '^{' "$O/bench.log" > "$O/bench.json"
