@@ -2098,6 +2098,7 @@ __global__ __launch_bounds__(256) void ivf_merge_ranks(const float* __restrict__
                                                     uint64_t d_stride, uint64_t i_stride, uint32_t nranks,
                                                     uint32_t n, uint32_t k, float* __restrict__ out_d,
                                                     uint64_t* __restrict__ out_i) {
+    chain_prio();
     const uint32_t q = blockIdx.x * 4 + wave_index();
     if (q >= n) return;
     WaveTopK<R> tk;

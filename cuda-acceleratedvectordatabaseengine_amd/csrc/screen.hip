@@ -156,6 +156,7 @@ __global__ __launch_bounds__(256) void ivf_screen_pairs(const float* __restrict_
                                                         uint32_t* __restrict__ thr4, uint32_t* __restrict__ scnt,
                                                         uint32_t* __restrict__ ovf, uint32_t* __restrict__ counters,
                                                         uint32_t* __restrict__ ubcnt) {
+    chain_prio();
     const int lane = lane_id();
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < 4 * BP; e += gridDim.x * blockDim.x) thr4[e] = kThrInf;
     if (scnt)  // (the deferred scan: survivor counts, overflow marks and the candidate count)
@@ -297,6 +298,7 @@ __global__ __launch_bounds__(256) void ivf_screen_pairs_i8(const float* __restri
                                                            float4* __restrict__ pst, uint32_t* __restrict__ thr4,
                                                            uint32_t* __restrict__ scnt, uint32_t* __restrict__ ovf,
                                                            uint32_t* __restrict__ counters, uint32_t* __restrict__ ubcnt) {
+    chain_prio();
     const int lane = lane_id();
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < 4 * BP; e += gridDim.x * blockDim.x) thr4[e] = kThrInf;
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < BP; e += gridDim.x * blockDim.x) {

@@ -64,7 +64,7 @@ if has bench; then
     grep '^{' "$O/bench_mix.log" > "$O/bench_mix.json" && cut -c 1-400 "$O/bench_mix.json"
 fi
 if has trace; then
-    for inf in 1 2; do
+    for inf in 1 3; do
         run trace_inflight$inf 300 rocprofv3 --kernel-trace --stats -d "$O/trace_inflight$inf" -o k -f csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu --inflight $inf --latency-batches 0
         find "$O/trace_inflight$inf" -name '*kernel_stats.csv' -exec cp {} "$O/kernel_stats_inflight$inf.csv" \;
         head -6 "$O/kernel_stats_inflight$inf.csv"
