@@ -346,7 +346,10 @@ int vdb_ivf_set_coarse_mode(vdb_ivf* index, int mode);
  * then feeds two 16-query A operands, inline: two wave halves), "screen_defer" (1, default:
  * the screen collects candidates against upper-bound thresholds and re-checks afterwards only
  * the survivors of each (query, list) pair's final threshold; 0: re-checks inline as
- * candidates appear), "screen_cand_cap" (collected candidates per batch, default 4M; a pair
+ * candidates appear), "screen_recheck2" (1, default: the survivors are re-checked in two passes —
+ * each pair's k smallest lower bounds first, then only the others not above their k-th exact
+ * distance; in the file-home tier as two read phases; 0: every survivor in one pass; results are
+ * identical), "screen_cand_cap" (collected candidates per batch, default 4M; a pair
  * beyond it is recomputed over its whole list, a file-home tier batch re-run with more, up to
  * "tier_cand_max" (32M: beyond it that batch is served by the exact list-cache path)),
  * "tier_row_direct" (1, default: the screened tier reads survivors' rows with O_DIRECT),
