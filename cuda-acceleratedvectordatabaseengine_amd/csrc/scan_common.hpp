@@ -50,12 +50,13 @@ __device__ __forceinline__ uint32_t wave_index() {
 // rows, the screen's selection, re-check and merges) over the collect kernel's waves sharing
 // their SIMDs (s_setprio; the collect keeps the hardware default 0). With batches in flight a
 // batch's chain runs beside another batch's collect; raising it shortens the chain without
-// slowing the stream: the 1/8 shard at 3 in flight 0.262 -> 0.251 ms per step, every rank of
-// the 8-GPU emulation 0.276-0.287 -> 0.266-0.270 ms, the headline unchanged (round 6,
+// slowing the stream: the 1/8 shard at 3 in flight 0.262 -> 0.251 ms per step at priority 2,
+// every rank of the 8-GPU emulation 0.276-0.287 -> 0.266-0.270 ms, the headline unchanged;
+// priority 3 (the highest) 1 % faster again at both, same box (round 6,
 // tools/build_chain_prio_variant.sh A/B, profiles/r06_sweep_chain_prio.jsonl). Never changes
 // results.
 #ifndef VDB_CHAIN_PRIO
-#define VDB_CHAIN_PRIO 2
+#define VDB_CHAIN_PRIO 3
 #endif
 __device__ __forceinline__ void chain_prio() {
     if constexpr (VDB_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(VDB_CHAIN_PRIO);
