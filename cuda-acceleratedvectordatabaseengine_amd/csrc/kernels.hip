@@ -327,9 +327,8 @@ __device__ __forceinline__ float exact_row(const float* __restrict__ qrow, const
 // top-P: P lists have exact distance <= tau); exact distances of the candidates;
 // top-P by (dist, list) as the reference's partial_sort on std::pair
 // (cpp:324-333). Non-finite bounds make a list a candidate; NaN distances order
-// last. Candidate centroid rows are staged in LDS (coalesced loads, rows padded by
-// 4 floats so the lane-per-row reads are conflict-free) in chunks of `ch` rows;
-// one lane per candidate then runs the reference's sequential sum.
+// last. One lane per candidate runs the reference's sequential sum over its centroid
+// row, read from the table with the loads issued well ahead (`ch`: only checked).
 template <int R, int M>
 __global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict__ approx,
                                                          const float* __restrict__ delta,
@@ -345,8 +344,8 @@ __global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict
     __shared__ uint32_t s_n;
     const uint32_t q = blockIdx.x;
     if (q >= B) return;
-    // (LDS audit: s_top_* hold 4 R x 64 entries, s_ci one chunk of <= 64 rows; the host
-    // launch checks both, this early-out is the device's last line)
+    // (LDS audit: s_top_* hold 4 R x 64 entries; the host launch checks P and the query
+    // row's LDS (ch > 0), this early-out is the device's last line)
     if (P > 64u * R || ch > 64u || ch == 0u) return;
     const int lane = lane_id();
     const uint32_t w = wave_index();
@@ -447,66 +446,62 @@ __global__ __launch_bounds__(256) void ivf_select_rerank(const float* __restrict
     __threadfence_block();
     __syncthreads();
     const uint32_t n = s_n;
-    // pass 3: exact sequential distances of the candidates, ch rows at a time
-    const uint32_t rs = dp / 4 + 1;  // LDS row stride in float4 (one float4 of padding)
-    float4* q_l = smem;  // the query row (broadcast reads)
-    float4* rows = smem + dp / 4;
-    for (uint32_t e = threadIdx.x; e < dp / 4; e += 256) q_l[e] = ((const float4*)(qpad + (size_t)q * dp))[e];
+    // pass 3: exact sequential distances of the candidates. Candidate j: wave (j / 64) % 4,
+    // lane j % 64, its row read straight from the centroid table (L2 / MALL: the coarse step
+    // just read it) 16 to 32 float4 ahead of the dependent add chain; the query row in LDS.
+    // (Round 6: the rows were staged in LDS in chunks of 19 rows that only wave 0 summed, so a
+    // query's ~40 candidates took 2 - 3 chunk rounds of load, barrier and 768-step chain.)
+    const uint32_t n4 = dp / 4;  // (a multiple of 16)
+    float4* q_l = smem;          // the query row (broadcast reads)
+    for (uint32_t e = threadIdx.x; e < n4; e += 256) q_l[e] = ((const float4*)(qpad + (size_t)q * dp))[e];
+    __syncthreads();
     WaveTopK<R> tk;
     tk.init();
     float kd = __builtin_inff();
     uint64_t ki = kNoId;
-    __shared__ uint32_t s_ci[64];
-    for (uint32_t i0 = 0; i0 < n; i0 += ch) {
-        const uint32_t cnt = min(ch, n - i0);
-        __syncthreads();  // previous chunk consumed
-        if (threadIdx.x < cnt) s_ci[threadIdx.x] = cl[i0 + threadIdx.x];
-        __syncthreads();
-        // rows to LDS: independent loads, up to 32 per thread in flight (one round for
-        // the usual ~40 candidate rows at 768 dims)
-        const uint32_t n4 = dp / 4;
-        const uint32_t tot = cnt * n4;
-        for (uint32_t e0 = threadIdx.x; e0 < tot; e0 += 256 * 24) {
-            float4 v[24];
+    for (uint32_t j0 = w * 64; j0 < n; j0 += 256) {
+        const uint32_t j = j0 + lane;
+        const bool valid = j < n;
+        const uint32_t c = valid ? cl[j] : 0u;
+        const float4* x = (const float4*)(cent_rm + (size_t)c * dp);
+        const uint32_t last = n4 - 1;
+        float acc = 0.0f;
+        float4 xa[16], xb[16];
 #pragma unroll
-            for (int u = 0; u < 24; ++u) {  // unconditional (clamped) loads keep v in registers
-                const uint32_t e = min(e0 + u * 256, tot - 1);
-                const uint32_t r = e / n4, t = e - r * n4;
-                v[u] = ((const float4*)(cent_rm + (size_t)s_ci[r] * dp))[t];
-            }
+        for (int u = 0; u < 16; ++u) xa[u] = x[min((uint32_t)u, last)], xb[u] = x[min(16u + u, last)];
+        uint32_t t0 = 0;
+        for (; t0 + 32 <= n4; t0 += 32) {
 #pragma unroll
-            for (int u = 0; u < 24; ++u) {
-                const uint32_t e = e0 + u * 256;
-                const uint32_t r = e / n4, t = e - r * n4;
-                if (e < tot) rows[r * rs + t] = v[u];
-            }
+            for (int u = 0; u < 16; ++u) acc = acc4<M>(acc, q_l[t0 + u], xa[u]);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) xa[u] = x[min(t0 + 32 + u, last)];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) acc = acc4<M>(acc, q_l[t0 + 16 + u], xb[u]);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) xb[u] = x[min(t0 + 48 + u, last)];
+        }
+        if (t0 < n4) {  // (n4 = 32 m + 16: the last 16 are in xa)
+#pragma unroll
+            for (int u = 0; u < 16; ++u) acc = acc4<M>(acc, q_l[t0 + u], xa[u]);
+        }
+        const float d = valid ? nan_last(dist_finish<M>(acc)) : __builtin_inff();
+        offer_lanes<R>(tk, valid && d <= kd, d, (uint64_t)c, (int)P, kd, ki);
+    }
+    if (n > 64) {  // (more than one wave's candidates: the top-P of the four waves' lists)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            s_top_d[(w * R + r) * 64 + lane] = tk.d[r];
+            s_top_i[(w * R + r) * 64 + lane] = (uint32_t)tk.id[r];
         }
         __syncthreads();
         if (w == 0) {
-            // lane j: sequential sum over candidate row j; LDS reads double-buffered 8
-            // float4 ahead of the dependent add chain (n4 is a multiple of 16)
-            for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {
-                const uint32_t j = j0 + lane;
-                const bool valid = j < cnt;
-                const float4* x = rows + (valid ? j : 0) * rs;
-                float acc = 0.0f;
-                float4 xa[8], qa[8], xb[8], qb[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) xa[u] = x[u], qa[u] = q_l[u];
-                for (uint32_t t0 = 0; t0 < n4; t0 += 16) {
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) xb[u] = x[t0 + 8 + u], qb[u] = q_l[t0 + 8 + u];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) acc = acc4<M>(acc, qa[u], xa[u]);
-                    const uint32_t tn = t0 + 16 < n4 ? t0 + 16 : 0;
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) xa[u] = x[tn + u], qa[u] = q_l[tn + u];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) acc = acc4<M>(acc, qb[u], xb[u]);
-                }
-                const float d = valid ? nan_last(dist_finish<M>(acc)) : __builtin_inff();
-                const uint32_t c = valid ? s_ci[j] : 0u;
-                offer_lanes<R>(tk, valid && d <= kd, d, (uint64_t)c, (int)P, kd, ki);
+            tk.init();
+            kd = __builtin_inff();
+            ki = kNoId;
+            for (uint32_t e0 = 0; e0 < 4 * R * 64; e0 += 64) {
+                const float dd = s_top_d[e0 + lane];
+                const uint32_t id = s_top_i[e0 + lane];
+                offer_lanes<R>(tk, id != 0xFFFFFFFFu && dd <= kd, dd, (uint64_t)id, (int)P, kd, ki);
             }
         }
     }
@@ -2513,10 +2508,9 @@ void launch_coarse_mfma(int metric, const float* cent_rm, uint32_t nlist, uint32
 // chunk's candidate ids (plus slack).
 static constexpr size_t rerank_static_lds(int regs) { return (size_t)4 * regs * 64 * 8 + 512; }
 
-// (LDS budget of one re-rank workgroup: 64 KB, so it runs beside collect workgroups of the
-// batches in flight. Round 5 took the whole CU (51 candidate rows per chunk at 768 dims), and
-// with batches in flight its workgroups waited for CUs to drain: 96 us against 31 us alone
-// under a kernel trace. 19 rows per chunk at 768 dims.)
+// (rerank_rows: how many candidate rows of dp dims would fit a 64 KB workgroup beside the query
+// row; > 0 is the exact coarse path's feasibility test. Since round 6 the kernel stages only
+// the query row: the candidates' rows are read from the table by their lanes.)
 constexpr size_t kRerankLds = 64 * 1024;
 uint32_t rerank_rows(uint32_t dp, int regs) {
     const size_t fixed = (size_t)dp * 4 + rerank_static_lds(regs);
@@ -2530,11 +2524,11 @@ void launch_select_rerank(int metric, int regs, const float* approx, const float
                           uint32_t nlist, uint32_t dp, const float* qpad, uint32_t B, uint32_t P, uint32_t* cand,
                           uint32_t* probes, hipStream_t s) {
     const uint32_t ch = rerank_rows(dp, regs);
-    // (the kernel's fixed LDS: s_top_* of 4 regs x 64 entries hold the partial top-P lists,
-    // s_ci one chunk of <= 64 candidate rows)
+    // (the kernel's fixed LDS: s_top_* of 4 regs x 64 entries hold the partial top-P lists;
+    // ch > 0: the query row fits beside them)
     if (P > 64u * (uint32_t)regs || ch == 0 || ch > 64)
         throw std::length_error("launch_select_rerank: nprobe above the top-P registers or no LDS chunk");
-    const size_t lds = ((size_t)dp / 4 + (size_t)ch * (dp / 4 + 1)) * sizeof(float4);
+    const size_t lds = (size_t)dp / 4 * sizeof(float4);  // (the query row)
 #define VDB_SR(R)                                                                                             \
     do {                                                                                                      \
         static const bool raised_ = [] {                                                                      \

@@ -53,8 +53,8 @@ if has mfma; then
     # the bench build's assignment (10M x 4096 bounds on the 2x2 kernel) and the search
     # batches' coarse step; rocprofv3 -L first, for the record of the counters present
     rocprofv3 -L > "$O/counters_available.txt" 2>&1 || true
-    run pmc_mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "ivf_coarse|ivf_assign|ivf_select_rerank" -d "$O/pmc_mfma" -o m -f csv -- python3 bench.py $SHORT
-    run trace_mfma 300 rocprofv3 --kernel-trace --stats --kernel-include-regex "ivf_coarse|ivf_assign|ivf_select_rerank" -d "$O/trace_mfma" -o t -f csv -- python3 bench.py $SHORT
+    run pmc_mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "ivf_coarse|ivf_assign|ivf_select_rerank|ivf_screen_collect|ivf_screen_recheck2" -d "$O/pmc_mfma" -o m -f csv -- python3 bench.py $SHORT
+    run trace_mfma 300 rocprofv3 --kernel-trace --stats --kernel-include-regex "ivf_coarse|ivf_assign|ivf_select_rerank|ivf_screen_collect|ivf_screen_recheck2" -d "$O/trace_mfma" -o t -f csv -- python3 bench.py $SHORT
     python3 tools/mfma_report.py "$O/pmc_mfma" "$O/trace_mfma" "$O/mfma.json" | tail -30
 fi
 if has bench; then
